@@ -1,0 +1,108 @@
+/* mlvae.h -- C ABI of libmlvae.so, the MI355X (gfx950) kernels of the ML-VAE training step.
+ *
+ * Conventions
+ *   - Every entry point returns int: 0 ok, 1 bad argument, 2 HIP launch/runtime error;
+ *     the text of the last error of the calling thread is mlvae_last_error().
+ *   - The caller owns every device buffer and workspace; the library never allocates.
+ *   - Calls are stream-ordered on `stream` (a hipStream_t passed as void*) and reentrant.
+ *   - Tensors are fp32, row-major [B*T, C] with row n = b*T + t (the reference's batch_first
+ *     [B,T,C] layout, ref:src/modules/decoder.py:14), leading dimension in elements.
+ *   - prec: 0 = fp32 (exact f32 MFMA, the parity mode), 1 = bf16 operands / fp32 accumulate.
+ *
+ * The reference is pure Python (SURVEY.md section 0): it has no FFI.  Each entry below names
+ * the reference code whose work it replaces; the Python drop-in layer (ml-vae_amd/modules,
+ * ml-vae_amd/models) binds these through ctypes (INTEGRATION.md).
+ */
+#ifndef MLVAE_H
+#define MLVAE_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* mlvae_last_error(void);
+int mlvae_abi_version(void);
+int mlvae_device_check(char* arch_out, int len);
+
+/* C = epi(alpha*op(A).op(B) + bias1 + bias2 + beta*C).  trans_a: A stored [K][M];
+ * trans_b: B stored [N][K].  epi 0 none, 1 LeakyReLU(0.01), 2 multiply by lrelu'(aux).
+ * kshift/kshift_T (trans_b = 0): B row k reads row k+kshift when 0 <= k%T + kshift < T, else 0.
+ * Replaces nn.Linear forward/backward (ref:src/modules/fc_block.py:10-16,
+ * ref:src/modules/vanilla_vae.py:18-24) and the LSTM input projections and weight
+ * gradients (ref:src/modules/decoder.py:14-15,22). */
+size_t mlvae_gemm_workspace_size(int M, int N, int K);
+int mlvae_gemm(int prec, int trans_a, int trans_b, int M, int N, int K, float alpha,
+               const float* A, int lda, const float* B, int ldb, float beta, float* C, int ldc,
+               const float* bias1, const float* bias2, int epi, const float* aux, int ldaux,
+               int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream);
+
+/* Bidirectional LSTM layer recurrence, both directions in one persistent launch.
+ * gates [B*T, 8H]: in = x W_ih^T + b_ih + b_hh (cols [0,4H) forward, [4H,8H) reverse);
+ *                  out = activated gates i,f,g,o (saved for the backward).
+ * cells [B*T, 2H], y [B*T, 2H] (forward half | reverse half) = nn.LSTM output.
+ * Replaces the recurrent part of nn.LSTM (ref:src/modules/decoder.py:22). */
+int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes, size_t* flag_bytes);
+int mlvae_lstm_fwd(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                   float* gates, float* cells, float* y, void* xbuf, size_t xbytes,
+                   unsigned* flags, size_t flag_bytes, int* err, void* stream);
+/* BPTT: gates in = activated gates from mlvae_lstm_fwd, out = pre-activation gate grads dG.
+ * dy = gradient wrt the layer output y.  Weight/input grads follow as GEMMs on dG. */
+int mlvae_lstm_bwd(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                   float* gates, const float* cells, const float* dy, void* xbuf, size_t xbytes,
+                   unsigned* flags, size_t flag_bytes, int* err, void* stream);
+
+/* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
+ * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */
+int mlvae_elbo_partials_count(int B, int T, int C);
+int mlvae_reparam_kl_fwd(int B, int T, int Z, const float* ml, int ldml, const float* eps,
+                         const float* lens, float* z, float* kl_out, float* partials,
+                         void* stream);
+int mlvae_reparam_kl_bwd(int B, int T, int Z, const float* ml, int ldml, const float* eps,
+                         const float* lens, const int* count, const float* dz, const float* dkl,
+                         float kl_scale, float* dml, int lddml, void* stream);
+/* Reconstruction term (ref:src/modules/decoder.py:37-53; loss_type 0 likelihood, 1 mse)
+ * with masked partial sums and, when dmux != NULL, its gradient. */
+int mlvae_recon(int B, int T, int F, int loss_type, const float* mux, int ldmu, const float* lvx,
+                int ldlv, const float* x, int ldx, const float* lens, const int* count,
+                float* rec_out, float* partials, const float* drec, float rec_scale, float* dmux,
+                float* dlvx, void* stream);
+/* out[3] = {kld_loss, recon_loss, w_kl*kld + w_rec*recon}
+ * (ref:src/utils/data_utils.py:67-104, ref:src/models/md_model.py:189-213). */
+int mlvae_elbo_finalize(const float* kl_partials, int nk, const float* rec_partials, int nr,
+                        const float* lens, const int* count, int B, int T, int Z, int F,
+                        float w_kl, float w_rec, float* out, void* stream);
+/* count (optional, device int) overrides the valid-frame count derived from lens: a
+ * data-parallel shard passes the all-reduced global count so that its loss/gradients are
+ * its exact share of the global masked mean (SURVEY.md 8(e)(i)). */
+int mlvae_count_frames(const float* lens, int B, int T, int* out, void* stream);
+/* eps ~ N(0,1) from Philox-4x32-10(seed, offset + i): shard-invariant reparameterisation noise
+ * (replaces torch.randn_like at ref:src/modules/vanilla_vae.py:39). */
+int mlvae_randn(size_t n, unsigned long long seed, unsigned long long offset, float* out,
+                void* stream);
+/* apply_lens_to_loss(loss[B,T,C], lens, reduction 0 mean / 1 batchmean / 2 batch);
+ * out holds 2*B floats (results first). */
+int mlvae_masked_mean(int B, int T, int C, const float* loss, const float* lens, int reduction,
+                      float* out, void* stream);
+
+/* check_gradients + Adam (ref:src/models/md_model.py:82-86, model.yaml:45-47). */
+int mlvae_sumsq_partials_count(size_t n);
+int mlvae_grad_sumsq(const float* grads, size_t n, double* partials, void* stream);
+int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
+                    size_t n, const double* partials, int nparts, const float* loss, int* step,
+                    int* nonfinite, float lr, float beta1, float beta2, float eps,
+                    float max_norm, float* norm_out, void* stream);
+
+/* bias gradients: out[c] = beta*out[c] + sum_n in[n][c]; out2 (optional) gets a copy. */
+size_t mlvae_colsum_workspace_size(int N, int C);
+int mlvae_colsum(int N, int C, const float* in, int ld, float* out, float* out2, float beta,
+                 float* ws, size_t ws_bytes, void* stream);
+
+/* y = x * mask; mask = given (already scaled) or Philox(seed, i) keep-prob 1-p scaled 1/(1-p).
+ * Inter-layer dropout of nn.LSTM in train mode (ref:src/modules/decoder.py:14). */
+int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
+                  unsigned long long seed, float p, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,88 @@
+// Shared device helpers for the ML-VAE CDNA4 (gfx950) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// Compute precision of a matrix product (operands; accumulation is always fp32).
+enum MlvaePrec { PREC_F32 = 0, PREC_BF16 = 1 };
+
+#define MLVAE_NEG_SLOPE 0.01f  // nn.LeakyReLU default (ref:src/modules/fc_block.py:11)
+
+// Record an error string for mlvae_last_error() (capi.cpp).
+extern "C" void mlvae_set_error(const char* fmt, ...);
+
+#define MLVAE_CHECK_LAUNCH()                                               \
+  do {                                                                     \
+    hipError_t e__ = hipGetLastError();                                    \
+    if (e__ != hipSuccess) {                                               \
+      mlvae_set_error("%s: launch failed: %s", __func__, hipGetErrorString(e__)); \
+      return 2;                                                            \
+    }                                                                      \
+  } while (0)
+
+__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : MLVAE_NEG_SLOPE * x; }
+__device__ __forceinline__ float lrelu_d(float post) { return post > 0.f ? 1.f : MLVAE_NEG_SLOPE; }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// bf16 round-to-nearest-even, NaN-preserving (plain cast -> v_cvt_pk_bf16_f32).
+__device__ __forceinline__ short f2bf(float x) {
+  __hip_bfloat16 h = __float2bfloat16(x);
+  return *reinterpret_cast<short*>(&h);
+}
+__device__ __forceinline__ float bf2f(short s) {
+  unsigned u = ((unsigned)(unsigned short)s) << 16;
+  return __uint_as_float(u);
+}
+
+// ---- write-through (sc1) hand-off primitives (MI355X_MICROARCH.md "Valid forms" row 1)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ld_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /*sc1*/);
+}
+__device__ __forceinline__ void st_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16 /*sc1*/);
+}
+__device__ __forceinline__ void st_sc1_b32(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16 /*sc1*/);
+}
+__device__ __forceinline__ void st_sc1_b16(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned short v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, 16 /*sc1*/);
+}
+__device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Number of valid frames of one utterance under SpeechBrain length_to_mask semantics
+// (ref:src/utils/data_utils.py:86-87): t valid iff (float)t < fp32(rel_len * T).
+__device__ __forceinline__ int valid_frames(float rel_len, int T) {
+  float lim = rel_len * (float)T;
+  if (!(lim > 0.f)) return 0;
+  float c = ceilf(lim);
+  return c >= (float)T ? T : (int)c;
+}
+
+// Wave-level sum (64 lanes) with a fixed butterfly order (deterministic).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

@@ -1,0 +1,203 @@
+// Optimizer step and small reductions of the VAE train step.
+//
+//   check_gradients (SpeechBrain Brain, un-vendored; called ref:src/models/md_model.py:82):
+//     non-finite loss -> skip the update; else clip_grad_norm_(params, max_grad_norm=5.0)
+//   torch.optim.Adam(lr) (ref:src/models/test_vanilla_vae/model.yaml:45-47), defaults
+//     betas (0.9, 0.999), eps 1e-8, no weight decay, bias-corrected; step counter on device.
+//   bias gradients: deterministic column sums over the B*T rows.
+//   inter-layer LSTM dropout (p = 0.15 in train mode, ref:src/models/test_vanilla_vae/model.yaml:25):
+//     counter-based Philox-4x32-10 keyed by (seed, element index): the backward re-derives the
+//     forward mask instead of storing it.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- grad norm
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, size_t n,
+                                                    double* __restrict__ partials) {
+  __shared__ double sm[4];
+  double acc = 0.0;
+  const size_t n4 = n / 4;
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 v = g4[i];
+    acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += 256) acc += (double)g[i] * g[i];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+
+struct AdamArgs {
+  float* p; float* m; float* v; const float* g;
+  size_t n;
+  const double* partials; int nparts;
+  const float* loss;          // skip the step when non-finite (may be null)
+  const int* step;            // completed steps so far (device); this update uses step+1
+  float lr, b1, b2, eps, max_norm;
+  float* norm_out;            // total grad norm (may be null)
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  __shared__ float coef_s;
+  __shared__ int skip_s;
+  __shared__ float step_size_s, bc2s_s;
+  if (threadIdx.x == 0) {
+    double ss = 0.0;
+    for (int i = 0; i < a.nparts; ++i) ss += a.partials[i];
+    const float total = (float)sqrt(ss);
+    float coef = a.max_norm / (total + 1e-6f);
+    coef = coef < 1.f ? coef : 1.f;  // clamp(max=1): a NaN norm propagates like torch
+    if (!(total == total)) coef = total;
+    coef_s = coef;
+    skip_s = (a.loss && !isfinite(*a.loss)) ? 1 : 0;
+    const int t = *a.step + 1;
+    const double bc1 = 1.0 - pow((double)a.b1, (double)t);
+    const double bc2 = 1.0 - pow((double)a.b2, (double)t);
+    step_size_s = (float)((double)a.lr / bc1);
+    bc2s_s = (float)sqrt(bc2);
+    if (blockIdx.x == 0 && a.norm_out) *a.norm_out = total;
+  }
+  __syncthreads();
+  if (skip_s) return;
+  const float coef = coef_s, step_size = step_size_s, bc2s = bc2s_s;
+  const float w1 = 1.f - a.b1, w2 = 1.f - a.b2;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (size_t)gridDim.x * 256) {
+    const float g = a.g[i] * coef;
+    float m = a.m[i], v = a.v[i];
+    m = m + w1 * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
+    v = v * a.b2 + w2 * g * g;             // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
+    const float denom = sqrtf(v) / bc2s + a.eps;
+    a.p[i] = a.p[i] + (-step_size) * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
+    a.m[i] = m;
+    a.v[i] = v;
+  }
+}
+
+__global__ void step_counter_kernel(const float* loss, int* step, int* nonfinite) {
+  if (threadIdx.x || blockIdx.x) return;
+  if (loss && !isfinite(*loss)) { if (nonfinite) *nonfinite += 1; }
+  else *step += 1;
+}
+
+// ---------------------------------------------------------------- column sums
+// partial[r][c] = sum over rows [r*rows_per, ...) of in[row][c]; then out[c] = sum_r partial[r][c]
+__global__ __launch_bounds__(256) void colsum_partial(int N, int C, const float* __restrict__ in,
+                                                      int ld, int rows_per, float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += in[(size_t)r * ld + c];
+  part[(size_t)blockIdx.y * C + c] = s;
+}
+__global__ __launch_bounds__(256) void colsum_final(int C, int R, const float* __restrict__ part,
+                                                    float* __restrict__ out, float* __restrict__ out2,
+                                                    float beta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += part[(size_t)r * C + c];
+  out[c] = beta != 0.f ? beta * out[c] + s : s;
+  if (out2) out2[c] = out[c];
+}
+
+// ---------------------------------------------------------------- dropout
+__device__ __forceinline__ void philox_round(unsigned& c0, unsigned& c1, unsigned& c2, unsigned& c3,
+                                             unsigned k0, unsigned k1) {
+  const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+  const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+  const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0;
+  const unsigned hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
+  const unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+  c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+}
+__device__ __forceinline__ unsigned philox_u32(unsigned long long seed, unsigned long long idx) {
+  unsigned c0 = (unsigned)idx, c1 = (unsigned)(idx >> 32), c2 = 0x5851F42Du, c3 = 0x14057B7Eu;
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c0, c1, c2, c3, k0, k1);
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+__global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __restrict__ x,
+                                                      float* __restrict__ y,
+                                                      const float* __restrict__ mask,
+                                                      unsigned long long seed, float p) {
+  const float keep = 1.f - p, scale = 1.f / keep;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    float m;
+    if (mask) m = mask[i];
+    else m = ((philox_u32(seed, i) >> 8) * (1.f / 16777216.f)) < keep ? scale : 0.f;
+    y[i] = x[i] * m;
+  }
+}
+
+int grid_for(size_t total, int cap) {
+  size_t g = (total + 255) / 256;
+  if (g > (size_t)cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" int mlvae_sumsq_partials_count(size_t n) { return grid_for(n / 4 + 1, 1024); }
+
+extern "C" int mlvae_grad_sumsq(const float* g, size_t n, double* partials, void* stream) {
+  if (((uintptr_t)g & 15) != 0) { mlvae_set_error("grad_sumsq: grads must be 16-byte aligned"); return 1; }
+  sumsq_kernel<<<mlvae_sumsq_partials_count(n), 256, 0, (hipStream_t)stream>>>(g, n, partials);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
+                               size_t n, const double* partials, int nparts, const float* loss,
+                               int* step, int* nonfinite, float lr, float beta1, float beta2,
+                               float eps, float max_norm, float* norm_out, void* stream) {
+  AdamArgs a;
+  a.p = params; a.m = exp_avg; a.v = exp_avg_sq; a.g = grads; a.n = n; a.partials = partials;
+  a.nparts = nparts; a.loss = loss; a.step = step; a.lr = lr; a.b1 = beta1; a.b2 = beta2;
+  a.eps = eps; a.max_norm = max_norm; a.norm_out = norm_out;
+  hipStream_t s = (hipStream_t)stream;
+  adam_kernel<<<grid_for(n, 2048), 256, 0, s>>>(a);
+  step_counter_kernel<<<1, 64, 0, s>>>(loss, step, nonfinite);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" size_t mlvae_colsum_workspace_size(int N, int C) {
+  int R = (N + 255) / 256;
+  if (R > 64) R = 64;
+  return (size_t)R * C * sizeof(float);
+}
+
+// out[c] (+= if beta) = sum_n in[n][c]; out2 (optional) receives a copy (b_ih / b_hh pairs)
+extern "C" int mlvae_colsum(int N, int C, const float* in, int ld, float* out, float* out2,
+                            float beta, float* ws, size_t ws_bytes, void* stream) {
+  if (C == 0) return 0;
+  int R = (N + 255) / 256;
+  if (R > 64) R = 64;
+  if (R < 1) R = 1;
+  if (!ws || ws_bytes < (size_t)R * C * sizeof(float)) { mlvae_set_error("colsum: workspace too small"); return 1; }
+  const int rows_per = (N + R - 1) / R;
+  hipStream_t s = (hipStream_t)stream;
+  colsum_partial<<<dim3((C + 255) / 256, R), 256, 0, s>>>(N, C, in, ld, rows_per, ws);
+  colsum_final<<<(C + 255) / 256, 256, 0, s>>>(C, R, ws, out, out2, beta);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
+                             unsigned long long seed, float p, void* stream) {
+  if (p < 0.f || p >= 1.f) { mlvae_set_error("dropout: p=%f out of range", p); return 1; }
+  dropout_kernel<<<grid_for(n, 2048), 256, 0, (hipStream_t)stream>>>(n, x, y, mask, seed, p);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}

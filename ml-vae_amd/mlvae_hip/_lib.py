@@ -1,0 +1,91 @@
+"""ctypes binding of libmlvae.so (C ABI declared in include/mlvae.h).
+
+The library is the product: there is no CPU fallback.  ``lib()`` raises if the
+in-tree ``libmlvae.so`` is missing or cannot be loaded, and ``check()`` turns a
+non-zero status into a RuntimeError carrying ``mlvae_last_error()``.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmlvae.so")
+
+P = C.c_void_p
+I = C.c_int
+F = C.c_float
+SZ = C.c_size_t
+U64 = C.c_ulonglong
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS = {
+    "mlvae_last_error": [],
+    "mlvae_abi_version": [],
+    "mlvae_device_check": [C.c_char_p, I],
+    "mlvae_gemm_workspace_size": [I, I, I],
+    "mlvae_gemm": [I, I, I, I, I, I, F, P, I, P, I, F, P, I, P, P, I, P, I, I, I, P, SZ, P],
+    "mlvae_lstm_workspace_size": [I, I, I, C.POINTER(SZ), C.POINTER(SZ)],
+    "mlvae_lstm_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, SZ, P, P],
+    "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, SZ, P, P],
+    "mlvae_elbo_partials_count": [I, I, I],
+    "mlvae_reparam_kl_fwd": [I, I, I, P, I, P, P, P, P, P, P],
+    "mlvae_reparam_kl_bwd": [I, I, I, P, I, P, P, P, P, P, F, P, I, P],
+    "mlvae_recon": [I, I, I, I, P, I, P, I, P, I, P, P, P, P, P, F, P, P, P],
+    "mlvae_elbo_finalize": [P, I, P, I, P, P, I, I, I, I, F, F, P, P],
+    "mlvae_masked_mean": [I, I, I, P, P, I, P, P],
+    "mlvae_count_frames": [P, I, I, P, P],
+    "mlvae_randn": [SZ, U64, U64, P, P],
+    "mlvae_sumsq_partials_count": [SZ],
+    "mlvae_grad_sumsq": [P, SZ, P, P],
+    "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P],
+    "mlvae_colsum_workspace_size": [I, I],
+    "mlvae_colsum": [I, I, P, I, P, P, F, P, SZ, P],
+    "mlvae_dropout": [SZ, P, P, P, U64, F, P],
+}
+_RESTYPE = {
+    "mlvae_last_error": C.c_char_p,
+    "mlvae_gemm_workspace_size": SZ,
+    "mlvae_colsum_workspace_size": SZ,
+}
+
+_lib = None
+
+
+class MlvaeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmlvae.so (once).  Raises if it is absent: the HIP path has no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MlvaeError(
+                f"{LIB_PATH} is missing: build it with `python -m mlvae_hip.build` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        h = C.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, I)
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def last_error():
+    return lib().mlvae_last_error().decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc != 0:
+        raise MlvaeError(f"{what or 'mlvae'} failed (status {rc}): {last_error()}")
+    return rc
+
+
+def device_check():
+    buf = C.create_string_buffer(64)
+    rc = lib().mlvae_device_check(buf, 64)
+    return rc, buf.value.decode()

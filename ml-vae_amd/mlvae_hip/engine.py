@@ -1,0 +1,473 @@
+"""The VAE training step on MI355X: flat parameter/gradient/Adam buffers plus a fixed
+sequence of libmlvae.so launches (no autograd, no torch compute kernels on the path).
+
+One ``train_step`` = the reference's ``MDModel.fit_batch`` for the test_vanilla_vae
+recipe (ref:src/models/md_model.py:54-88 with
+ref:src/models/test_vanilla_vae/model.py:19-55):
+
+  encoder   FC(F->E) LReLU FC(E->E) LReLU -> [mu | log_var] FC(E->2Z)       (3 GEMMs)
+  ELBO-1    z = eps*exp(lv/2) + mu ; KL ; masked partial sums                (1 kernel)
+  decoder   L x [input-projection GEMM + persistent BiLSTM recurrence]      (2L launches)
+            (+ inter-layer dropout in train mode)
+  heads     FC(2H->2C) fused for both heads, then FC(C->C), FC(C->F) per head
+  ELBO-2    reconstruction NLL/MSE + masked sums + d/d(mu_x, lv_x)           (1 kernel)
+  backward  dgrad/wgrad GEMMs, BPTT recurrence, column sums for biases
+  step      grad sum-of-squares -> clip(5.0) + Adam + device step counter  (no host sync)
+
+Every tensor is row-major [B*T, C]; the flat parameter buffer keeps pairs that a fused
+launch reads as one matrix adjacent (mean/log_var heads, both LSTM directions).
+"""
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+PREC = {"fp32": 0, "bf16": 1}
+LOSS = {"likelihood": 0, "mse": 1}
+EPI_NONE, EPI_LRELU, EPI_DLRELU = 0, 1, 2
+
+
+@dataclass
+class VAEConfig:
+    """Dimensions/hyper-parameters of the recipe (ref:src/models/test_vanilla_vae/model.yaml:17-54)."""
+    F: int = 80             # input_size (feature dim)
+    E: int = 64             # enc_fc_size
+    Z: int = 32             # latent_size
+    H: int = 512            # dec_rnn_hidden_size
+    L: int = 2              # dec_rnn_num_layers
+    C: int = 64             # dec_fc_size
+    dropout: float = 0.15   # dec_rnn_dropout
+    loss_type: str = "likelihood"
+    kld_weight: float = 1e-3
+    recon_weight: float = 1.0
+    lr: float = 1e-3
+    betas: tuple = (0.9, 0.999)
+    adam_eps: float = 1e-8
+    max_grad_norm: float = 5.0
+    prec: str = "fp32"      # "fp32" (exact parity mode) or "bf16" (bf16 MFMA operands)
+
+    def check(self):
+        for k in ("F", "E", "Z", "H", "C"):
+            v = getattr(self, k)
+            if v <= 0 or v % 4:
+                raise ValueError(f"{k}={v}: every width must be a positive multiple of 4")
+        if self.loss_type not in LOSS:
+            raise ValueError(f"Invalid loss type: {self.loss_type}")
+        if self.prec not in PREC:
+            raise ValueError(f"prec must be one of {list(PREC)}")
+        return self
+
+
+def reference_shapes(cfg):
+    """Reference parameter names/shapes in Brain.modules.parameters() order
+    (encoder: ref:src/modules/vanilla_vae.py:13-19; decoder: ref:src/modules/decoder.py:14-17)."""
+    F, E, Z, H, L, C = cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C
+    s = OrderedDict()
+    s["encoder.fc.0.blocks.0.weight"] = (E, F)
+    s["encoder.fc.0.blocks.0.bias"] = (E,)
+    s["encoder.fc.0.blocks.2.weight"] = (E, E)
+    s["encoder.fc.0.blocks.2.bias"] = (E,)
+    s["encoder.mean_fc.weight"] = (Z, E)
+    s["encoder.mean_fc.bias"] = (Z,)
+    s["encoder.log_var_fc.weight"] = (Z, E)
+    s["encoder.log_var_fc.bias"] = (Z,)
+    for l in range(L):
+        din = Z if l == 0 else 2 * H
+        for sfx in ("", "_reverse"):
+            s[f"decoder.rnn.weight_ih_l{l}{sfx}"] = (4 * H, din)
+            s[f"decoder.rnn.weight_hh_l{l}{sfx}"] = (4 * H, H)
+            s[f"decoder.rnn.bias_ih_l{l}{sfx}"] = (4 * H,)
+            s[f"decoder.rnn.bias_hh_l{l}{sfx}"] = (4 * H,)
+    for head in ("mean_fc", "log_var_fc"):
+        dims = [2 * H, C, C, F]
+        for i in range(3):
+            s[f"decoder.{head}.blocks.{2 * i}.weight"] = (dims[i + 1], dims[i])
+            s[f"decoder.{head}.blocks.{2 * i}.bias"] = (dims[i + 1],)
+    return s
+
+
+def _engine_order(cfg):
+    """Flat-buffer order: groups listed together are laid out back to back (no padding),
+    so one launch can read them as a single stacked matrix/vector."""
+    g = [["encoder.fc.0.blocks.0.weight"], ["encoder.fc.0.blocks.0.bias"],
+         ["encoder.fc.0.blocks.2.weight"], ["encoder.fc.0.blocks.2.bias"],
+         ["encoder.mean_fc.weight", "encoder.log_var_fc.weight"],
+         ["encoder.mean_fc.bias", "encoder.log_var_fc.bias"]]
+    for l in range(cfg.L):
+        for kind in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+            g.append([f"decoder.rnn.{kind}_l{l}", f"decoder.rnn.{kind}_l{l}_reverse"])
+    g.append(["decoder.mean_fc.blocks.0.weight", "decoder.log_var_fc.blocks.0.weight"])
+    g.append(["decoder.mean_fc.blocks.0.bias", "decoder.log_var_fc.blocks.0.bias"])
+    for head in ("mean_fc", "log_var_fc"):
+        for i in (2, 4):
+            g.append([f"decoder.{head}.blocks.{i}.weight"])
+            g.append([f"decoder.{head}.blocks.{i}.bias"])
+    return g
+
+
+class ParamLayout:
+    def __init__(self, cfg):
+        self.shapes = reference_shapes(cfg)
+        self.offsets = {}
+        off = 0
+        for group in _engine_order(cfg):
+            off = (off + 3) // 4 * 4  # 16-byte aligned group start
+            for name in group:
+                self.offsets[name] = off
+                n = 1
+                for d in self.shapes[name]:
+                    n *= d
+                off += n
+        self.total = (off + 3) // 4 * 4
+        assert set(self.offsets) == set(self.shapes)
+
+    def numel(self, name):
+        n = 1
+        for d in self.shapes[name]:
+            n *= d
+        return n
+
+
+class _Work:
+    """Activation/gradient workspaces for one (B, T): allocated once, reused every step."""
+
+    def __init__(self, cfg, B, T, device):
+        N = B * T
+        F, E, Z, H, L, C = cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C
+        f = dict(device=device, dtype=torch.float32)
+        self.B, self.T, self.N = B, T, N
+        self.E1 = torch.empty(N, E, **f)
+        self.E2 = torch.empty(N, E, **f)
+        self.ML = torch.empty(N, 2 * Z, **f)
+        self.Zs = torch.empty(N, Z, **f)
+        self.eps = torch.empty(N, Z, **f)
+        self.G = [torch.empty(N, 8 * H, **f) for _ in range(L)]
+        self.Cs = [torch.empty(N, 2 * H, **f) for _ in range(L)]
+        self.Y = [torch.empty(N, 2 * H, **f) for _ in range(L)]
+        self.Yd = [torch.empty(N, 2 * H, **f) if cfg.dropout > 0 else None for _ in range(L - 1)]
+        self.P1 = torch.empty(N, 2 * C, **f)
+        self.P2m = torch.empty(N, C, **f)
+        self.P2v = torch.empty(N, C, **f)
+        self.MUX = torch.empty(N, F, **f)
+        self.LVX = torch.empty(N, F, **f)
+        # backward
+        self.dMUX = torch.empty(N, F, **f)
+        self.dLVX = torch.empty(N, F, **f)
+        self.dP2m = torch.empty(N, C, **f)
+        self.dP2v = torch.empty(N, C, **f)
+        self.dP1 = torch.empty(N, 2 * C, **f)
+        self.dY = [torch.empty(N, 2 * H, **f) for _ in range(L)]
+        self.dZs = torch.empty(N, Z, **f)
+        self.dML = torch.empty(N, 2 * Z, **f)
+        self.dE2 = torch.empty(N, E, **f)
+        self.dE1 = torch.empty(N, E, **f)
+        l = lib()
+        self.nk = l.mlvae_elbo_partials_count(B, T, Z)
+        self.nr = l.mlvae_elbo_partials_count(B, T, F)
+        self.pk = torch.empty(self.nk, **f)
+        self.pr = torch.empty(self.nr, **f)
+        self.loss = torch.zeros(3, **f)   # [kld_loss, recon_loss, total]
+        self.count = torch.zeros(1, device=device, dtype=torch.int32)
+        # GEMM split-K workspace: the largest any call of the step asks for
+        shapes = [(N, E, F), (N, E, E), (N, 2 * Z, E), (N, 2 * C, 2 * H), (N, C, C), (N, F, C),
+                  (F, C, N), (C, C, N), (2 * C, 2 * H, N), (2 * Z, E, N), (E, E, N), (E, F, N),
+                  (N, 2 * H, 8 * H), (N, Z, 8 * H), (4 * H, H, N)]
+        for li in range(L):
+            din = Z if li == 0 else 2 * H
+            shapes += [(N, 8 * H, din), (8 * H, din, N)]
+        ws = max(l.mlvae_gemm_workspace_size(m, n, k) for m, n, k in shapes)
+        cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
+        self.gws = torch.empty(max(ws, cs, 16) // 4 + 1, **f)
+        self.gws_bytes = self.gws.numel() * 4
+        xb, fb = _lib.SZ(), _lib.SZ()
+        check(l.mlvae_lstm_workspace_size(B, H, PREC[cfg.prec], _lib.C.byref(xb), _lib.C.byref(fb)),
+              "lstm_workspace_size")
+        self.xbuf = torch.empty(max(xb.value, 16), device=device, dtype=torch.uint8)
+        self.flags = torch.zeros(max(fb.value, 16) // 4, device=device, dtype=torch.int32)
+        self.err = torch.zeros(1, device=device, dtype=torch.int32)
+
+
+def _p(t, off=0):
+    return t.data_ptr() + 4 * off
+
+
+class VAEEngine:
+    """MI355X-native train/eval step of the VanillaVAE + BiLSTM-decoder recipe."""
+
+    def __init__(self, cfg, device="cuda", params=None, seed=123456):
+        self.cfg = cfg.check()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("VAEEngine runs on the HIP device only (no CPU fallback)")
+        lib()
+        self.layout = ParamLayout(cfg)
+        n = self.layout.total
+        f = dict(device=self.device, dtype=torch.float32)
+        self.flat = torch.zeros(n, **f)
+        self.grad = torch.zeros(n, **f)
+        self.exp_avg = torch.zeros(n, **f)
+        self.exp_avg_sq = torch.zeros(n, **f)
+        self.step_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self.nonfinite_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self.grad_norm = torch.zeros(1, **f)
+        self.nparts = lib().mlvae_sumsq_partials_count(n)
+        self.sq_parts = torch.zeros(self.nparts, device=self.device, dtype=torch.float64)
+        self.seed = seed
+        self.rng_step = 0
+        self._work = {}
+        self.process_group = None   # set by mlvae_hip.dist for data parallel
+        self.world = 1
+        self.global_offset = 0      # first global utterance index of this shard
+        if params is not None:
+            self.load_reference_params(params)
+
+    # ------------------------------------------------------------------ parameters
+    def view(self, name, buf=None):
+        buf = self.flat if buf is None else buf
+        o = self.layout.offsets[name]
+        return buf[o:o + self.layout.numel(name)].view(self.layout.shapes[name])
+
+    def named_parameters(self):
+        return OrderedDict((k, self.view(k)) for k in self.layout.shapes)
+
+    def named_grads(self):
+        return OrderedDict((k, self.view(k, self.grad)) for k in self.layout.shapes)
+
+    def load_reference_params(self, params):
+        with torch.no_grad():
+            for k, v in params.items():
+                self.view(k).copy_(torch.as_tensor(v, dtype=torch.float32))
+
+    def _ptr(self, name, buf=None):
+        return _p(self.flat if buf is None else buf, self.layout.offsets[name])
+
+    def work(self, B, T):
+        key = (B, T)
+        if key not in self._work:
+            self._work = {key: _Work(self.cfg, B, T, self.device)}  # keep one shape resident
+        return self._work[key]
+
+    # ------------------------------------------------------------------ launch helpers
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _gemm(self, w, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, bias1=None, bias2=None, epi=0,
+              aux=None, ldaux=0, kshift_T=0, kshift=0, beta=0.0):
+        check(lib().mlvae_gemm(PREC[self.cfg.prec], ta, tb, M, N, K, 1.0, A, lda, B, ldb, beta, C,
+                               ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift,
+                               _p(w.gws), w.gws_bytes, self._stream()), "mlvae_gemm")
+
+    def _colsum(self, w, N, Cn, src, ld, out, out2=None):
+        check(lib().mlvae_colsum(N, Cn, src, ld, out, out2, 0.0, _p(w.gws), w.gws_bytes,
+                                 self._stream()), "mlvae_colsum")
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x, lens, eps=None, train=False, dropout_masks=None, need_grad_inputs=False):
+        """compute_forward + compute_objectives.  x [B,T,F] fp32 (normalised features),
+        lens [B] relative lengths.  Returns the workspace (outputs stay on device)."""
+        cfg = self.cfg
+        B, T, Fdim = x.shape
+        if Fdim != cfg.F:
+            raise ValueError(f"feature dim {Fdim} != input_size {cfg.F}")
+        x = x.contiguous()
+        lens = lens.to(device=self.device, dtype=torch.float32).contiguous()
+        w = self.work(B, T)
+        w.x, w.lens = x, lens
+        N, E, Z, H, C, Fd = w.N, cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
+        l, s = lib(), self._stream()
+        X = _p(x)
+        count = None
+        if self.world > 1:
+            count = self._global_count(w)
+        # ---- reparameterisation noise
+        if eps is None:
+            check(l.mlvae_randn(N * Z, self.seed, self._eps_offset(T) + self.rng_step * (1 << 40),
+                                _p(w.eps), s), "mlvae_randn")
+            eps_t = w.eps
+        else:
+            eps_t = eps.to(self.device, torch.float32).contiguous().view(N, Z)
+        w.eps_used = eps_t
+        # ---- encoder (ref:src/modules/vanilla_vae.py:21-28)
+        self._gemm(w, 0, 1, N, E, Fd, X, Fd, self._ptr("encoder.fc.0.blocks.0.weight"), Fd,
+                   _p(w.E1), E, bias1=self._ptr("encoder.fc.0.blocks.0.bias"), epi=EPI_LRELU)
+        self._gemm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
+                   _p(w.E2), E, bias1=self._ptr("encoder.fc.0.blocks.2.bias"), epi=EPI_LRELU)
+        self._gemm(w, 0, 1, N, 2 * Z, E, _p(w.E2), E, self._ptr("encoder.mean_fc.weight"), E,
+                   _p(w.ML), 2 * Z, bias1=self._ptr("encoder.mean_fc.bias"))
+        check(l.mlvae_reparam_kl_fwd(B, T, Z, _p(w.ML), 2 * Z, _p(eps_t), _p(lens), _p(w.Zs),
+                                     None, _p(w.pk), s), "reparam_kl_fwd")
+        # ---- decoder BiLSTM (ref:src/modules/decoder.py:22)
+        xin, din = w.Zs, Z
+        w.layer_in = []
+        for li in range(cfg.L):
+            w.layer_in.append((xin, din))
+            self._gemm(w, 0, 1, N, 8 * H, din, _p(xin), din,
+                       self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
+                       bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                       bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+            check(l.mlvae_lstm_fwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                   self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                   _p(w.Cs[li]), _p(w.Y[li]), _p(w.xbuf), w.xbuf.numel(),
+                                   _p(w.flags), w.flags.numel() * 4, _p(w.err), s), "lstm_fwd")
+            xin, din = w.Y[li], 2 * H
+            if li < cfg.L - 1 and train and cfg.dropout > 0:
+                xin = w.Yd[li]
+                self._dropout(w, li, w.Y[li], xin, dropout_masks)
+        w.rnn_out = w.Y[cfg.L - 1]
+        # ---- heads (ref:src/modules/decoder.py:24-25, FCBlock ref:src/modules/fc_block.py:9-16)
+        R = _p(w.rnn_out)
+        self._gemm(w, 0, 1, N, 2 * C, 2 * H, R, 2 * H, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                   2 * H, _p(w.P1), 2 * C, bias1=self._ptr("decoder.mean_fc.blocks.0.bias"),
+                   epi=EPI_LRELU)
+        for hd, P2, out in (("mean_fc", w.P2m, w.MUX), ("log_var_fc", w.P2v, w.LVX)):
+            off = 0 if hd == "mean_fc" else C
+            self._gemm(w, 0, 1, N, C, C, _p(w.P1, off), 2 * C,
+                       self._ptr(f"decoder.{hd}.blocks.2.weight"), C, _p(P2), C,
+                       bias1=self._ptr(f"decoder.{hd}.blocks.2.bias"), epi=EPI_LRELU)
+            self._gemm(w, 0, 1, N, Fd, C, _p(P2), C, self._ptr(f"decoder.{hd}.blocks.4.weight"), C,
+                       _p(out), Fd, bias1=self._ptr(f"decoder.{hd}.blocks.4.bias"))
+        # ---- ELBO part 2 (+ its gradient when training)
+        lt = LOSS[cfg.loss_type]
+        w_kl, w_rec = self.loss_weights()
+        dmux = _p(w.dMUX) if train else None
+        dlvx = _p(w.dLVX) if (train and lt == 0) else None
+        check(l.mlvae_recon(B, T, Fd, lt, _p(w.MUX), Fd, _p(w.LVX), Fd, X, Fd, _p(lens), count,
+                            None, _p(w.pr), None, w_rec, dmux, dlvx, s), "recon")
+        check(l.mlvae_elbo_finalize(_p(w.pk), w.nk, _p(w.pr), w.nr, _p(lens), count, B, T, Z, Fd,
+                                    w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
+        return w
+
+    def loss_weights(self):
+        return float(self.cfg.kld_weight), float(self.cfg.recon_weight)
+
+    def _eps_offset(self, T):
+        return self.global_offset * T * self.cfg.Z
+
+    def _dropout(self, w, li, src, dst, masks):
+        mask_ptr = None
+        if masks is not None:
+            m = masks[li].to(self.device, torch.float32).contiguous()
+            w.__dict__.setdefault("_masks", {})[li] = m
+            mask_ptr = _p(m)
+        seed = (self.seed * 1000003 + self.rng_step * 131 + li) & ((1 << 63) - 1)
+        check(lib().mlvae_dropout(src.numel(), _p(src), _p(dst), mask_ptr, seed, self.cfg.dropout,
+                                  self._stream()), "dropout")
+        w.__dict__.setdefault("_drop_seed", {})[li] = (seed, mask_ptr)
+
+    def _global_count(self, w):
+        import torch.distributed as dist
+        check(lib().mlvae_count_frames(_p(w.lens), w.B, w.T, _p(w.count), self._stream()), "count")
+        dist.all_reduce(w.count, group=self.process_group)
+        return _p(w.count)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, w):
+        cfg = self.cfg
+        B, T, N = w.B, w.T, w.N
+        E, Z, H, C, Fd = cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
+        l, s = lib(), self._stream()
+        g = self.grad
+        gp = lambda name: self._ptr(name, g)
+        mse = cfg.loss_type == "mse"
+        count = _p(w.count) if self.world > 1 else None
+        # ---- heads tail
+        heads = [("mean_fc", w.P2m, w.dMUX, w.dP2m, 0)]
+        if not mse:
+            heads.append(("log_var_fc", w.P2v, w.dLVX, w.dP2v, C))
+        for hd, P2, dOut, dP2, off in heads:
+            W3, W2 = self._ptr(f"decoder.{hd}.blocks.4.weight"), self._ptr(f"decoder.{hd}.blocks.2.weight")
+            self._gemm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C, epi=EPI_DLRELU,
+                       aux=_p(P2), ldaux=C)
+            self._gemm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
+            self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
+            self._gemm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C, epi=EPI_DLRELU,
+                       aux=_p(w.P1, off), ldaux=2 * C)
+            self._gemm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
+                       gp(f"decoder.{hd}.blocks.2.weight"), C)
+            self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
+        K1 = C if mse else 2 * C  # mse: the log_var head gets no gradient (torch: grad None)
+        R = _p(w.rnn_out)
+        self._gemm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                   2 * H, _p(w.dY[cfg.L - 1]), 2 * H)
+        self._gemm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
+                   gp("decoder.mean_fc.blocks.0.weight"), 2 * H)
+        self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
+        # ---- BiLSTM layers, top to bottom
+        for li in range(cfg.L - 1, -1, -1):
+            xin, din = w.layer_in[li]
+            Gl = w.G[li]
+            check(l.mlvae_lstm_bwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                   self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
+                                   _p(w.Cs[li]), _p(w.dY[li]), _p(w.xbuf), w.xbuf.numel(),
+                                   _p(w.flags), w.flags.numel() * 4, _p(w.err), s), "lstm_bwd")
+            dx = w.dZs if li == 0 else w.dY[li - 1]
+            self._gemm(w, 0, 0, N, din, 8 * H, _p(Gl), 8 * H,
+                       self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din)
+            self._gemm(w, 1, 0, 8 * H, din, N, _p(Gl), 8 * H, _p(xin), din,
+                       gp(f"decoder.rnn.weight_ih_l{li}"), din)
+            self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl), 8 * H, _p(w.Y[li]), 2 * H,
+                       gp(f"decoder.rnn.weight_hh_l{li}"), H, kshift_T=T, kshift=-1)
+            self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
+                       gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, kshift_T=T, kshift=1)
+            self._colsum(w, N, 8 * H, _p(Gl), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
+                         gp(f"decoder.rnn.bias_hh_l{li}"))
+            if li > 0 and xin is not w.Y[li - 1]:  # dropout between layers li-1 and li
+                seed, mask_ptr = w._drop_seed[li - 1]
+                check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
+                      "dropout_bwd")
+        # ---- encoder
+        w_kl, _ = self.loss_weights()
+        check(l.mlvae_reparam_kl_bwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(w.lens), count,
+                                     _p(w.dZs), None, w_kl, _p(w.dML), 2 * Z, s), "reparam_kl_bwd")
+        self._gemm(w, 0, 0, N, E, 2 * Z, _p(w.dML), 2 * Z, self._ptr("encoder.mean_fc.weight"), E,
+                   _p(w.dE2), E, epi=EPI_DLRELU, aux=_p(w.E2), ldaux=E)
+        self._gemm(w, 1, 0, 2 * Z, E, N, _p(w.dML), 2 * Z, _p(w.E2), E, gp("encoder.mean_fc.weight"), E)
+        self._colsum(w, N, 2 * Z, _p(w.dML), 2 * Z, gp("encoder.mean_fc.bias"))
+        self._gemm(w, 0, 0, N, E, E, _p(w.dE2), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
+                   _p(w.dE1), E, epi=EPI_DLRELU, aux=_p(w.E1), ldaux=E)
+        self._gemm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp("encoder.fc.0.blocks.2.weight"), E)
+        self._colsum(w, N, E, _p(w.dE2), E, gp("encoder.fc.0.blocks.2.bias"))
+        self._gemm(w, 1, 0, E, Fd, N, _p(w.dE1), E, _p(w.x), Fd, gp("encoder.fc.0.blocks.0.weight"), Fd)
+        self._colsum(w, N, E, _p(w.dE1), E, gp("encoder.fc.0.blocks.0.bias"))
+
+    # ------------------------------------------------------------------ optimizer
+    def optimizer_step(self, w):
+        """check_gradients (non-finite loss -> skip; clip_grad_norm_ 5.0) + Adam, on device."""
+        cfg, l, s = self.cfg, lib(), self._stream()
+        if self.world > 1:
+            self._allreduce_grads(w)
+        check(l.mlvae_grad_sumsq(_p(self.grad), self.layout.total, self.sq_parts.data_ptr(), s), "sumsq")
+        b1, b2 = cfg.betas
+        check(l.mlvae_adam_step(_p(self.flat), _p(self.exp_avg), _p(self.exp_avg_sq), _p(self.grad),
+                                self.layout.total, self.sq_parts.data_ptr(), self.nparts,
+                                _p(w.loss, 2), self.step_ctr.data_ptr(), self.nonfinite_ctr.data_ptr(),
+                                cfg.lr, b1, b2, cfg.adam_eps, cfg.max_grad_norm,
+                                _p(self.grad_norm), s), "adam")
+
+    def _allreduce_grads(self, w):
+        import torch.distributed as dist
+        dist.all_reduce(self.grad, group=self.process_group)
+        dist.all_reduce(w.loss, group=self.process_group)
+
+    def train_step(self, x, lens, eps=None, dropout_masks=None):
+        """One fit_batch: forward, backward, clip + Adam.  Returns the device tensor
+        [kld_loss, recon_loss, loss] (no host synchronisation)."""
+        w = self.forward(x, lens, eps=eps, train=True, dropout_masks=dropout_masks)
+        self.backward(w)
+        self.optimizer_step(w)
+        self.rng_step += 1
+        return w.loss
+
+    def eval_step(self, x, lens, eps=None):
+        w = self.forward(x, lens, eps=eps, train=False)
+        self.rng_step += 1
+        return w.loss
+
+    def check_errors(self):
+        """Host-synchronising check of the persistent kernels' spin-timeout word."""
+        for w in self._work.values():
+            if int(w.err.item()) != 0:
+                raise RuntimeError("LSTM recurrence hand-off timed out (err word set)")
