@@ -40,16 +40,20 @@ int mlvae_gemm(int prec, int trans_a, int trans_b, int M, int N, int K, float al
  * gates [B*T, 8H]: in = x W_ih^T + b_ih + b_hh (cols [0,4H) forward, [4H,8H) reverse);
  *                  out = activated gates i,f,g,o (saved for the backward).
  * cells [B*T, 2H], y [B*T, 2H] (forward half | reverse half) = nn.LSTM output.
+ * xbuf: exchange workspace (size from mlvae_lstm_workspace_size); err: device int set to 1
+ * if a hand-off wait timed out (the launch then completes with undefined outputs).
  * Replaces the recurrent part of nn.LSTM (ref:src/modules/decoder.py:22). */
-int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes, size_t* flag_bytes);
+int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes);
 int mlvae_lstm_fwd(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
-                   float* gates, float* cells, float* y, void* xbuf, size_t xbytes,
-                   unsigned* flags, size_t flag_bytes, int* err, void* stream);
+                   float* gates, float* cells, float* y, void* xbuf, size_t xbytes, int* err,
+                   void* stream);
 /* BPTT: gates in = activated gates from mlvae_lstm_fwd, out = pre-activation gate grads dG.
  * dy = gradient wrt the layer output y.  Weight/input grads follow as GEMMs on dG. */
 int mlvae_lstm_bwd(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                    float* gates, const float* cells, const float* dy, void* xbuf, size_t xbytes,
-                   unsigned* flags, size_t flag_bytes, int* err, void* stream);
+                   int* err, void* stream);
+/* Diagnostics: record per-step phase stamps of workgroup 0 into buf (NULL disables). */
+int mlvae_lstm_set_debug(void* buf);
 
 /* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
  * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */
@@ -90,7 +94,7 @@ int mlvae_grad_sumsq(const float* grads, size_t n, double* partials, void* strea
 int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
                     size_t n, const double* partials, int nparts, const float* loss, int* step,
                     int* nonfinite, float lr, float beta1, float beta2, float eps,
-                    float max_norm, float* norm_out, void* stream);
+                    float max_norm, float* norm_out, float* hyp_scratch, void* stream);
 
 /* bias gradients: out[c] = beta*out[c] + sum_n in[n][c]; out2 (optional) gets a copy. */
 size_t mlvae_colsum_workspace_size(int N, int C);

@@ -25,7 +25,7 @@ extern "C" int mlvae_device_check(char* name_out, int len) {
     return 1;
   }
   int dev = 0;
-  hipGetDevice(&dev);
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) { mlvae_set_error("hipGetDeviceProperties failed"); return 1; }
   if (name_out && len > 0) snprintf(name_out, len, "%s", p.gcnArchName);

@@ -32,6 +32,15 @@ extern "C" void mlvae_set_error(const char* fmt, ...);
 __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : MLVAE_NEG_SLOPE * x; }
 __device__ __forceinline__ float lrelu_d(float post) { return post > 0.f ? 1.f : MLVAE_NEG_SLOPE; }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// sigmoid / tanh on the hardware exp + rcp (|err| ~1e-7): the cell update is on the
+// recurrence's serial path
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+__device__ __forceinline__ float tanh_fast(float x) {
+  // tanh(x) = 1 - 2/(1+e^{2x}); saturates cleanly for |x| large
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
+}
 
 // bf16 round-to-nearest-even, NaN-preserving (plain cast -> v_cvt_pk_bf16_f32).
 __device__ __forceinline__ short f2bf(float x) {

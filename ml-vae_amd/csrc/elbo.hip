@@ -133,16 +133,32 @@ __global__ __launch_bounds__(256) void recon_kernel(
 }
 
 // out = [kld_loss, recon_loss, total] = [sum_kl/(cnt*Z), sum_rec/(cnt*F), w_kl*kld + w_rec*rec]
-__global__ void finalize_kernel(const float* pk, int nk, const float* pr, int nr,
-                                const float* lens, const int* count, int B, int T, int Z, int F,
-                                float w_kl, float w_rec, float* out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double sk = 0.0, sr = 0.0;
-  for (int i = 0; i < nk; ++i) sk += pk[i];
-  for (int i = 0; i < nr; ++i) sr += pr[i];
-  const int c = count ? *count : total_frames(lens, B, T);
-  const float kld = (float)(sk / ((double)c * Z));
-  const float rec = (float)(sr / ((double)c * F));
+// one 256-thread block; partials folded in a fixed order (strided fp64 + tree): deterministic
+__global__ __launch_bounds__(256) void finalize_kernel(const float* pk, int nk, const float* pr,
+                                                       int nr, const float* lens, const int* count,
+                                                       int B, int T, int Z, int F, float w_kl,
+                                                       float w_rec, float* out) {
+  __shared__ double sk[256], sr[256];
+  __shared__ int sc[256];
+  double a = 0.0, b = 0.0;
+  int cnt = 0;
+  for (int i = threadIdx.x; i < nk; i += 256) a += pk[i];
+  for (int i = threadIdx.x; i < nr; i += 256) b += pr[i];
+  for (int i = threadIdx.x; i < B; i += 256) cnt += valid_frames(lens[i], T);
+  sk[threadIdx.x] = a; sr[threadIdx.x] = b; sc[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      sk[threadIdx.x] += sk[threadIdx.x + o];
+      sr[threadIdx.x] += sr[threadIdx.x + o];
+      sc[threadIdx.x] += sc[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const int c = count ? *count : sc[0];
+  const float kld = (float)(sk[0] / ((double)c * Z));
+  const float rec = (float)(sr[0] / ((double)c * F));
   out[0] = kld;
   out[1] = rec;
   float tot = 0.f;  // ref:src/models/md_model.py:191-202 accumulates in dict order (kld, recon)
@@ -267,7 +283,7 @@ extern "C" int mlvae_recon(int B, int T, int F, int loss_type, const float* mux,
 extern "C" int mlvae_elbo_finalize(const float* pk, int nk, const float* pr, int nr,
                                    const float* lens, const int* count, int B, int T, int Z, int F,
                                    float w_kl, float w_rec, float* out, void* stream) {
-  finalize_kernel<<<1, 64, 0, (hipStream_t)stream>>>(pk, nk, pr, nr, lens, count, B, T, Z, F,
+  finalize_kernel<<<1, 256, 0, (hipStream_t)stream>>>(pk, nk, pr, nr, lens, count, B, T, Z, F,
                                                      w_kl, w_rec, out);
   MLVAE_CHECK_LAUNCH();
   return 0;

@@ -95,13 +95,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   constexpr int LDK = BK + Lds<PREC>::PAD;
   constexpr int WM = BM / 2, WN = BN / 2, MB = WM / 32, NB = WN / 32;
   constexpr int NCA = BM * BK / 4 / 256, NCB = BN * BK / 4 / 256;  // chunks per thread
-  static_assert(NCA >= 1 && NCB >= 1, "tile too small");
+  static_assert(NCA >= 1 && NCB >= 1 && NCA <= 4 && NCB <= 4, "tile size");
   __shared__ __attribute__((aligned(16))) LT As[BM * LDK];
   __shared__ __attribute__((aligned(16))) LT Bs[BN * LDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  // XCD-aware tile order (bijective): blocks b, b+8, ... share an XCD's L2, so each XCD gets a
+  // contiguous run of tiles; consecutive tiles share the A row-panel (all n for one m).
+  const int TM = (g.M + BM - 1) / BM, TN = (g.N + BN - 1) / BN, ntiles = TM * TN;
+  int tile;
+  {
+    const int b = blockIdx.x, xcd = b % 8, local = b / 8, q = ntiles / 8, r = ntiles % 8;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  }
+  const int m0 = (tile / TN) * BM, n0 = (tile % TN) * BN;
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const bool shiftK = (!TB) && g.kshift != 0;
@@ -114,57 +122,59 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
-  f32x4 ra[NCA], rb[NCB];
-  auto gload = [&](int k0) {
+  // K-contiguous operand: float4 chunks along k (NC per thread).
+  // M-contiguous operand (stored [K][rows]): 4k x 4r blocks, transposed in registers so the
+  // LDS image stays [row][k] and every LDS store is one 8/16-byte write.
+  constexpr int NBA = (BK / 4) * (BM / 4), NBB = (BK / 4) * (BN / 4);  // 4x4 blocks per tile
+  f32x4 ra[4], rb[4];
+  auto load_kc = [&](f32x4* r, const float* base, int ld, int r0, int R, int k0, bool vec, int NC) {
 #pragma unroll
-    for (int c = 0; c < NCA; ++c) {
+    for (int c = 0; c < NC; ++c) {
       int idx = tid + 256 * c;
-      if (!TA) {
-        int r = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
-        ra[c] = load_chunk<true>(g.A, g.lda, m0 + r, k0 + kc, g.M, kend, g.vecA, 0, 0, false);
-      } else {
-        int kr = idx / (BM / 4), mc = (idx % (BM / 4)) * 4;
-        ra[c] = load_chunk<false>(g.A, g.lda, m0 + mc, k0 + kr, g.M, kend, g.vecA, 0, 0, false);
-      }
+      int rr = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
+      r[c] = load_chunk<true>(base, ld, r0 + rr, k0 + kc, R, kend, vec, 0, 0, false);
     }
+  };
+  auto load_mc = [&](f32x4* r, const float* base, int ld, int r0, int R, int k0, bool vec, int NB_,
+                     bool shift) {
+    if (tid < NB_) {
+      // lanes sweep k first: 8 lanes cover one 4-row x 32-k strip -> conflict-free LDS stores,
+      // and every load instruction still reads whole 128-byte row segments
+      const int kq = (tid % (BK / 4)) * 4;
+      const int rq = (tid / (BK / 4)) * 4;
 #pragma unroll
-    for (int c = 0; c < NCB; ++c) {
+      for (int e = 0; e < 4; ++e)
+        r[e] = load_chunk<false>(base, ld, r0 + rq, k0 + kq + e, R, kend, vec, g.kshiftT, g.kshift, shift);
+    }
+  };
+  auto store_kc = [&](LT* L, const f32x4* r, int NC) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
       int idx = tid + 256 * c;
-      if (TB) {
-        int r = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
-        rb[c] = load_chunk<true>(g.B, g.ldb, n0 + r, k0 + kc, g.N, kend, g.vecB, 0, 0, false);
-      } else {
-        int kr = idx / (BN / 4), nc = (idx % (BN / 4)) * 4;
-        rb[c] = load_chunk<false>(g.B, g.ldb, n0 + nc, k0 + kr, g.N, kend, g.vecB, g.kshiftT,
-                                  g.kshift, shiftK);
+      int rr = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
+      store4_kcont<PREC>(&L[rr * LDK + kc], r[c]);
+    }
+  };
+  auto store_mc = [&](LT* L, const f32x4* r, int NB_) {
+    if (tid < NB_) {
+      const int kq = (tid % (BK / 4)) * 4;
+      const int rq = (tid / (BK / 4)) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f32x4 t = {r[0][e], r[1][e], r[2][e], r[3][e]};
+        store4_kcont<PREC>(&L[(rq + e) * LDK + kq], t);
       }
     }
   };
+  auto gload = [&](int k0) {
+    if (!TA) load_kc(ra, g.A, g.lda, m0, g.M, k0, g.vecA, NCA);
+    else load_mc(ra, g.A, g.lda, m0, g.M, k0, g.vecA, NBA, false);
+    if (TB) load_kc(rb, g.B, g.ldb, n0, g.N, k0, g.vecB, NCB);
+    else load_mc(rb, g.B, g.ldb, n0, g.N, k0, g.vecB, NBB, shiftK);
+  };
   auto lstore = [&]() {
-#pragma unroll
-    for (int c = 0; c < NCA; ++c) {
-      int idx = tid + 256 * c;
-      if (!TA) {
-        int r = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
-        store4_kcont<PREC>(&As[r * LDK + kc], ra[c]);
-      } else {
-        int kr = idx / (BM / 4), mc = (idx % (BM / 4)) * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) store1<PREC>(&As[(mc + e) * LDK + kr], ra[c][e]);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) {
-      int idx = tid + 256 * c;
-      if (TB) {
-        int r = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
-        store4_kcont<PREC>(&Bs[r * LDK + kc], rb[c]);
-      } else {
-        int kr = idx / (BN / 4), nc = (idx % (BN / 4)) * 4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) store1<PREC>(&Bs[(nc + e) * LDK + kr], rb[c][e]);
-      }
-    }
+    if (!TA) store_kc(As, ra, NCA); else store_mc(As, ra, NBA);
+    if (TB) store_kc(Bs, rb, NCB); else store_mc(Bs, rb, NBB);
   };
 
   const int l32 = lane & 31, h = lane >> 5;
@@ -280,8 +290,10 @@ static void gemm_plan(int M, int N, int K, int* bm, int* bn, int* splits, int* k
   *bn = big ? 128 : 64;
   const long tiles = (long)((M + *bm - 1) / *bm) * ((N + *bn - 1) / *bn);
   int s = 1;
-  if (tiles < 256 && K >= 4 * BK * 8) {
-    s = (int)((512 + tiles - 1) / tiles);
+  // long-K products (weight gradients over B*T rows): split K until ~3 blocks per CU are
+  // resident, so the load latency of one block hides behind the MFMAs of the others
+  if (tiles < 768 && K >= 4 * BK * 8) {
+    s = (int)((768 + tiles - 1) / tiles);
     int maxs = K / (BK * 8);  // keep >= 8 k-tiles per split
     if (s > maxs) s = maxs;
     if (s > 64) s = 64;
@@ -324,7 +336,7 @@ extern "C" int mlvae_gemm(int prec, int trans_a, int trans_b, int M, int N, int 
   }
   g.splits = s; g.kchunk = kc;
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((N + bn - 1) / bn, (M + bm - 1) / bm, s);
+  dim3 grid(((N + bn - 1) / bn) * ((M + bm - 1) / bm), 1, s);
   if (bm == 128) {
     if (prec == PREC_F32) launch_t<128, 128, PREC_F32>(g, grid, trans_a, trans_b, st);
     else launch_t<128, 128, PREC_BF16>(g, grid, trans_a, trans_b, st);

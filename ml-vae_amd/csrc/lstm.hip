@@ -13,76 +13,99 @@
 //   its W_hh rows (4*HJ gate rows, interleaved  r = jj*4 + q  so one MFMA lane ends up
 //   holding i,f,g,o of one (unit, utterance)) stay resident in LDS for all T steps;
 //   the cell state c lives in a register of that lane.
-// Per step the workgroups of one (dir, group) all-gather h_{t-1} through a small exchange
-// buffer: payload stored write-through (sc1), every storing wave drains vmcnt, one lane
-// raises the slice's step flag (relaxed agent store), consumers poll the group's flags with
-// one wave, barrier, then read the payload with sc1 loads straight into MFMA operands
-// (MI355X_MICROARCH.md "Valid forms", row 1: one workgroup per CU, hipMalloc memory).
-// The backward pass all-gathers the pre-activation gate gradients dG_t instead and
-// forms dh_{t-1} = dG_t W_hh for its own hidden slice from a resident W_hh^T column slice.
+//
+// Hand-off (per step, between the workgroups of one (dir, batch group)): the data IS the
+// flag.  Every 8-byte granule of the exchange buffer (4 bf16 or 2 fp32 values) is written by
+// ONE write-through (sc1) 8-byte store and carries a one-bit step tag in the least significant
+// mantissa bit of its first value; a consumer issues all its operand loads (sc1, straight into
+// MFMA operand registers), checks every granule's tag and re-issues until all match.  Four
+// slots (step mod 4) with tag = ((step >> 2) + 1) & 1 make a stale granule (4 steps old, or
+// the zero fill) always fail the check; no consumer can lag a producer by 4 steps because
+// every step needs every producer's previous step (MI355X_MICROARCH.md "Valid forms": R2
+// granules, one workgroup per CU, hipMalloc memory).  There is no flag, no drain before a
+// publish and no workgroup barrier on the forward step's critical path.
+// The backward pass all-gathers the pre-activation gate gradients dG_t the same way and forms
+// dh_{t-1} = dG_t W_hh for its own hidden slice from a resident W_hh^T column slice.
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
 constexpr int BG = 16;             // utterances per batch group (= MFMA N/M tile)
-constexpr int MAX_NJ = 64;         // hidden slices per group (flag stride)
-constexpr unsigned SPIN_LIMIT = 1u << 22;
+constexpr int NSLOT = 4;           // exchange slots (step mod 4)
+constexpr unsigned SPIN_LIMIT = 1u << 20;
 constexpr int MIN_LDS = 82 * 1024; // > half of 160 KiB: one workgroup per CU (residency)
 
 struct LstmArgs {
   int B, T, H;        // B = utterances handled by this launch (<= NB*16)
   int NB, NJ, HJ;     // batch groups, hidden slices per group, hidden units per slice
-  int Kp;             // H rounded up to 128 (fwd exchange row stride / MFMA K)
-  int K4p;            // 4H rounded up to 128 (bwd exchange row stride / MFMA K)
+  int Kp;             // H padded (pow2 >= 128): fwd exchange row stride / MFMA K
+  int K4p;            // 4H padded (pow2 >= 128): bwd exchange row stride / MFMA K
   const float* W0;    // W_hh forward dir  [4H, H]
   const float* W1;    // W_hh reverse dir  [4H, H]
   float* G;           // [B*T, 8H] fwd: in x-proj(+biases) out activated gates; bwd: in gates, out dG
   float* Cs;          // [B*T, 2H] cell states (fwd writes, bwd reads)
   float* Y;           // [B*T, 2H] fwd: out h; bwd: in dY (grad wrt layer output)
-  void* xbuf;         // exchange buffer [2 dirs][NB][2 slots][16][Kp or K4p]
-  unsigned* flags;    // [2][NB][MAX_NJ]
+  void* xbuf;         // exchange buffer [2 dirs][NB][NSLOT][16][Kp or K4p]
   int* err;
+  unsigned long long* dbg;  // optional per-step phase stamps of workgroup 0 (diagnostics)
+  int dbg_mode;             // diagnostics: bit0 = skip saved-activation stores (timing only)
 };
 
+// Phase stamps (s_memtime) of workgroup 0, thread 0: dbg[s*8 + phase]
+#define STAMP(ph)                                                              \
+  do {                                                                         \
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                          \
+      a.dbg[(size_t)s * 8 + (ph)] = __builtin_amdgcn_s_memtime();              \
+  } while (0)
+
 template <int PREC> struct Elt;
-template <> struct Elt<PREC_F32> { typedef float T; };
-template <> struct Elt<PREC_BF16> { typedef short T; };
+template <> struct Elt<PREC_F32> { typedef float T; static constexpr int GE = 2; };   // per granule
+template <> struct Elt<PREC_BF16> { typedef short T; static constexpr int GE = 4; };
 
-__device__ __forceinline__ bool wait_group(const unsigned* flags, int NJ, unsigned target,
-                                           int lane, int* err) {
-  unsigned spins = 0;
-  while (true) {
-    unsigned f = lane < NJ ? ld_flag(flags + lane) : 0xffffffffu;
-    if (__all(f >= target)) return true;
-    if (++spins > SPIN_LIMIT) {
-      if (lane == 0) atomicExch(err, 1);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
+__device__ __forceinline__ unsigned step_tag(int s) { return (unsigned)(((s >> 2) + 1) & 1); }
+
+// Granule packing: value 0 carries the tag in its least significant bit.
+__device__ __forceinline__ unsigned long long pack_bf16(float v0, float v1, float v2, float v3,
+                                                        unsigned tag) {
+  const unsigned e0 = ((unsigned)(unsigned short)f2bf(v0) & ~1u) | tag;
+  const unsigned lo = e0 | ((unsigned)(unsigned short)f2bf(v1) << 16);
+  const unsigned hi = (unsigned)(unsigned short)f2bf(v2) | ((unsigned)(unsigned short)f2bf(v3) << 16);
+  return ((unsigned long long)hi << 32) | lo;
 }
-
-__device__ __forceinline__ void drain_and_publish(unsigned* flag, unsigned value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_flag(flag, value);
-  }
+__device__ __forceinline__ unsigned long long pack_f32(float v0, float v1, unsigned tag) {
+  const unsigned e0 = (__float_as_uint(v0) & ~1u) | tag;
+  return ((unsigned long long)__float_as_uint(v1) << 32) | e0;
+}
+// one 8-byte write-through store per granule (buffer_store_dwordx2 ... sc1)
+__device__ __forceinline__ void st_granule(__amdgpu_buffer_rsrc_t r, unsigned byte_off,
+                                           unsigned long long v) {
+  u32x2 w = {(unsigned)v, (unsigned)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, byte_off, 0, 16 /*sc1*/);
+}
+// a 16-byte load holds two granules; their tags sit in dwords 0 and 2
+__device__ __forceinline__ bool tags_ok(u32x4 v, unsigned tag, bool g0, bool g1) {
+  return (!g0 || (v[0] & 1u) == tag) && (!g1 || (v[2] & 1u) == tag);
 }
 
 // ---------------------------------------------------------------------------------------
 // forward recurrence
 // ---------------------------------------------------------------------------------------
-template <int PREC, int HJ>
+// K is split over the 4 waves (each polls/loads a quarter of h_{t-1}: 4x less hand-off
+// traffic than every wave reading all of it) and partials are reduced through LDS:
+// double-buffered for bf16 (one barrier per step); single-buffered for fp32, whose
+// resident weights leave no room for a second buffer (two barriers).
+template <int PREC, int HJ, int NL>
 __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
   typedef typename Elt<PREC>::T ET;
-  constexpr int ROWS = 4 * HJ, MT = ROWS / 16, KS = MT >= 4 ? 1 : 4 / MT;
-  constexpr int KSTEP = PREC == PREC_F32 ? 16 : 32;  // k consumed per operand load
+  constexpr int ROWS = 4 * HJ, MT = ROWS / 16;       // gate rows, 16-row MFMA tiles
+  constexpr int KS = 4;
+  constexpr int NRED = PREC == PREC_F32 ? 1 : 2;     // reduction buffers
+  constexpr int KSTEP = PREC == PREC_F32 ? 16 : 32;  // k consumed per 16-byte operand load
+  constexpr int EPL = PREC == PREC_F32 ? 4 : 8;      // elements per 16-byte load
+  constexpr int GE = Elt<PREC>::GE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int LDW = a.Kp + (PREC == PREC_F32 ? 4 : 8);
-  ET* Wl = reinterpret_cast<ET*>(smem);
-  float* red = reinterpret_cast<float*>(smem + (size_t)ROWS * LDW * sizeof(ET));
+  f32x4* red0 = reinterpret_cast<f32x4*>(smem);  // [NRED][4][MT][64] partials
   __shared__ int abort_flag;
 
   const int ngroups = 2 * a.NB;
@@ -92,107 +115,185 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* W = dir ? a.W1 : a.W0;
 
-  // resident weight slice: row r = jj*4 + q  <-  W_hh[q*H + j0 + jj][:], zero padded to Kp
-  for (int idx = tid; idx < ROWS * a.Kp; idx += 256) {
-    int r = idx / a.Kp, k = idx % a.Kp;
-    int jj = r >> 2, q = r & 3;
-    float v = k < H ? W[(size_t)(q * H + j0 + jj) * H + k] : 0.f;
-    if constexpr (PREC == PREC_F32) Wl[r * LDW + k] = v; else Wl[r * LDW + k] = f2bf(v);
+  // wave w owns M-tile w: lane (bi, q) holds gates i,f,g,o of unit 4w+q, utterance bi.
+  // Every wave computes partials of all MT tiles over its quarter of K.
+  const int bi = lane & 15, q = lane >> 4;
+  const bool owner = wave < MT;
+  const int jj = wave * 4 + q;
+  const int bglob = grp * BG + bi;
+  const bool valid = owner && bglob < a.B;
+  const int kb = wave * (a.Kp / 4);
+  const bool loader = true;
+
+  // The resident weight slice lives in registers as ready MFMA A-fragments:
+  // tile m row r = jj*4 + q  <-  W_hh[q*H + j0 + jj][k], zero padded to Kp.
+  typedef typename std::conditional<PREC == PREC_F32, f32x4, bf16x8>::type WFrag;
+  WFrag wreg[NL][MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int r = m * 16 + bi;
+    const float* wrow = W + (size_t)((r & 3) * H + j0 + (r >> 2)) * H;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int k0 = kb + i * KSTEP + EPL * q;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {  // clamped, unconditional loads: no per-element branch
+        const float ld = wrow[min(k0 + e, H - 1)];
+        const float v = k0 + e < H ? ld : 0.f;
+        if constexpr (PREC == PREC_F32) wreg[i][m][e] = v; else wreg[i][m][e] = f2bf(v);
+      }
+    }
   }
   if (tid == 0) abort_flag = 0;
   __syncthreads();
 
-  const int mt = wave % MT, ks = wave / MT;
-  const bool active = ks < KS && wave < MT * KS;
-  const bool owner = active && ks == 0;  // lanes that own (unit, utterance) cells
-  const int bi = lane & 15, q = lane >> 4;
-  const int jj = mt * 4 + q;             // owned unit (owner lanes)
-  const int bglob = grp * BG + bi;
-  const bool valid = owner && bglob < a.B;
-  const int kper = a.Kp / KS, kb = ks * kper;
+  const size_t xslot = (size_t)BG * a.Kp;  // elements per slot
+  ET* xb = reinterpret_cast<ET*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
+  auto xr = make_rsrc(xb, (unsigned)(NSLOT * xslot * sizeof(ET)));
 
-  const size_t xstride = (size_t)BG * a.Kp;  // one slot
-  ET* xb = reinterpret_cast<ET*>(a.xbuf) + (size_t)(dir * a.NB + grp) * 2 * xstride;
-  const unsigned xbytes = (unsigned)(2 * xstride * sizeof(ET));
-  auto xr = make_rsrc(xb, xbytes);
-  unsigned* gflags = a.flags + (size_t)(dir * a.NB + grp) * MAX_NJ;
-
-  float c = 0.f;
-  for (int s = 0; s < T; ++s) {
-    const int t = dir ? T - 1 - s : s;
-    const size_t n = (size_t)bglob * T + t;
-    float gx[4] = {0.f, 0.f, 0.f, 0.f};
-    if (valid) {
-      const float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + jj;
+  // input projection of step s, loaded one step ahead (issued before the previous step's
+  // plain stores, so the compiler never has to drain those stores to order an aliasing load)
+  float gx[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_gx = [&](int s_) {
+    if (valid && s_ < T) {
+      const int t_ = dir ? T - 1 - s_ : s_;
+      const float* gp = a.G + ((size_t)bglob * T + t_) * 8 * H + dir * 4 * H + j0 + jj;
 #pragma unroll
       for (int g = 0; g < 4; ++g) gx[g] = gp[g * H];
     }
+  };
+  load_gx(0);
+  float c = 0.f;
+  for (int s = 0; s < T; ++s) {
+    STAMP(0);
+    const int t = dir ? T - 1 - s : s;
+    const size_t n = (size_t)bglob * T + t;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4* red = red0 + (NRED == 2 ? (s & 1) * 4 * MT * 64 : 0);
     if (s > 0) {
-      if (wave == 0 && !wait_group(gflags, a.NJ, (unsigned)s, lane, a.err)) abort_flag = 1;
-      __syncthreads();
-      if (abort_flag) break;
-      if (active) {
-        const unsigned slot_off = (unsigned)(((s - 1) & 1) * xstride);
-        const ET* wrow = Wl + (mt * 16 + bi) * LDW;
-        for (int kk = kb; kk < kb + kper; kk += KSTEP) {
-          if constexpr (PREC == PREC_F32) {
-            u32x4 hv = ld_sc1_b128(xr, (slot_off + bi * a.Kp + kk + 4 * q) * 4);
-            f32x4 wv = *reinterpret_cast<const f32x4*>(wrow + kk + 4 * q);
+      if (loader) {
+        // poll = load: issue every operand load, check every granule's tag, retry until fresh
+        const unsigned tag = step_tag(s - 1);
+        const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * a.Kp + kb + EPL * q;
+        u32x4 hv[NL];
+        unsigned spins = 0;
+        unsigned long long t_issue = 0;
+        while (true) {
+          if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[e], __uint_as_float(hv[e]), acc, 0, 0, 0);
-          } else {
-            u32x4 hv = ld_sc1_b128(xr, (slot_off + bi * a.Kp + kk + 8 * q) * 2);
-            bf16x8 wv = *reinterpret_cast<const bf16x8*>(wrow + kk + 8 * q);
-            bf16x8 hb = *reinterpret_cast<bf16x8*>(&hv);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, hb, acc, 0, 0, 0);
+          for (int i = 0; i < NL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * KSTEP) * sizeof(ET));
+          bool ok = true;
+#pragma unroll
+          for (int i = 0; i < NL; ++i) {
+            const int k0 = kb + i * KSTEP + EPL * q;
+            ok &= tags_ok(hv[i], tag, k0 < H, k0 + GE < H);
+          }
+          if (__all(ok)) break;
+          if (++spins > SPIN_LIMIT) {
+            if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+        STAMP(1);
+        if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
+          a.dbg[(size_t)s * 8 + 5] = t_issue;
+          a.dbg[(size_t)s * 8 + 6] = spins;
+        }
+        f32x4 part[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) part[m] = acc;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            if constexpr (PREC == PREC_F32) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                part[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wreg[i][m][e], __uint_as_float(hv[i][e]), part[m], 0, 0, 0);
+            } else {
+              bf16x8 hb = *reinterpret_cast<bf16x8*>(&hv[i]);
+              part[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[i][m], hb, part[m], 0, 0, 0);
+            }
           }
         }
+        if constexpr (KS == 1) {
+          acc = part[0];
+        } else {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) red[(wave * MT + m) * 64 + lane] = part[m];
+        }
       }
+      STAMP(2);
       if constexpr (KS > 1) {
-        if (active && ks > 0) *reinterpret_cast<f32x4*>(red + (((ks - 1) * MT + mt) * 64 + lane) * 4) = acc;
         __syncthreads();
         if (owner) {
 #pragma unroll
-          for (int p = 1; p < KS; ++p) {
-            f32x4 o = *reinterpret_cast<const f32x4*>(red + (((p - 1) * MT + mt) * 64 + lane) * 4);
-            acc += o;
-          }
+          for (int w = 0; w < 4; ++w) acc += red[(w * MT + wave) * 64 + lane];
+        }
+        if (NRED == 1) __syncthreads();  // red is reused next step
+      } else {
+        if (abort_flag) break;
+      }
+      if (KS > 1 && abort_flag) break;
+      STAMP(3);
+    }
+    float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, hv = 0.f;
+    if (owner) {
+      if (valid) {
+        // acc[q'] = recurrent part of gate q' for unit jj, utterance bi
+        ig = sigmoid_fast(acc[0] + gx[0]);
+        fg = sigmoid_fast(acc[1] + gx[1]);
+        gg = tanh_fast(acc[2] + gx[2]);
+        og = sigmoid_fast(acc[3] + gx[3]);
+        c = fg * c + ig * gg;
+        hv = og * tanh_fast(c);
+      }
+      if (s + 1 < T) {
+        // gather 4 (bf16) / 2 (fp32) consecutive units of one utterance into one granule;
+        // padded utterances publish zeros so every granule a consumer checks gets written
+        const unsigned tag = step_tag(s);
+        const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * a.Kp + j0 + wave * 4;
+        if constexpr (PREC == PREC_F32) {
+          const float h1 = __shfl(hv, lane + 16, 64);
+          if ((q & 1) == 0) st_granule(xr, (unsigned)((row + q) * sizeof(ET)), pack_f32(hv, h1, tag));
+        } else {
+          const float h1 = __shfl(hv, lane + 16, 64);
+          const float h2 = __shfl(hv, lane + 32, 64);
+          const float h3 = __shfl(hv, lane + 48, 64);
+          if (q == 0) st_granule(xr, (unsigned)(row * sizeof(ET)), pack_bf16(hv, h1, h2, h3, tag));
         }
       }
     }
-    if (valid) {
-      // acc[q'] = recurrent part of gate q' for unit jj, utterance bi
-      float ig = sigmoidf_(acc[0] + gx[0]);
-      float fg = sigmoidf_(acc[1] + gx[1]);
-      float gg = tanhf(acc[2] + gx[2]);
-      float og = sigmoidf_(acc[3] + gx[3]);
-      c = fg * c + ig * gg;
-      float hv = og * tanhf(c);
+    STAMP(4);
+    load_gx(s + 1);
+    if (valid && !(a.dbg_mode & 1)) {  // saved activations: plain stores, off the critical path
       float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + jj;
       gp[0] = ig; gp[H] = fg; gp[2 * H] = gg; gp[3 * H] = og;
       a.Cs[n * 2 * H + dir * H + j0 + jj] = c;
       a.Y[n * 2 * H + dir * H + j0 + jj] = hv;
-      const unsigned off = (unsigned)((s & 1) * xstride + bi * a.Kp + j0 + jj);
-      if constexpr (PREC == PREC_F32) st_sc1_b32(xr, off * 4, __float_as_uint(hv));
-      else st_sc1_b16(xr, off * 2, (unsigned short)f2bf(hv));
     }
-    if (s + 1 < T) drain_and_publish(gflags + js, (unsigned)(s + 1));
   }
 }
 
 // ---------------------------------------------------------------------------------------
 // backward recurrence (BPTT)
 // ---------------------------------------------------------------------------------------
-template <int PREC, int HJ>
+// HJ units per workgroup: HJ <= 16 -> one 16-wide MFMA N-tile (padded), one unit per thread;
+// HJ = 32 -> two N-tiles and two units per thread.  Larger HJ = fewer workgroups per group,
+// and the all-gather volume (every workgroup reads the group's whole dG_t) scales with that
+// count, so the backward prefers HJ = 32.
+template <int PREC, int HJ, int NL>
 __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
   typedef typename Elt<PREC>::T ET;
   constexpr int KSTEP = PREC == PREC_F32 ? 16 : 32;
+  constexpr int EPL = PREC == PREC_F32 ? 4 : 8;
+  constexpr int GE = Elt<PREC>::GE;
+  constexpr int NT = HJ > 16 ? HJ / 16 : 1;   // MFMA N-tiles (units)
+  constexpr int UPT = NT;                      // units per thread in the cell phase
+  constexpr int RW = 16 * NT;                  // reduction row width (units)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int LDW = a.K4p + (PREC == PREC_F32 ? 4 : 8);
-  ET* Wt = reinterpret_cast<ET*>(smem);  // [16 cols (unit jj)][K4p] : W_hh[g][j0+jj]
-  float* red = reinterpret_cast<float*>(smem + (size_t)16 * LDW * sizeof(ET));  // [4][16][16]
+  float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][16 utterances][RW] partials
   __shared__ int abort_flag;
 
   const int ngroups = 2 * a.NB;
@@ -202,191 +303,311 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* W = dir ? a.W1 : a.W0;
 
-  for (int idx = tid; idx < 16 * a.K4p; idx += 256) {
-    int jj = idx / a.K4p, g = idx % a.K4p;
-    float v = (jj < HJ && g < G4) ? W[(size_t)g * H + j0 + jj] : 0.f;
-    if constexpr (PREC == PREC_F32) Wt[jj * LDW + g] = v; else Wt[jj * LDW + g] = f2bf(v);
+  // MFMA roles: A = dG (rows = utterances), B = W_hh^T slice (cols = units), K = 4H over 4 waves
+  const int bi = lane & 15, q = lane >> 4;
+  const int kb = wave * (a.K4p / 4);
+  // cell roles: thread -> (utterance cb, units cj + 16u); a wave holds 4 utterances
+  const int cb = tid >> 4, cj = tid & 15;
+  const int bglob = grp * BG + cb;
+  const bool bvalid = bglob < a.B;
+
+  // resident W_hh^T column slice as ready MFMA B-fragments: tile nt, column bi = unit nt*16+bi
+  typedef typename std::conditional<PREC == PREC_F32, f32x4, bf16x8>::type WFrag;
+  WFrag wreg[NL][NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int u = nt * 16 + bi;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int g0 = kb + i * KSTEP + EPL * q;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {  // clamped, unconditional loads: no per-element branch
+        const float ld = W[(size_t)min(g0 + e, G4 - 1) * H + j0 + min(u, HJ - 1)];
+        const float v = (u < HJ && g0 + e < G4) ? ld : 0.f;
+        if constexpr (PREC == PREC_F32) wreg[i][nt][e] = v; else wreg[i][nt][e] = f2bf(v);
+      }
+    }
   }
   if (tid == 0) abort_flag = 0;
   __syncthreads();
 
-  // MFMA roles: A = dG (rows = utterances), B = W_hh^T slice (cols = units), K = 4H over 4 waves
-  const int bi = lane & 15, q = lane >> 4;
-  const int kper = a.K4p / 4, kb = wave * kper;
-  // cell roles: thread -> (utterance cb, unit cj)
-  const int cb = tid >> 4, cj = tid & 15;
-  const int bglob = grp * BG + cb;
-  const bool valid = cj < HJ && bglob < a.B;
-  const int j = j0 + cj;
+  const size_t xslot = (size_t)BG * a.K4p;
+  ET* xb = reinterpret_cast<ET*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
+  auto xr = make_rsrc(xb, (unsigned)(NSLOT * xslot * sizeof(ET)));
 
-  const size_t xstride = (size_t)BG * a.K4p;
-  ET* xb = reinterpret_cast<ET*>(a.xbuf) + (size_t)(dir * a.NB + grp) * 2 * xstride;
-  auto xr = make_rsrc(xb, (unsigned)(2 * xstride * sizeof(ET)));
-  unsigned* gflags = a.flags + (size_t)(dir * a.NB + grp) * MAX_NJ;
-  const int grp_b0 = grp * BG;
-
-  float dc = 0.f;
-  for (int s = 0; s < T; ++s) {
-    const int t = dir ? s : T - 1 - s;          // reverse of the forward processing order
-    const int tprev = dir ? t + 1 : t - 1;       // the forward's previous step
-    const size_t n = (size_t)bglob * T + t;
-    // prefetch this step's cell inputs
-    float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f, cc = 0.f, cp = 0.f, dy = 0.f;
-    if (valid) {
-      const float* gp = a.G + n * 8 * H + dir * 4 * H + j;
-      gi = gp[0]; gf = gp[H]; gg = gp[2 * H]; go = gp[3 * H];
-      cc = a.Cs[n * 2 * H + dir * H + j];
-      if (tprev >= 0 && tprev < T) cp = a.Cs[((size_t)bglob * T + tprev) * 2 * H + dir * H + j];
-      dy = a.Y[n * 2 * H + dir * H + j];
-    }
-    float dhrec = 0.f;
-    if (s > 0) {
-      if (wave == 0 && !wait_group(gflags, a.NJ, (unsigned)s, lane, a.err)) abort_flag = 1;
-      __syncthreads();
-      if (abort_flag) break;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const unsigned slot_off = (unsigned)(((s - 1) & 1) * xstride);
-      const ET* wcol = Wt + bi * LDW;  // B operand column = unit bi
-      for (int kk = kb; kk < kb + kper; kk += KSTEP) {
-        if constexpr (PREC == PREC_F32) {
-          u32x4 gv = ld_sc1_b128(xr, (slot_off + bi * a.K4p + kk + 4 * q) * 4);
-          f32x4 wv = *reinterpret_cast<const f32x4*>(wcol + kk + 4 * q);
+  // cell inputs of step s (saved gates, c_t, c_{t-1}, dY) per owned unit, loaded one step
+  // ahead and issued before the previous step's dG stores (no store drain on aliasing loads)
+  float gi[UPT], gf[UPT], gg[UPT], go[UPT], cc[UPT], cp[UPT], dy[UPT], dc[UPT];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(gv[e]), wv[e], acc, 0, 0, 0);
-        } else {
-          u32x4 gv = ld_sc1_b128(xr, (slot_off + bi * a.K4p + kk + 8 * q) * 2);
-          bf16x8 gb = *reinterpret_cast<bf16x8*>(&gv);
-          bf16x8 wv = *reinterpret_cast<const bf16x8*>(wcol + kk + 8 * q);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gb, wv, acc, 0, 0, 0);
+  for (int u = 0; u < UPT; ++u) { gi[u] = gf[u] = gg[u] = go[u] = cc[u] = cp[u] = dy[u] = dc[u] = 0.f; }
+  auto load_cell = [&](int s_) {
+    if (bvalid && s_ < T) {
+      const int t_ = dir ? s_ : T - 1 - s_;
+      const int tp_ = dir ? t_ + 1 : t_ - 1;
+      const bool has_prev = tp_ >= 0 && tp_ < T;
+      const size_t n_ = (size_t)bglob * T + t_;
+      const size_t np_ = (size_t)bglob * T + min(max(tp_, 0), T - 1);
+#pragma unroll
+      for (int u = 0; u < UPT; ++u) {
+        const int uu = cj + 16 * u;
+        if (uu < HJ) {
+          const int j = j0 + uu;
+          const float* gp = a.G + n_ * 8 * H + dir * 4 * H + j;
+          gi[u] = gp[0]; gf[u] = gp[H]; gg[u] = gp[2 * H]; go[u] = gp[3 * H];
+          cc[u] = a.Cs[n_ * 2 * H + dir * H + j];
+          const float cpl = a.Cs[np_ * 2 * H + dir * H + j];
+          cp[u] = has_prev ? cpl : 0.f;
+          dy[u] = a.Y[n_ * 2 * H + dir * H + j];
         }
       }
-      // C layout: col = lane&15 = unit, row = 4*(lane>>4)+r = utterance
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(wave * 16 + 4 * q + r) * 16 + bi] = acc[r];
-      __syncthreads();
-      dhrec = red[(0 * 16 + cb) * 16 + cj] + red[(1 * 16 + cb) * 16 + cj] +
-              red[(2 * 16 + cb) * 16 + cj] + red[(3 * 16 + cb) * 16 + cj];
     }
-    if (valid) {
-      const float dh = dy + dhrec;
-      const float tc = tanhf(cc);
-      const float d_o = dh * tc;
-      const float dcs = dc + dh * go * (1.f - tc * tc);
-      const float di = dcs * gg, dgg = dcs * gi, df = dcs * cp;
-      dc = dcs * gf;
-      const float dai = di * gi * (1.f - gi);
-      const float daf = df * gf * (1.f - gf);
-      const float dag = dgg * (1.f - gg * gg);
-      const float dao = d_o * go * (1.f - go);
-      float* gp = a.G + n * 8 * H + dir * 4 * H + j;
-      gp[0] = dai; gp[H] = daf; gp[2 * H] = dag; gp[3 * H] = dao;
-      const unsigned off = (unsigned)((s & 1) * xstride + cb * a.K4p + j);
-      if constexpr (PREC == PREC_F32) {
-        st_sc1_b32(xr, (off + 0 * H) * 4, __float_as_uint(dai));
-        st_sc1_b32(xr, (off + 1 * H) * 4, __float_as_uint(daf));
-        st_sc1_b32(xr, (off + 2 * H) * 4, __float_as_uint(dag));
-        st_sc1_b32(xr, (off + 3 * H) * 4, __float_as_uint(dao));
-      } else {
-        st_sc1_b16(xr, (off + 0 * H) * 2, (unsigned short)f2bf(dai));
-        st_sc1_b16(xr, (off + 1 * H) * 2, (unsigned short)f2bf(daf));
-        st_sc1_b16(xr, (off + 2 * H) * 2, (unsigned short)f2bf(dag));
-        st_sc1_b16(xr, (off + 3 * H) * 2, (unsigned short)f2bf(dao));
+  };
+  load_cell(0);
+  for (int s = 0; s < T; ++s) {
+    STAMP(0);
+    const int t = dir ? s : T - 1 - s;          // reverse of the forward processing order
+    const size_t n = (size_t)bglob * T + t;
+    float* rb = red + (s & 1) * 4 * 16 * RW;
+    float dhrec[UPT];
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) dhrec[u] = 0.f;
+    if (s > 0) {
+      const unsigned tag = step_tag(s - 1);
+      const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * a.K4p + kb + EPL * q;
+      u32x4 gv[NL];
+      unsigned spins = 0;
+      unsigned long long t_issue = 0;
+      while (true) {
+        if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < NL; ++i) gv[i] = ld_sc1_b128(xr, (ebase + i * KSTEP) * sizeof(ET));
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const int g0 = kb + i * KSTEP + EPL * q;
+          ok &= tags_ok(gv[i], tag, g0 < G4, g0 + GE < G4);
+        }
+        if (__all(ok)) break;
+        if (++spins > SPIN_LIMIT) {
+          if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      STAMP(1);
+      if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.dbg[(size_t)s * 8 + 5] = t_issue;
+        a.dbg[(size_t)s * 8 + 6] = spins;
+      }
+      f32x4 acc[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          if constexpr (PREC == PREC_F32) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(gv[i][e]), wreg[i][nt][e], acc[nt], 0, 0, 0);
+          } else {
+            bf16x8 gb = *reinterpret_cast<bf16x8*>(&gv[i]);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gb, wreg[i][nt], acc[nt], 0, 0, 0);
+          }
+        }
+      }
+      // C layout: col = lane&15 = unit (of tile nt), row = 4*(lane>>4)+r = utterance
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rb[(wave * 16 + 4 * q + r) * RW + nt * 16 + bi] = acc[nt][r];
+      STAMP(2);
+      __syncthreads();  // double-buffered red: one barrier per step
+      STAMP(3);
+      if (abort_flag) break;
+#pragma unroll
+      for (int u = 0; u < UPT; ++u) {
+        const int uu = cj + 16 * u;
+        dhrec[u] = rb[(0 * 16 + cb) * RW + uu] + rb[(1 * 16 + cb) * RW + uu] +
+                   rb[(2 * 16 + cb) * RW + uu] + rb[(3 * 16 + cb) * RW + uu];
       }
     }
-    (void)grp_b0;
-    if (s + 1 < T) drain_and_publish(gflags + js, (unsigned)(s + 1));
+    float dG[UPT][4];
+    float sgi[UPT], sgf[UPT], sgg[UPT], sgo[UPT], scc[UPT], scp[UPT], sdy[UPT];
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      sgi[u] = gi[u]; sgf[u] = gf[u]; sgg[u] = gg[u]; sgo[u] = go[u];
+      scc[u] = cc[u]; scp[u] = cp[u]; sdy[u] = dy[u];
+    }
+    load_cell(s + 1);
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) {
+      dG[u][0] = dG[u][1] = dG[u][2] = dG[u][3] = 0.f;
+      if (bvalid && cj + 16 * u < HJ) {
+        const float dh = sdy[u] + dhrec[u];
+        const float tc = tanh_fast(scc[u]);
+        const float d_o = dh * tc;
+        const float dcs = dc[u] + dh * sgo[u] * (1.f - tc * tc);
+        const float di = dcs * sgg[u], dgg = dcs * sgi[u], df = dcs * scp[u];
+        dc[u] = dcs * sgf[u];
+        dG[u][0] = di * sgi[u] * (1.f - sgi[u]);
+        dG[u][1] = df * sgf[u] * (1.f - sgf[u]);
+        dG[u][2] = dgg * (1.f - sgg[u] * sgg[u]);
+        dG[u][3] = d_o * sgo[u] * (1.f - sgo[u]);
+      }
+    }
+    if (s + 1 < T) {
+      // granules of 4 (bf16) / 2 (fp32) consecutive units of one gate and utterance; the
+      // lanes of consecutive units are adjacent (cj = tid & 15); padded utterances publish 0
+      const unsigned tag = step_tag(s);
+#pragma unroll
+      for (int u = 0; u < UPT; ++u) {
+        const int uu = cj + 16 * u;
+        const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)cb * a.K4p + j0 + uu;
+        if constexpr (PREC == PREC_F32) {
+          float v1[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v1[g] = __shfl(dG[u][g], lane + 1, 64);
+          if (uu < HJ && (cj & 1) == 0) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              st_granule(xr, (unsigned)((row + (size_t)g * H) * sizeof(ET)), pack_f32(dG[u][g], v1[g], tag));
+          }
+        } else {
+          float v1[4], v2[4], v3[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            v1[g] = __shfl(dG[u][g], lane + 1, 64);
+            v2[g] = __shfl(dG[u][g], lane + 2, 64);
+            v3[g] = __shfl(dG[u][g], lane + 3, 64);
+          }
+          if (uu < HJ && (cj & 3) == 0) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              st_granule(xr, (unsigned)((row + (size_t)g * H) * sizeof(ET)),
+                         pack_bf16(dG[u][g], v1[g], v2[g], v3[g], tag));
+          }
+        }
+      }
+    }
+    STAMP(4);
+    if (bvalid) {  // dG for the weight-gradient GEMMs: plain stores after the hand-off
+#pragma unroll
+      for (int u = 0; u < UPT; ++u) {
+        const int uu = cj + 16 * u;
+        if (uu < HJ) {
+          float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + uu;
+          gp[0] = dG[u][0]; gp[H] = dG[u][1]; gp[2 * H] = dG[u][2]; gp[3 * H] = dG[u][3];
+        }
+      }
+    }
   }
 }
 
 struct Plan {
-  int NB, NJ, HJ, Kp, K4p;
-  size_t lds_fwd, lds_bwd, xbytes_fwd, xbytes_bwd;
+  int NB, NJ, HJ, Kp, K4p;   // NJ/HJ of the launch being planned (fwd or bwd)
+  size_t lds, xbytes_fwd, xbytes_bwd;
 };
 
-int pick_hj(int H) { return H % 16 == 0 ? 16 : (H % 8 == 0 ? 8 : (H % 4 == 0 ? 4 : 0)); }
+int pow2_at_least(int v) { int p = 1; while (p < v) p <<= 1; return p; }
 
-Plan make_plan(int B, int H, int prec) {
+int pick_hj(int H, bool fwd, int prec) {
+  // HJ = 32 halves the backward's all-gather traffic but measured slower at c2 (5.6 vs
+  // 5.0 us/step: per-workgroup load latency, not aggregate bandwidth, bounds the step);
+  // kept selectable for larger H.
+  if (!fwd && prec == PREC_BF16 && H % 32 == 0 && H >= 2048) return 32;
+  return H % 16 == 0 ? 16 : (H % 8 == 0 ? 8 : (H % 4 == 0 ? 4 : 0));
+}
+
+Plan make_plan(int B, int H, int prec, bool fwd) {
   Plan p;
-  p.HJ = pick_hj(H);
+  p.HJ = pick_hj(H, fwd, prec);
   p.NJ = p.HJ ? H / p.HJ : 0;
   p.NB = (B + BG - 1) / BG;
-  p.Kp = (H + 127) / 128 * 128;
-  p.K4p = (4 * H + 127) / 128 * 128;
+  p.Kp = pow2_at_least(H < 128 ? 128 : H);
+  p.K4p = pow2_at_least(4 * H < 128 ? 128 : 4 * H);
   const size_t esz = prec == PREC_F32 ? 4 : 2;
-  const int pad = prec == PREC_F32 ? 4 : 8;
-  p.lds_fwd = (size_t)4 * p.HJ * (p.Kp + pad) * esz + 3 * 64 * 4 * 4 * 4;
-  p.lds_bwd = (size_t)16 * (p.K4p + pad) * esz + 4 * 16 * 16 * 4;
-  if (p.lds_fwd < MIN_LDS) p.lds_fwd = MIN_LDS;
-  if (p.lds_bwd < MIN_LDS) p.lds_bwd = MIN_LDS;
-  p.xbytes_fwd = (size_t)2 * p.NB * 2 * BG * p.Kp * esz;
-  p.xbytes_bwd = (size_t)2 * p.NB * 2 * BG * p.K4p * esz;
+  const int hjt = p.HJ > 16 ? p.HJ : 16;
+  p.lds = fwd ? (size_t)(prec == PREC_F32 ? 1 : 2) * 4 * (p.HJ / 4) * 64 * 16
+              : (size_t)2 * 4 * 16 * hjt * 4;
+  if (p.lds < MIN_LDS) p.lds = MIN_LDS;
+  p.xbytes_fwd = (size_t)2 * p.NB * NSLOT * BG * p.Kp * esz;
+  p.xbytes_bwd = (size_t)2 * p.NB * NSLOT * BG * p.K4p * esz;
   return p;
 }
 
-int max_batch_per_launch(int H) {
+int max_batch_per_launch(int H, bool fwd, int prec) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  int hj = pick_hj(H);
+  int hj = pick_hj(H, fwd, prec);
   int nj = hj ? H / hj : 1;
   int nb = cus / (2 * nj);
   return nb * BG;
 }
 
-template <int PREC, int HJ>
-int launch(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
+template <int PREC, int HJ, int NL>
+int launch_nl(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
   dim3 grid(2 * a.NB * a.NJ);
-  if (fwd) {
-    auto k = lstm_fwd_kernel<PREC, HJ>;
-    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_fwd) != hipSuccess) {
-      mlvae_set_error("lstm: cannot reserve %zu B LDS", p.lds_fwd);
-      return 2;
-    }
-    k<<<grid, 256, p.lds_fwd, s>>>(a);
-  } else {
-    auto k = lstm_bwd_kernel<PREC, HJ>;
-    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bwd) != hipSuccess) {
-      mlvae_set_error("lstm: cannot reserve %zu B LDS", p.lds_bwd);
-      return 2;
-    }
-    k<<<grid, 256, p.lds_bwd, s>>>(a);
+  auto k = fwd ? lstm_fwd_kernel<PREC, HJ, NL> : lstm_bwd_kernel<PREC, HJ, NL>;
+  const size_t lds = p.lds;
+  if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    mlvae_set_error("lstm: cannot reserve %zu B LDS", lds);
+    return 2;
   }
+  k<<<grid, 256, lds, s>>>(a);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
 
+template <int PREC, int HJ>
+int launch(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
+  constexpr int KSTEP = PREC == PREC_F32 ? 16 : 32;
+  constexpr int KSF = 4;  // forward K split (see lstm_fwd_kernel)
+  const int nl = fwd ? a.Kp / (KSF * KSTEP) : a.K4p / (4 * KSTEP);
+  switch (nl) {
+    case 1: return launch_nl<PREC, HJ, 1>(fwd, a, p, s);
+    case 2: return launch_nl<PREC, HJ, 2>(fwd, a, p, s);
+    case 4: return launch_nl<PREC, HJ, 4>(fwd, a, p, s);
+    case 8: return launch_nl<PREC, HJ, 8>(fwd, a, p, s);
+    case 16: return launch_nl<PREC, HJ, 16>(fwd, a, p, s);
+    case 32: return launch_nl<PREC, HJ, 32>(fwd, a, p, s);
+    default:
+      mlvae_set_error("lstm: H=%d needs %d operand loads per wave (max 32)", a.H, nl);
+      return 1;
+  }
+}
+
+unsigned long long* g_dbg = nullptr;
+int g_dbg_mode = 0;
+
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
-        float* Cs, float* Y, void* xbuf, size_t xbytes, unsigned* flags, size_t fbytes, int* err,
-        hipStream_t st) {
+        float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st) {
   if (B <= 0 || T <= 0) return 0;
   if (H <= 0 || H % 4 != 0) { mlvae_set_error("lstm: H=%d must be a positive multiple of 4", H); return 1; }
   if (prec != PREC_F32 && prec != PREC_BF16) { mlvae_set_error("lstm: bad prec %d", prec); return 1; }
-  const int bmax = max_batch_per_launch(H);
+  const int bmax = max_batch_per_launch(H, fwd, prec);
   if (bmax < BG) { mlvae_set_error("lstm: H=%d too large for one resident launch", H); return 1; }
-  Plan full = make_plan(bmax < B ? bmax : B, H, prec);
-  if (full.NJ > MAX_NJ) { mlvae_set_error("lstm: H=%d needs %d slices > %d", H, full.NJ, MAX_NJ); return 1; }
+  Plan full = make_plan(bmax < B ? bmax : B, H, prec, fwd);
   const size_t need_x = fwd ? full.xbytes_fwd : full.xbytes_bwd;
-  const size_t need_f = (size_t)2 * full.NB * MAX_NJ * sizeof(unsigned);
-  if (!xbuf || xbytes < need_x || !flags || fbytes < need_f || !err) {
-    mlvae_set_error("lstm: workspace too small (need x=%zu flags=%zu)", need_x, need_f);
+  if (!xbuf || xbytes < need_x || !err) {
+    mlvae_set_error("lstm: exchange workspace too small (need %zu B)", need_x);
     return 1;
   }
   // batch chunks of <= bmax utterances (rows are independent)
   for (int b0 = 0; b0 < B; b0 += bmax) {
     const int bc = B - b0 < bmax ? B - b0 : bmax;
-    Plan p = make_plan(bc, H, prec);
+    Plan p = make_plan(bc, H, prec, fwd);
     LstmArgs a;
     a.B = bc; a.T = T; a.H = H; a.NB = p.NB; a.NJ = p.NJ; a.HJ = p.HJ; a.Kp = p.Kp; a.K4p = p.K4p;
     a.W0 = W0; a.W1 = W1;
     a.G = G + (size_t)b0 * T * 8 * H;
     a.Cs = Cs + (size_t)b0 * T * 2 * H;
     a.Y = Y + (size_t)b0 * T * 2 * H;
-    a.xbuf = xbuf; a.flags = flags; a.err = err;
-    // re-initialise every polled word and the zero padding of the exchange rows
-    if (hipMemsetAsync(flags, 0, need_f, st) != hipSuccess ||
-        hipMemsetAsync(xbuf, 0, fwd ? p.xbytes_fwd : p.xbytes_bwd, st) != hipSuccess) {
+    a.xbuf = xbuf; a.err = err; a.dbg = g_dbg; a.dbg_mode = g_dbg_mode;
+    // re-initialise the exchange every call: zero fill = stale tag, zero padding
+    if (hipMemsetAsync(xbuf, 0, fwd ? p.xbytes_fwd : p.xbytes_bwd, st) != hipSuccess) {
       mlvae_set_error("lstm: memset failed");
       return 2;
     }
@@ -395,7 +616,8 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
       rc = p.HJ == 16 ? launch<PREC_F32, 16>(fwd, a, p, st)
          : p.HJ == 8 ? launch<PREC_F32, 8>(fwd, a, p, st) : launch<PREC_F32, 4>(fwd, a, p, st);
     } else {
-      rc = p.HJ == 16 ? launch<PREC_BF16, 16>(fwd, a, p, st)
+      rc = p.HJ == 32 ? launch<PREC_BF16, 32>(fwd, a, p, st)
+         : p.HJ == 16 ? launch<PREC_BF16, 16>(fwd, a, p, st)
          : p.HJ == 8 ? launch<PREC_BF16, 8>(fwd, a, p, st) : launch<PREC_BF16, 4>(fwd, a, p, st);
     }
     if (rc) return rc;
@@ -405,27 +627,38 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
 
 }  // namespace
 
-extern "C" int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes, size_t* fbytes) {
+extern "C" int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes) {
   if (H <= 0 || H % 4 != 0) { mlvae_set_error("lstm: H=%d must be a positive multiple of 4", H); return 1; }
-  const int bmax = max_batch_per_launch(H);
-  Plan p = make_plan(bmax < B ? bmax : B, H, prec);
-  *xbytes = p.xbytes_fwd > p.xbytes_bwd ? p.xbytes_fwd : p.xbytes_bwd;
-  *fbytes = (size_t)2 * p.NB * MAX_NJ * sizeof(unsigned);
+  const int bf = max_batch_per_launch(H, true, prec), bb = max_batch_per_launch(H, false, prec);
+  Plan pf = make_plan(bf < B ? bf : B, H, prec, true);
+  Plan pb = make_plan(bb < B ? bb : B, H, prec, false);
+  *xbytes = pf.xbytes_fwd > pb.xbytes_bwd ? pf.xbytes_fwd : pb.xbytes_bwd;
   return 0;
 }
 
 extern "C" int mlvae_lstm_fwd(int prec, int B, int T, int H, const float* w_hh_fwd,
                               const float* w_hh_rev, float* gates, float* cells, float* y,
-                              void* xbuf, size_t xbytes, unsigned* flags, size_t fbytes, int* err,
-                              void* stream) {
-  return run(true, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, cells, y, xbuf, xbytes, flags, fbytes,
-             err, (hipStream_t)stream);
+                              void* xbuf, size_t xbytes, int* err, void* stream) {
+  return run(true, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, cells, y, xbuf, xbytes, err,
+             (hipStream_t)stream);
 }
 
 extern "C" int mlvae_lstm_bwd(int prec, int B, int T, int H, const float* w_hh_fwd,
                               const float* w_hh_rev, float* gates, const float* cells,
-                              const float* dy, void* xbuf, size_t xbytes, unsigned* flags,
-                              size_t fbytes, int* err, void* stream) {
+                              const float* dy, void* xbuf, size_t xbytes, int* err, void* stream) {
   return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, const_cast<float*>(cells),
-             const_cast<float*>(dy), xbuf, xbytes, flags, fbytes, err, (hipStream_t)stream);
+             const_cast<float*>(dy), xbuf, xbytes, err, (hipStream_t)stream);
+}
+
+// Diagnostics: when set, the next recurrence launches record per-step phase stamps of
+// workgroup 0 into buf[T*8] (s_memtime ticks).  Pass NULL to disable.
+extern "C" int mlvae_lstm_set_debug(void* buf) {
+  g_dbg = reinterpret_cast<unsigned long long*>(buf);
+  return 0;
+}
+
+// Diagnostics only (timing experiments): bit0 skips the forward's saved-activation stores.
+extern "C" int mlvae_lstm_set_debug_mode(int mode) {
+  g_dbg_mode = mode;
+  return 0;
 }

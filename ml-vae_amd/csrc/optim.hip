@@ -34,46 +34,69 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 struct AdamArgs {
   float* p; float* m; float* v; const float* g;
   size_t n;
-  const double* partials; int nparts;
-  const float* loss;          // skip the step when non-finite (may be null)
-  const int* step;            // completed steps so far (device); this update uses step+1
-  float lr, b1, b2, eps, max_norm;
-  float* norm_out;            // total grad norm (may be null)
+  const float* hyp;           // [coef, skip, step_size, bc2_sqrt] from adam_prologue
+  float b1, b2, eps;
 };
 
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-  __shared__ float coef_s;
-  __shared__ int skip_s;
-  __shared__ float step_size_s, bc2s_s;
-  if (threadIdx.x == 0) {
-    double ss = 0.0;
-    for (int i = 0; i < a.nparts; ++i) ss += a.partials[i];
-    const float total = (float)sqrt(ss);
-    float coef = a.max_norm / (total + 1e-6f);
-    coef = coef < 1.f ? coef : 1.f;  // clamp(max=1): a NaN norm propagates like torch
-    if (!(total == total)) coef = total;
-    coef_s = coef;
-    skip_s = (a.loss && !isfinite(*a.loss)) ? 1 : 0;
-    const int t = *a.step + 1;
-    const double bc1 = 1.0 - pow((double)a.b1, (double)t);
-    const double bc2 = 1.0 - pow((double)a.b2, (double)t);
-    step_size_s = (float)((double)a.lr / bc1);
-    bc2s_s = (float)sqrt(bc2);
-    if (blockIdx.x == 0 && a.norm_out) *a.norm_out = total;
-  }
+// clip coefficient, non-finite skip and bias corrections, once per step (one block):
+// total = ||g||_2 from the sum-of-squares partials folded in a fixed order.
+__global__ __launch_bounds__(256) void adam_prologue(const double* partials, int nparts,
+                                                     const float* loss, const int* step, float lr,
+                                                     float b1, float b2, float max_norm,
+                                                     float* hyp, float* norm_out) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) a += partials[i];
+  red[threadIdx.x] = a;
   __syncthreads();
-  if (skip_s) return;
-  const float coef = coef_s, step_size = step_size_s, bc2s = bc2s_s;
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const float total = (float)sqrt(red[0]);
+  float coef = max_norm / (total + 1e-6f);
+  coef = coef < 1.f ? coef : 1.f;  // clamp(max=1)
+  if (!(total == total)) coef = total;  // a NaN norm propagates as in torch
+  const int t = *step + 1;
+  const double bc1 = 1.0 - pow((double)b1, (double)t);
+  const double bc2 = 1.0 - pow((double)b2, (double)t);
+  hyp[0] = coef;
+  hyp[1] = (loss && !isfinite(*loss)) ? 1.f : 0.f;
+  hyp[2] = (float)((double)lr / bc1);
+  hyp[3] = (float)sqrt(bc2);
+  if (norm_out) *norm_out = total;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  if (a.hyp[1] != 0.f) return;  // check_gradients: non-finite loss -> skip the update
+  const float coef = a.hyp[0], step_size = a.hyp[2], bc2s = a.hyp[3];
   const float w1 = 1.f - a.b1, w2 = 1.f - a.b2;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (size_t)gridDim.x * 256) {
-    const float g = a.g[i] * coef;
-    float m = a.m[i], v = a.v[i];
-    m = m + w1 * (g - m);                  // exp_avg.lerp_(grad, 1-beta1)
-    v = v * a.b2 + w2 * g * g;             // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
-    const float denom = sqrtf(v) / bc2s + a.eps;
-    a.p[i] = a.p[i] + (-step_size) * (m / denom);  // addcdiv_(exp_avg, denom, -step_size)
-    a.m[i] = m;
-    a.v[i] = v;
+  const size_t n4 = a.n / 4;
+  f32x4* p4 = reinterpret_cast<f32x4*>(a.p);
+  f32x4* m4 = reinterpret_cast<f32x4*>(a.m);
+  f32x4* v4 = reinterpret_cast<f32x4*>(a.v);
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(a.g);
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 g = g4[i] * coef, m = m4[i], v = v4[i], p = p4[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m[e] = m[e] + w1 * (g[e] - m[e]);               // exp_avg.lerp_(grad, 1-beta1)
+      v[e] = v[e] * a.b2 + w2 * g[e] * g[e];          // mul_(beta2).addcmul_(g, g, 1-beta2)
+      const float denom = sqrtf(v[e]) / bc2s + a.eps;
+      p[e] = p[e] + (-step_size) * (m[e] / denom);    // addcdiv_(exp_avg, denom, -step_size)
+    }
+    p4[i] = p; m4[i] = m; v4[i] = v;
+  }
+  if (blockIdx.x == 0) {
+    for (size_t i = n4 * 4 + threadIdx.x; i < a.n; i += 256) {
+      const float g = a.g[i] * coef;
+      float m = a.m[i], v = a.v[i];
+      m = m + w1 * (g - m);
+      v = v * a.b2 + w2 * g * g;
+      a.p[i] = a.p[i] + (-step_size) * (m / (sqrtf(v) / bc2s + a.eps));
+      a.m[i] = m; a.v[i] = v;
+    }
   }
 }
 
@@ -84,15 +107,34 @@ __global__ void step_counter_kernel(const float* loss, int* step, int* nonfinite
 }
 
 // ---------------------------------------------------------------- column sums
-// partial[r][c] = sum over rows [r*rows_per, ...) of in[row][c]; then out[c] = sum_r partial[r][c]
+// Block = 64 columns x a chunk of rows; 256 threads = 16 column quads x 16 row lanes, float4
+// loads, fixed-order LDS fold -> part[chunk][c]; colsum_final folds the chunks in order.
 __global__ __launch_bounds__(256) void colsum_partial(int N, int C, const float* __restrict__ in,
-                                                      int ld, int rows_per, float* __restrict__ part) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+                                                      int ld, int rows_per, int vec,
+                                                      float* __restrict__ part) {
+  __shared__ f32x4 red[16][16];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cq * 4;
   const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += in[(size_t)r * ld + c];
-  part[(size_t)blockIdx.y * C + c] = s;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    if (vec && c + 3 < C) {
+      for (int r = r0 + rl; r < r1; r += 16) acc += *reinterpret_cast<const f32x4*>(in + (size_t)r * ld + c);
+    } else {
+      for (int r = r0 + rl; r < r1; r += 16)
+        for (int e = 0; e < 4; ++e)
+          if (c + e < C) acc[e] += in[(size_t)r * ld + c + e];
+    }
+  }
+  red[rl][cq] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int q = threadIdx.x >> 2, e = threadIdx.x & 3;
+    float s = 0.f;
+    for (int i = 0; i < 16; ++i) s += red[i][q][e];
+    const int cc = blockIdx.x * 64 + threadIdx.x;
+    if (cc < C) part[(size_t)blockIdx.y * C + cc] = s;
+  }
 }
 __global__ __launch_bounds__(256) void colsum_final(int C, int R, const float* __restrict__ part,
                                                     float* __restrict__ out, float* __restrict__ out2,
@@ -100,9 +142,20 @@ __global__ __launch_bounds__(256) void colsum_final(int C, int R, const float* _
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
+#pragma unroll 8
   for (int r = 0; r < R; ++r) s += part[(size_t)r * C + c];
   out[c] = beta != 0.f ? beta * out[c] + s : s;
   if (out2) out2[c] = out[c];
+}
+
+static int colsum_chunks(int N, int C) {
+  const int cb = (C + 63) / 64;
+  int R = (1024 + cb - 1) / cb;
+  const int rmax = (N + 63) / 64;  // >= 64 rows per chunk
+  if (R > rmax) R = rmax;
+  if (R > 256) R = 256;
+  if (R < 1) R = 1;
+  return R;
 }
 
 // ---------------------------------------------------------------- dropout
@@ -157,38 +210,42 @@ extern "C" int mlvae_grad_sumsq(const float* g, size_t n, double* partials, void
   return 0;
 }
 
+// hyp: device scratch of >= 4 floats (clip coef, skip flag, step size, sqrt(bias corr 2))
 extern "C" int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
                                size_t n, const double* partials, int nparts, const float* loss,
                                int* step, int* nonfinite, float lr, float beta1, float beta2,
-                               float eps, float max_norm, float* norm_out, void* stream) {
-  AdamArgs a;
-  a.p = params; a.m = exp_avg; a.v = exp_avg_sq; a.g = grads; a.n = n; a.partials = partials;
-  a.nparts = nparts; a.loss = loss; a.step = step; a.lr = lr; a.b1 = beta1; a.b2 = beta2;
-  a.eps = eps; a.max_norm = max_norm; a.norm_out = norm_out;
+                               float eps, float max_norm, float* norm_out, float* hyp,
+                               void* stream) {
+  if (!hyp || (((uintptr_t)params | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq | (uintptr_t)grads) & 15)) {
+    mlvae_set_error("adam_step: needs hyp scratch and 16-byte aligned buffers");
+    return 1;
+  }
   hipStream_t s = (hipStream_t)stream;
-  adam_kernel<<<grid_for(n, 2048), 256, 0, s>>>(a);
+  adam_prologue<<<1, 256, 0, s>>>(partials, nparts, loss, step, lr, beta1, beta2, max_norm, hyp,
+                                  norm_out);
+  AdamArgs a;
+  a.p = params; a.m = exp_avg; a.v = exp_avg_sq; a.g = grads; a.n = n; a.hyp = hyp;
+  a.b1 = beta1; a.b2 = beta2; a.eps = eps;
+  adam_kernel<<<grid_for(n / 4 + 1, 2048), 256, 0, s>>>(a);
   step_counter_kernel<<<1, 64, 0, s>>>(loss, step, nonfinite);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" size_t mlvae_colsum_workspace_size(int N, int C) {
-  int R = (N + 255) / 256;
-  if (R > 64) R = 64;
-  return (size_t)R * C * sizeof(float);
+  return (size_t)colsum_chunks(N, C) * C * sizeof(float);
 }
 
 // out[c] (+= if beta) = sum_n in[n][c]; out2 (optional) receives a copy (b_ih / b_hh pairs)
 extern "C" int mlvae_colsum(int N, int C, const float* in, int ld, float* out, float* out2,
                             float beta, float* ws, size_t ws_bytes, void* stream) {
   if (C == 0) return 0;
-  int R = (N + 255) / 256;
-  if (R > 64) R = 64;
-  if (R < 1) R = 1;
+  const int R = colsum_chunks(N, C);
   if (!ws || ws_bytes < (size_t)R * C * sizeof(float)) { mlvae_set_error("colsum: workspace too small"); return 1; }
   const int rows_per = (N + R - 1) / R;
+  const int vec = (((uintptr_t)in & 15) == 0) && (ld % 4 == 0);
   hipStream_t s = (hipStream_t)stream;
-  colsum_partial<<<dim3((C + 255) / 256, R), 256, 0, s>>>(N, C, in, ld, rows_per, ws);
+  colsum_partial<<<dim3((C + 63) / 64, R), 256, 0, s>>>(N, C, in, ld, rows_per, vec, ws);
   colsum_final<<<(C + 255) / 256, 256, 0, s>>>(C, R, ws, out, out2, beta);
   MLVAE_CHECK_LAUNCH();
   return 0;

@@ -23,9 +23,9 @@ _SIGS = {
     "mlvae_device_check": [C.c_char_p, I],
     "mlvae_gemm_workspace_size": [I, I, I],
     "mlvae_gemm": [I, I, I, I, I, I, F, P, I, P, I, F, P, I, P, P, I, P, I, I, I, P, SZ, P],
-    "mlvae_lstm_workspace_size": [I, I, I, C.POINTER(SZ), C.POINTER(SZ)],
-    "mlvae_lstm_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, SZ, P, P],
-    "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, SZ, P, P],
+    "mlvae_lstm_workspace_size": [I, I, I, C.POINTER(SZ)],
+    "mlvae_lstm_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_elbo_partials_count": [I, I, I],
     "mlvae_reparam_kl_fwd": [I, I, I, P, I, P, P, P, P, P, P],
     "mlvae_reparam_kl_bwd": [I, I, I, P, I, P, P, P, P, P, F, P, I, P],
@@ -36,10 +36,12 @@ _SIGS = {
     "mlvae_randn": [SZ, U64, U64, P, P],
     "mlvae_sumsq_partials_count": [SZ],
     "mlvae_grad_sumsq": [P, SZ, P, P],
-    "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P],
+    "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P, P],
     "mlvae_colsum_workspace_size": [I, I],
     "mlvae_colsum": [I, I, P, I, P, P, F, P, SZ, P],
     "mlvae_dropout": [SZ, P, P, P, U64, F, P],
+    "mlvae_lstm_set_debug": [P],
+    "mlvae_lstm_set_debug_mode": [I],
 }
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,

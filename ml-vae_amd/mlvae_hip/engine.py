@@ -181,12 +181,11 @@ class _Work:
         ws = max(l.mlvae_gemm_workspace_size(m, n, k) for m, n, k in shapes)
         cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
         self.gws = torch.empty(max(ws, cs, 16) // 4 + 1, **f)
+        self.gws_side = torch.empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
         self.gws_bytes = self.gws.numel() * 4
-        xb, fb = _lib.SZ(), _lib.SZ()
-        check(l.mlvae_lstm_workspace_size(B, H, PREC[cfg.prec], _lib.C.byref(xb), _lib.C.byref(fb)),
-              "lstm_workspace_size")
+        xb = _lib.SZ()
+        check(l.mlvae_lstm_workspace_size(B, H, PREC[cfg.prec], _lib.C.byref(xb)), "lstm_workspace_size")
         self.xbuf = torch.empty(max(xb.value, 16), device=device, dtype=torch.uint8)
-        self.flags = torch.zeros(max(fb.value, 16) // 4, device=device, dtype=torch.int32)
         self.err = torch.zeros(1, device=device, dtype=torch.int32)
 
 
@@ -213,11 +212,15 @@ class VAEEngine:
         self.step_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.nonfinite_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.grad_norm = torch.zeros(1, **f)
+        self.hyp = torch.zeros(4, **f)
         self.nparts = lib().mlvae_sumsq_partials_count(n)
         self.sq_parts = torch.zeros(self.nparts, device=self.device, dtype=torch.float64)
         self.seed = seed
         self.rng_step = 0
         self._work = {}
+        self.overlap = True         # weight-gradient GEMMs on a side stream
+        self.side_stream = torch.cuda.Stream(self.device)
+        self._on_side = False
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
         self.global_offset = 0      # first global utterance index of this shard
@@ -252,17 +255,41 @@ class VAEEngine:
 
     # ------------------------------------------------------------------ launch helpers
     def _stream(self):
+        if self._on_side:
+            return self.side_stream.cuda_stream
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def _gemm(self, w, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, bias1=None, bias2=None, epi=0,
               aux=None, ldaux=0, kshift_T=0, kshift=0, beta=0.0):
+        ws = w.gws_side if self._on_side else w.gws
         check(lib().mlvae_gemm(PREC[self.cfg.prec], ta, tb, M, N, K, 1.0, A, lda, B, ldb, beta, C,
                                ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift,
-                               _p(w.gws), w.gws_bytes, self._stream()), "mlvae_gemm")
+                               _p(ws), w.gws_bytes, self._stream()), "mlvae_gemm")
 
     def _colsum(self, w, N, Cn, src, ld, out, out2=None):
-        check(lib().mlvae_colsum(N, Cn, src, ld, out, out2, 0.0, _p(w.gws), w.gws_bytes,
+        ws = w.gws_side if self._on_side else w.gws
+        check(lib().mlvae_colsum(N, Cn, src, ld, out, out2, 0.0, _p(ws), w.gws_bytes,
                                  self._stream()), "mlvae_colsum")
+
+    def _side(self, fn):
+        """Run fn's launches on the side stream once everything queued so far on the main
+        stream is done (weight gradients overlap the next BPTT recurrence)."""
+        if not self.overlap:
+            return fn()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.side_stream.wait_event(ev)
+        self._on_side = True
+        try:
+            fn()
+        finally:
+            self._on_side = False
+
+    def _join_side(self):
+        if self.overlap:
+            ev = torch.cuda.Event()
+            ev.record(self.side_stream)
+            torch.cuda.current_stream(self.device).wait_event(ev)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, lens, eps=None, train=False, dropout_masks=None, need_grad_inputs=False):
@@ -311,7 +338,7 @@ class VAEEngine:
             check(l.mlvae_lstm_fwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                    self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
                                    _p(w.Cs[li]), _p(w.Y[li]), _p(w.xbuf), w.xbuf.numel(),
-                                   _p(w.flags), w.flags.numel() * 4, _p(w.err), s), "lstm_fwd")
+                                   _p(w.err), s), "lstm_fwd")
             xin, din = w.Y[li], 2 * H
             if li < cfg.L - 1 and train and cfg.dropout > 0:
                 xin = w.Yd[li]
@@ -373,28 +400,37 @@ class VAEEngine:
         gp = lambda name: self._ptr(name, g)
         mse = cfg.loss_type == "mse"
         count = _p(w.count) if self.world > 1 else None
-        # ---- heads tail
+        # ---- heads tail: dgrad chain on the main stream, wgrads on the side stream
         heads = [("mean_fc", w.P2m, w.dMUX, w.dP2m, 0)]
         if not mse:
             heads.append(("log_var_fc", w.P2v, w.dLVX, w.dP2v, C))
         for hd, P2, dOut, dP2, off in heads:
             W3, W2 = self._ptr(f"decoder.{hd}.blocks.4.weight"), self._ptr(f"decoder.{hd}.blocks.2.weight")
+
+            def wg3(hd=hd, dOut=dOut, P2=P2):
+                self._gemm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
+                self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
+            self._side(wg3)
             self._gemm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C, epi=EPI_DLRELU,
                        aux=_p(P2), ldaux=C)
-            self._gemm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
-            self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
+
+            def wg2(hd=hd, dP2=dP2, off=off):
+                self._gemm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
+                           gp(f"decoder.{hd}.blocks.2.weight"), C)
+                self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
+            self._side(wg2)
             self._gemm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C, epi=EPI_DLRELU,
                        aux=_p(w.P1, off), ldaux=2 * C)
-            self._gemm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
-                       gp(f"decoder.{hd}.blocks.2.weight"), C)
-            self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
         K1 = C if mse else 2 * C  # mse: the log_var head gets no gradient (torch: grad None)
         R = _p(w.rnn_out)
+
+        def wg1():
+            self._gemm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
+                       gp("decoder.mean_fc.blocks.0.weight"), 2 * H)
+            self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
+        self._side(wg1)
         self._gemm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
                    2 * H, _p(w.dY[cfg.L - 1]), 2 * H)
-        self._gemm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
-                   gp("decoder.mean_fc.blocks.0.weight"), 2 * H)
-        self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
         # ---- BiLSTM layers, top to bottom
         for li in range(cfg.L - 1, -1, -1):
             xin, din = w.layer_in[li]
@@ -402,18 +438,21 @@ class VAEEngine:
             check(l.mlvae_lstm_bwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                    self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
                                    _p(w.Cs[li]), _p(w.dY[li]), _p(w.xbuf), w.xbuf.numel(),
-                                   _p(w.flags), w.flags.numel() * 4, _p(w.err), s), "lstm_bwd")
+                                   _p(w.err), s), "lstm_bwd")
+
+            def wgl(li=li, Gl=Gl, xin=xin, din=din):
+                self._gemm(w, 1, 0, 8 * H, din, N, _p(Gl), 8 * H, _p(xin), din,
+                           gp(f"decoder.rnn.weight_ih_l{li}"), din)
+                self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl), 8 * H, _p(w.Y[li]), 2 * H,
+                           gp(f"decoder.rnn.weight_hh_l{li}"), H, kshift_T=T, kshift=-1)
+                self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
+                           gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, kshift_T=T, kshift=1)
+                self._colsum(w, N, 8 * H, _p(Gl), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
+                             gp(f"decoder.rnn.bias_hh_l{li}"))
+            self._side(wgl)
             dx = w.dZs if li == 0 else w.dY[li - 1]
             self._gemm(w, 0, 0, N, din, 8 * H, _p(Gl), 8 * H,
                        self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din)
-            self._gemm(w, 1, 0, 8 * H, din, N, _p(Gl), 8 * H, _p(xin), din,
-                       gp(f"decoder.rnn.weight_ih_l{li}"), din)
-            self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl), 8 * H, _p(w.Y[li]), 2 * H,
-                       gp(f"decoder.rnn.weight_hh_l{li}"), H, kshift_T=T, kshift=-1)
-            self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
-                       gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, kshift_T=T, kshift=1)
-            self._colsum(w, N, 8 * H, _p(Gl), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
-                         gp(f"decoder.rnn.bias_hh_l{li}"))
             if li > 0 and xin is not w.Y[li - 1]:  # dropout between layers li-1 and li
                 seed, mask_ptr = w._drop_seed[li - 1]
                 check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
@@ -422,16 +461,23 @@ class VAEEngine:
         w_kl, _ = self.loss_weights()
         check(l.mlvae_reparam_kl_bwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(w.lens), count,
                                      _p(w.dZs), None, w_kl, _p(w.dML), 2 * Z, s), "reparam_kl_bwd")
+
+        def wge2():
+            self._gemm(w, 1, 0, 2 * Z, E, N, _p(w.dML), 2 * Z, _p(w.E2), E, gp("encoder.mean_fc.weight"), E)
+            self._colsum(w, N, 2 * Z, _p(w.dML), 2 * Z, gp("encoder.mean_fc.bias"))
+        self._side(wge2)
         self._gemm(w, 0, 0, N, E, 2 * Z, _p(w.dML), 2 * Z, self._ptr("encoder.mean_fc.weight"), E,
                    _p(w.dE2), E, epi=EPI_DLRELU, aux=_p(w.E2), ldaux=E)
-        self._gemm(w, 1, 0, 2 * Z, E, N, _p(w.dML), 2 * Z, _p(w.E2), E, gp("encoder.mean_fc.weight"), E)
-        self._colsum(w, N, 2 * Z, _p(w.dML), 2 * Z, gp("encoder.mean_fc.bias"))
+
+        def wge1():
+            self._gemm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp("encoder.fc.0.blocks.2.weight"), E)
+            self._colsum(w, N, E, _p(w.dE2), E, gp("encoder.fc.0.blocks.2.bias"))
+        self._side(wge1)
         self._gemm(w, 0, 0, N, E, E, _p(w.dE2), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
                    _p(w.dE1), E, epi=EPI_DLRELU, aux=_p(w.E1), ldaux=E)
-        self._gemm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp("encoder.fc.0.blocks.2.weight"), E)
-        self._colsum(w, N, E, _p(w.dE2), E, gp("encoder.fc.0.blocks.2.bias"))
         self._gemm(w, 1, 0, E, Fd, N, _p(w.dE1), E, _p(w.x), Fd, gp("encoder.fc.0.blocks.0.weight"), Fd)
         self._colsum(w, N, E, _p(w.dE1), E, gp("encoder.fc.0.blocks.0.bias"))
+        self._join_side()
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_step(self, w):
@@ -445,7 +491,7 @@ class VAEEngine:
                                 self.layout.total, self.sq_parts.data_ptr(), self.nparts,
                                 _p(w.loss, 2), self.step_ctr.data_ptr(), self.nonfinite_ctr.data_ptr(),
                                 cfg.lr, b1, b2, cfg.adam_eps, cfg.max_grad_norm,
-                                _p(self.grad_norm), s), "adam")
+                                _p(self.grad_norm), _p(self.hyp), s), "adam")
 
     def _allreduce_grads(self, w):
         import torch.distributed as dist

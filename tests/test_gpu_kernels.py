@@ -124,19 +124,18 @@ def test_lstm_layer_fwd_bwd(prec, tol, B, T, H, D):
     Y = torch.empty(N, 2 * H, device="cuda")
     W0, W1 = p["w_hh"].cuda(), p["w_hh_reverse"].cuda()
     import ctypes
-    xb, fb = ctypes.c_size_t(), ctypes.c_size_t()
-    check(lib().mlvae_lstm_workspace_size(B, H, prec, ctypes.byref(xb), ctypes.byref(fb)))
+    xb = ctypes.c_size_t()
+    check(lib().mlvae_lstm_workspace_size(B, H, prec, ctypes.byref(xb)))
     xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
-    flags = torch.zeros(fb.value // 4, device="cuda", dtype=torch.int32)
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
     check(lib().mlvae_lstm_fwd(prec, B, T, H, P(W0), P(W1), P(G), P(Cs), P(Y), P(xbuf), xb.value,
-                               P(flags), fb.value, P(err), stream()))
+                               P(err), stream()))
     torch.cuda.synchronize()
     assert err.item() == 0
     assert rel_err(Y.view(B, T, 2 * H), y) < tol
     dY = dy.float().reshape(N, 2 * H).cuda().contiguous()
     check(lib().mlvae_lstm_bwd(prec, B, T, H, P(W0), P(W1), P(G), P(Cs), P(dY), P(xbuf), xb.value,
-                               P(flags), fb.value, P(err), stream()))
+                               P(err), stream()))
     torch.cuda.synchronize()
     assert err.item() == 0
     assert rel_err(G.view(B, T, 8 * H), dG_ref) < tol * 5
