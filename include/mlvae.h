@@ -91,10 +91,24 @@ int mlvae_masked_mean(int B, int T, int C, const float* loss, const float* lens,
 /* check_gradients + Adam (ref:src/models/md_model.py:82-86, model.yaml:45-47). */
 int mlvae_sumsq_partials_count(size_t n);
 int mlvae_grad_sumsq(const float* grads, size_t n, double* partials, void* stream);
+/* advance: 1 = single-tensor step (prologue + update + step counter); for a multi-tensor
+ * step over several buffers call with 0 for the first, -1 (reuse the prologue's hyp) for the
+ * middle ones and 1 for the last (which advances the device step counter). */
 int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
                     size_t n, const double* partials, int nparts, const float* loss, int* step,
                     int* nonfinite, float lr, float beta1, float beta2, float eps,
-                    float max_norm, float* norm_out, float* hyp_scratch, void* stream);
+                    float max_norm, float* norm_out, float* hyp_scratch, int advance,
+                    void* stream);
+
+/* clip_grad_norm_ over several separately stored grads: every grad's sum-of-squares
+ * partials go to one buffer (offsets), then each grad is scaled by min(max/(total+1e-6),1). */
+int mlvae_clip_scale(float* grads, size_t n, const double* partials, int nparts, float max_norm,
+                     float* norm_out, void* stream);
+
+/* module-level autograd helpers: dx = dy * lrelu'(y); d apply_lens_to_loss / d loss */
+int mlvae_lrelu_bwd(size_t n, const float* dy, const float* y, float* dx, void* stream);
+int mlvae_masked_mean_bwd(int B, int T, int C, const float* lens, int reduction, const float* g,
+                          float* dloss, void* stream);
 
 /* bias gradients: out[c] = beta*out[c] + sum_n in[n][c]; out2 (optional) gets a copy. */
 size_t mlvae_colsum_workspace_size(int N, int C);

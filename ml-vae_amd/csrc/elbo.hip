@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void reparam_kl_bwd_kernel(
     const float* __restrict__ lens, const int* __restrict__ count, const float* __restrict__ dz,
     const float* __restrict__ dkl, float kl_scale, float* __restrict__ dml, int lddml) {
   __shared__ float inv_count;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && !dkl) {  // the mask normaliser is only needed without dkl
     const int c = count ? *count : total_frames(lens, B, T);
     inv_count = c > 0 ? 1.f / ((float)c * (float)Z) : 0.f;
   }
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void recon_kernel(
     float* __restrict__ dmux, float* __restrict__ dlvx) {
   __shared__ float sm[4];
   __shared__ float inv_count;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && dmux && !drec) {  // only the fused-gradient mode needs it
     const int c = count ? *count : total_frames(lens, B, T);
     inv_count = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
   }
@@ -312,6 +312,59 @@ extern "C" int mlvae_randn(size_t n, unsigned long long seed, unsigned long long
   size_t g = (n + 255) / 256;
   if (g > 2048) g = 2048;
   randn_kernel<<<(int)g, 256, 0, (hipStream_t)stream>>>(n, seed, offset, out);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- autograd helpers for the module-level (drop-in nn.Module) path -------------------------
+__global__ __launch_bounds__(256) void lrelu_bwd_kernel(size_t n, const float* __restrict__ dy,
+                                                        const float* __restrict__ y,
+                                                        float* __restrict__ dx) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dx[i] = dy[i] * lrelu_d(y[i]);
+}
+
+// d/dloss of apply_lens_to_loss: dloss[b,t,c] = g * mask / denom  (reduction mean/batchmean)
+// or g[b] * mask / (valid_b * C) (batch); g = upstream grad (1 or B floats, device)
+__global__ __launch_bounds__(256) void masked_mean_bwd_kernel(int B, int T, int C,
+                                                              const float* __restrict__ lens,
+                                                              int reduction,
+                                                              const float* __restrict__ g,
+                                                              float* __restrict__ dloss) {
+  __shared__ int cnt;
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int b = 0; b < B; ++b) c += valid_frames(lens[b], T);
+    cnt = c;
+  }
+  __syncthreads();
+  const size_t total = (size_t)B * T * C;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int b = (int)(i / ((size_t)T * C)), t = (int)((i / C) % T);
+    const int vf = valid_frames(lens[b], T);
+    float v = 0.f;
+    if (t < vf) {
+      if (reduction == 0) v = g[0] / ((float)cnt * C);
+      else if (reduction == 1) v = g[0] / (float)B;
+      else v = g[b] / ((float)vf * C);
+    }
+    dloss[i] = v;
+  }
+}
+
+extern "C" int mlvae_lrelu_bwd(size_t n, const float* dy, const float* y, float* dx, void* stream) {
+  if (n == 0) return 0;
+  lrelu_bwd_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(n, dy, y, dx);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_masked_mean_bwd(int B, int T, int C, const float* lens, int reduction,
+                                     const float* g, float* dloss, void* stream) {
+  if ((size_t)B * T * C == 0) return 0;
+  if (reduction < 0 || reduction > 2) { mlvae_set_error("masked_mean_bwd: bad reduction"); return 1; }
+  masked_mean_bwd_kernel<<<grid_for((size_t)B * T * C), 256, 0, (hipStream_t)stream>>>(
+      B, T, C, lens, reduction, g, dloss);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

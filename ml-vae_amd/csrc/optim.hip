@@ -106,6 +106,30 @@ __global__ void step_counter_kernel(const float* loss, int* step, int* nonfinite
   else *step += 1;
 }
 
+// clip_grad_norm_ for separately allocated grads: coef from all partials (fixed order), then
+// g *= min(max_norm / (total + 1e-6), 1) on this tensor.
+__global__ __launch_bounds__(256) void clip_scale_kernel(float* __restrict__ g, size_t n,
+                                                         const double* __restrict__ partials,
+                                                         int nparts, float max_norm,
+                                                         float* norm_out) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) a += partials[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float total = (float)sqrt(red[0]);
+  float coef = max_norm / (total + 1e-6f);
+  coef = coef < 1.f ? coef : 1.f;
+  if (!(total == total)) coef = total;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) *norm_out = total;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    g[i] *= coef;
+}
+
 // ---------------------------------------------------------------- column sums
 // Block = 64 columns x a chunk of rows; 256 threads = 16 column quads x 16 row lanes, float4
 // loads, fixed-order LDS fold -> part[chunk][c]; colsum_final folds the chunks in order.
@@ -215,19 +239,29 @@ extern "C" int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq,
                                size_t n, const double* partials, int nparts, const float* loss,
                                int* step, int* nonfinite, float lr, float beta1, float beta2,
                                float eps, float max_norm, float* norm_out, float* hyp,
-                               void* stream) {
+                               int advance, void* stream) {
   if (!hyp || (((uintptr_t)params | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq | (uintptr_t)grads) & 15)) {
     mlvae_set_error("adam_step: needs hyp scratch and 16-byte aligned buffers");
     return 1;
   }
   hipStream_t s = (hipStream_t)stream;
-  adam_prologue<<<1, 256, 0, s>>>(partials, nparts, loss, step, lr, beta1, beta2, max_norm, hyp,
-                                  norm_out);
+  if (advance >= 0)  // advance < 0: reuse hyp from an earlier call of this optimizer step
+    adam_prologue<<<1, 256, 0, s>>>(partials, nparts, loss, step, lr, beta1, beta2, max_norm, hyp,
+                                    norm_out);
   AdamArgs a;
   a.p = params; a.m = exp_avg; a.v = exp_avg_sq; a.g = grads; a.n = n; a.hyp = hyp;
   a.b1 = beta1; a.b2 = beta2; a.eps = eps;
   adam_kernel<<<grid_for(n / 4 + 1, 2048), 256, 0, s>>>(a);
-  step_counter_kernel<<<1, 64, 0, s>>>(loss, step, nonfinite);
+  if (advance > 0) step_counter_kernel<<<1, 64, 0, s>>>(loss, step, nonfinite);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_clip_scale(float* g, size_t n, const double* partials, int nparts,
+                                float max_norm, float* norm_out, void* stream) {
+  if (n == 0) return 0;
+  clip_scale_kernel<<<grid_for(n, 512), 256, 0, (hipStream_t)stream>>>(g, n, partials, nparts,
+                                                                       max_norm, norm_out);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

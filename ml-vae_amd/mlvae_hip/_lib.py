@@ -36,10 +36,13 @@ _SIGS = {
     "mlvae_randn": [SZ, U64, U64, P, P],
     "mlvae_sumsq_partials_count": [SZ],
     "mlvae_grad_sumsq": [P, SZ, P, P],
-    "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P, P],
+    "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P, I, P],
     "mlvae_colsum_workspace_size": [I, I],
     "mlvae_colsum": [I, I, P, I, P, P, F, P, SZ, P],
     "mlvae_dropout": [SZ, P, P, P, U64, F, P],
+    "mlvae_lrelu_bwd": [SZ, P, P, P, P],
+    "mlvae_clip_scale": [P, SZ, P, I, F, P, P],
+    "mlvae_masked_mean_bwd": [I, I, I, P, I, P, P, P],
     "mlvae_lstm_set_debug": [P],
     "mlvae_lstm_set_debug_mode": [I],
 }

@@ -1,0 +1,40 @@
+"""Data parallel on batch, one process per GPU (torch.distributed; backend "nccl" = RCCL on
+ROCm, gloo for CPU tests).  SURVEY.md 8(e):
+
+* every rank trains its own shard of the global batch with replicated weights;
+* the flat gradient buffer (8.70 M fp32 = 34.8 MB at c2) is summed with ONE all-reduce;
+* the masked-mean denominators use the all-reduced valid-frame count, so each rank's
+  gradient is its exact share of the global masked mean and the SUM over ranks equals the
+  single-GPU gradient of the global batch (no 1/world rescale, exact for unequal lengths);
+* the loss scalars ride along so every rank takes the same non-finite-skip decision and
+  clips with the same global norm;
+* eps is drawn from a counter-based stream indexed by the global utterance offset, so the
+  sampled noise is independent of the rank count.
+"""
+import torch
+import torch.distributed as dist
+
+
+def attach(engine, rank, world, batch_per_rank, group=None):
+    """Make a VAEEngine data-parallel: shard offset, process group, identical weights."""
+    engine.process_group = group
+    engine.world = world
+    engine.global_offset = rank * batch_per_rank
+    broadcast_params(engine.flat, group)
+    return engine
+
+
+def broadcast_params(flat, group=None):
+    dist.broadcast(flat, src=0, group=group)
+
+
+def allreduce_step(grad_flat, loss3, group=None):
+    """Sum the flat gradient buffer and the [kld, recon, total] loss shares over ranks."""
+    dist.all_reduce(grad_flat, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(loss3, op=dist.ReduceOp.SUM, group=group)
+
+
+def allreduce_count(count, group=None):
+    """Global number of valid frames (int tensor [1])."""
+    dist.all_reduce(count, op=dist.ReduceOp.SUM, group=group)
+    return count

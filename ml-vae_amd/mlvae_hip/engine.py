@@ -239,6 +239,32 @@ class VAEEngine:
     def named_grads(self):
         return OrderedDict((k, self.view(k, self.grad)) for k in self.layout.shapes)
 
+    @classmethod
+    def from_modules(cls, encoder, decoder, device="cuda", prec="fp32", kld_weight=1e-3,
+                     recon_weight=1.0, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                     max_grad_norm=5.0, seed=123456):
+        """Build an engine whose flat buffer becomes the storage of the given modules'
+        parameters (VanillaVAE + Decoder, as the recipe yaml builds them): after this call
+        module.parameters() are views of engine.flat and their .grad views of engine.grad."""
+        lin0 = encoder.fc[0].linear_plan()[0][0]
+        heads = decoder.mean_fc.linear_plan()
+        cfg = VAEConfig(F=lin0.in_features, E=lin0.out_features,
+                        Z=encoder.mean_fc.out_features, H=decoder.rnn.hidden_size,
+                        L=decoder.rnn.num_layers, C=heads[0][0].out_features,
+                        dropout=float(decoder.rnn.dropout), loss_type=decoder.loss_type,
+                        kld_weight=kld_weight, recon_weight=recon_weight, lr=lr, betas=tuple(betas),
+                        adam_eps=eps, max_grad_norm=max_grad_norm, prec=prec)
+        params = OrderedDict()
+        for pre, mod in (("encoder.", encoder), ("decoder.", decoder)):
+            for n, p in mod.named_parameters():
+                params[pre + n] = p.detach()
+        eng = cls(cfg, device=device, params=params, seed=seed)
+        for pre, mod in (("encoder.", encoder), ("decoder.", decoder)):
+            for n, p in mod.named_parameters():
+                p.data = eng.view(pre + n)
+                p.grad = eng.view(pre + n, eng.grad)
+        return eng
+
     def load_reference_params(self, params):
         with torch.no_grad():
             for k, v in params.items():
@@ -385,9 +411,9 @@ class VAEEngine:
         w.__dict__.setdefault("_drop_seed", {})[li] = (seed, mask_ptr)
 
     def _global_count(self, w):
-        import torch.distributed as dist
+        from . import dist as mdist
         check(lib().mlvae_count_frames(_p(w.lens), w.B, w.T, _p(w.count), self._stream()), "count")
-        dist.all_reduce(w.count, group=self.process_group)
+        mdist.allreduce_count(w.count, self.process_group)
         return _p(w.count)
 
     # ------------------------------------------------------------------ backward
@@ -491,12 +517,11 @@ class VAEEngine:
                                 self.layout.total, self.sq_parts.data_ptr(), self.nparts,
                                 _p(w.loss, 2), self.step_ctr.data_ptr(), self.nonfinite_ctr.data_ptr(),
                                 cfg.lr, b1, b2, cfg.adam_eps, cfg.max_grad_norm,
-                                _p(self.grad_norm), _p(self.hyp), s), "adam")
+                                _p(self.grad_norm), _p(self.hyp), 1, s), "adam")
 
     def _allreduce_grads(self, w):
-        import torch.distributed as dist
-        dist.all_reduce(self.grad, group=self.process_group)
-        dist.all_reduce(w.loss, group=self.process_group)
+        from . import dist as mdist
+        mdist.allreduce_step(self.grad, w.loss, self.process_group)
 
     def train_step(self, x, lens, eps=None, dropout_masks=None):
         """One fit_batch: forward, backward, clip + Adam.  Returns the device tensor

@@ -1,0 +1,364 @@
+"""torch.autograd.Functions over libmlvae.so: the operator layer under the drop-in
+nn.Modules (modules/fc_block.py, modules/vanilla_vae.py, modules/decoder.py).
+
+Every forward and backward below is a libmlvae.so launch on the current HIP stream; torch
+only allocates the output tensors.  Inputs must be fp32 CUDA tensors (row-major [B, T, C]).
+The fused training step (mlvae_hip/engine.py) uses the same kernels without autograd.
+"""
+import ctypes
+
+import torch
+
+from ._lib import SZ, check, lib
+
+PREC = {"fp32": 0, "bf16": 1}
+_state = {"prec": "fp32"}
+_ws = {}
+
+
+def set_precision(prec):
+    """Operand precision of the matrix products: "fp32" (exact f32 MFMA) or "bf16"."""
+    if prec not in PREC:
+        raise ValueError(f"precision must be one of {list(PREC)}")
+    _state["prec"] = prec
+
+
+def get_precision():
+    return _state["prec"]
+
+
+def _prec():
+    return PREC[_state["prec"]]
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t, off=0):
+    return t.data_ptr() + 4 * off
+
+
+def _need(t, name):
+    if not (t.is_cuda and t.dtype == torch.float32):
+        raise TypeError(f"{name}: expected a float32 HIP tensor, got {t.dtype} on {t.device} "
+                        "(the HIP path has no CPU fallback)")
+    return t.contiguous()
+
+
+def _workspace(nbytes, key="gemm"):
+    dev = torch.cuda.current_device()
+    w = _ws.get((dev, key))
+    if w is None or w.numel() * 4 < nbytes:
+        w = torch.empty(max(nbytes // 4 + 1, 1024), device="cuda", dtype=torch.float32)
+        _ws[(dev, key)] = w
+    return w
+
+
+def gemm(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, bias1=None, bias2=None, epi=0, aux=None,
+         ldaux=0, beta=0.0, kshift_T=0, kshift=0):
+    """C = epi(op(A) op(B) + bias1 + bias2 + beta*C) on raw device pointers (ints)."""
+    l = lib()
+    ws = _workspace(l.mlvae_gemm_workspace_size(M, N, K))
+    check(l.mlvae_gemm(_prec(), ta, tb, M, N, K, 1.0, A, lda, B, ldb, beta, C, ldc, bias1, bias2,
+                       epi, aux, ldaux, kshift_T, kshift, _p(ws), ws.numel() * 4, _stream()),
+          "mlvae_gemm")
+
+
+def colsum(N, Cn, src, ld, out, out2=None, beta=0.0):
+    l = lib()
+    ws = _workspace(l.mlvae_colsum_workspace_size(N, Cn), "colsum")
+    check(l.mlvae_colsum(N, Cn, src, ld, out, out2, beta, _p(ws), ws.numel() * 4, _stream()),
+          "mlvae_colsum")
+
+
+def _rows(x):
+    return x.numel() // x.shape[-1]
+
+
+# --------------------------------------------------------------------------- Linear (+LReLU)
+class LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b), act = LeakyReLU(0.01) or identity (ref:src/modules/fc_block.py:10-16)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x, w = _need(x, "linear x"), _need(w, "linear weight")
+        b = _need(b, "linear bias") if b is not None else None
+        M, K = _rows(x), x.shape[-1]
+        N = w.shape[0]
+        y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
+        gemm(0, 1, M, N, K, _p(x), K, _p(w), K, _p(y), N, bias1=_p(b) if b is not None else None,
+             epi=1 if act else 0)
+        ctx.save_for_backward(x, w, y)
+        ctx.act, ctx.has_b = act, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = _need(dy, "linear grad")
+        M, K, N = _rows(x), x.shape[-1], w.shape[0]
+        if ctx.act:  # dpre = dy * lrelu'(y)
+            dpre = torch.empty_like(dy)
+            check(lib().mlvae_lrelu_bwd(dy.numel(), _p(dy), _p(y), _p(dpre), _stream()), "lrelu_bwd")
+        else:
+            dpre = dy
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            gemm(0, 0, M, K, N, _p(dpre), N, _p(w), K, _p(dx), K)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            gemm(1, 0, N, K, M, _p(dpre), N, _p(x), K, _p(dw), K)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(N, device=dy.device, dtype=torch.float32)
+            colsum(M, N, _p(dpre), N, _p(db))
+        return dx, dw, db, None
+
+
+def linear(x, w, b=None, act=False):
+    return LinearFn.apply(x, w, b, act)
+
+
+# --------------------------------------------------------------------------- ELBO part 1
+class ReparamKLFn(torch.autograd.Function):
+    """z = eps*exp(lv/2) + mu and per-element KL (ref:src/modules/vanilla_vae.py:37-45);
+    ml = [mu | log_var] along the last dim."""
+
+    @staticmethod
+    def forward(ctx, ml, eps):
+        ml, eps = _need(ml, "ml"), _need(eps, "eps")
+        Z = ml.shape[-1] // 2
+        N = _rows(ml)
+        z = torch.empty(*ml.shape[:-1], Z, device=ml.device, dtype=torch.float32)
+        kl = torch.empty_like(z)
+        # rows are independent: pass them as B=N utterances of T=1 frame (mask all-valid)
+        ones = _ones(N)
+        check(lib().mlvae_reparam_kl_fwd(N, 1, Z, _p(ml), 2 * Z, _p(eps), _p(ones), _p(z), _p(kl),
+                                         None, _stream()), "reparam_kl_fwd")
+        ctx.save_for_backward(ml, eps)
+        return z, kl
+
+    @staticmethod
+    def backward(ctx, dz, dkl):
+        ml, eps = ctx.saved_tensors
+        Z = ml.shape[-1] // 2
+        N = _rows(ml)
+        dz = _need(dz, "dz") if dz is not None else torch.zeros(*ml.shape[:-1], Z, device=ml.device)
+        dkl = _need(dkl, "dkl") if dkl is not None else torch.zeros_like(dz)
+        dml = torch.empty_like(ml)
+        check(lib().mlvae_reparam_kl_bwd(N, 1, Z, _p(ml), 2 * Z, _p(eps), _p(_ones(N)), None,
+                                         _p(dz), _p(dkl), 0.0, _p(dml), 2 * Z, _stream()),
+              "reparam_kl_bwd")
+        return dml, None
+
+
+def _ones(n):
+    dev = torch.cuda.current_device()
+    o = _ws.get((dev, "ones"))
+    if o is None or o.numel() < n:
+        o = torch.ones(max(n, 1024), device="cuda", dtype=torch.float32)
+        _ws[(dev, "ones")] = o
+    return o
+
+
+def randn(shape, generator=None):
+    """N(0,1) from the library's Philox stream; the seed is drawn from torch's (CPU) RNG so
+    torch.manual_seed (ref:src/config/run.yaml:2-3) makes it reproducible."""
+    seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator).item())
+    out = torch.empty(*shape, device="cuda", dtype=torch.float32)
+    check(lib().mlvae_randn(out.numel(), seed, 0, _p(out), _stream()), "randn")
+    return out
+
+
+# --------------------------------------------------------------------------- ELBO part 2
+LOSS = {"likelihood": 0, "mse": 1}
+
+
+class ReconFn(torch.autograd.Function):
+    """Per-element reconstruction loss (ref:src/modules/decoder.py:37-53)."""
+
+    @staticmethod
+    def forward(ctx, mux, lvx, x, loss_type):
+        mux, x = _need(mux, "mean"), _need(x, "target")
+        lt = LOSS[loss_type]
+        lvx = _need(lvx, "log_var") if lt == 0 else mux
+        F = mux.shape[-1]
+        N = _rows(mux)
+        rec = torch.empty_like(mux)
+        check(lib().mlvae_recon(N, 1, F, lt, _p(mux), F, _p(lvx), F, _p(x), F, _p(_ones(N)), None,
+                                _p(rec), None, None, 0.0, None, None, _stream()), "recon")
+        ctx.save_for_backward(mux, lvx, x)
+        ctx.lt = lt
+        return rec
+
+    @staticmethod
+    def backward(ctx, drec):
+        mux, lvx, x = ctx.saved_tensors
+        drec = _need(drec, "recon grad")
+        F, N = mux.shape[-1], _rows(mux)
+        dmux = torch.empty_like(mux)
+        dlvx = torch.empty_like(mux) if ctx.lt == 0 else None
+        check(lib().mlvae_recon(N, 1, F, ctx.lt, _p(mux), F, _p(lvx), F, _p(x), F, _p(_ones(N)),
+                                None, None, None, _p(drec), 0.0, _p(dmux),
+                                _p(dlvx) if dlvx is not None else None, _stream()), "recon_bwd")
+        return dmux, dlvx, None, None
+
+
+def recon_loss(mean, log_var, target, loss_type):
+    if loss_type not in LOSS:
+        raise ValueError(f"Invalid loss type: {loss_type}")  # ref:src/modules/decoder.py:50-51
+    return ReconFn.apply(mean, log_var if loss_type == "likelihood" else mean, target, loss_type)
+
+
+# --------------------------------------------------------------------------- masked mean
+RED = {"mean": 0, "batchmean": 1, "batch": 2}
+
+
+class MaskedMeanFn(torch.autograd.Function):
+    """apply_lens_to_loss (ref:src/utils/data_utils.py:67-104)."""
+
+    @staticmethod
+    def forward(ctx, loss, lens, reduction):
+        loss = _need(loss, "loss")
+        lens = _need(lens.to(loss.device, torch.float32), "lens")
+        B, T = loss.shape[0], loss.shape[1]
+        C = loss.numel() // (B * T) if B * T else 1
+        out = torch.empty(2 * B if B else 2, device=loss.device, dtype=torch.float32)
+        check(lib().mlvae_masked_mean(B, T, C, _p(loss), _p(lens), RED[reduction], _p(out),
+                                      _stream()), "masked_mean")
+        ctx.save_for_backward(lens)
+        ctx.shape, ctx.red = loss.shape, RED[reduction]
+        return out[:B].clone() if reduction == "batch" else out[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        (lens,) = ctx.saved_tensors
+        B, T = ctx.shape[0], ctx.shape[1]
+        C = 1
+        for d in ctx.shape[2:]:
+            C *= d
+        g = _need(g.reshape(-1), "grad")
+        dloss = torch.empty(ctx.shape, device=g.device, dtype=torch.float32)
+        check(lib().mlvae_masked_mean_bwd(B, T, C, _p(lens), ctx.red, _p(g), _p(dloss), _stream()),
+              "masked_mean_bwd")
+        return dloss, None, None
+
+
+def masked_mean(loss, lens, reduction="mean"):
+    if reduction not in RED:
+        raise ValueError(f"unknown reduction {reduction}")
+    return MaskedMeanFn.apply(loss, lens, reduction)
+
+
+# --------------------------------------------------------------------------- BiLSTM
+def _lstm_ws(B, H):
+    xb = SZ()
+    check(lib().mlvae_lstm_workspace_size(B, H, _prec(), ctypes.byref(xb)), "lstm_workspace_size")
+    x = _workspace(xb.value, "lstm_x")
+    err = _ws.get((torch.cuda.current_device(), "lstm_err"))
+    if err is None:
+        err = torch.zeros(1, device="cuda", dtype=torch.int32)
+        _ws[(torch.cuda.current_device(), "lstm_err")] = err
+    return x, err
+
+
+def _dropout(src, dst, seed, p):
+    check(lib().mlvae_dropout(src.numel(), _p(src), _p(dst), None, seed, p, _stream()), "dropout")
+
+
+class BiLSTMFn(torch.autograd.Function):
+    """nn.LSTM(bidirectional=True, batch_first=True) on libmlvae (ref:src/modules/decoder.py:14-15,22):
+    per layer an input-projection GEMM per direction + the persistent recurrence; inter-layer
+    dropout (Philox, recomputed in backward) in train mode.  weights = the layer-major list
+    [w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r] * L."""
+
+    @staticmethod
+    def forward(ctx, x, H, L, dropout, seed, *weights):
+        x = _need(x, "lstm input")
+        B, T, _ = x.shape
+        N = B * T
+        l = lib()
+        xbuf, err = _lstm_ws(B, H)
+        saved, inputs, seeds = [], [], []
+        h = x
+        for li in range(L):
+            w = [_need(t, "lstm weight") for t in weights[8 * li:8 * li + 8]]
+            din = h.shape[-1]
+            G = torch.empty(N, 8 * H, device=x.device, dtype=torch.float32)
+            for d in range(2):
+                wi, _, bi, bh = w[4 * d:4 * d + 4]
+                gemm(0, 1, N, 4 * H, din, _p(h), din, _p(wi), din, _p(G, 4 * H * d), 8 * H,
+                     bias1=_p(bi), bias2=_p(bh))
+            Cs = torch.empty(N, 2 * H, device=x.device, dtype=torch.float32)
+            Y = torch.empty(B, T, 2 * H, device=x.device, dtype=torch.float32)
+            check(l.mlvae_lstm_fwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(Y),
+                                   _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_fwd")
+            inputs.append(h)
+            saved += [G, Cs, Y]
+            h = Y
+            if li < L - 1 and dropout > 0:
+                s = (seed * 1000003 + li) & ((1 << 63) - 1)
+                hd = torch.empty_like(Y)
+                _dropout(Y, hd, s, dropout)
+                seeds.append(s)
+                h = hd
+            else:
+                seeds.append(None)
+        ctx.save_for_backward(*inputs, *saved, *weights)
+        ctx.H, ctx.L, ctx.dropout, ctx.seeds = H, L, dropout, seeds
+        return h
+
+    @staticmethod
+    def backward(ctx, dy):
+        H, L = ctx.H, ctx.L
+        t = ctx.saved_tensors
+        inputs, saved, weights = t[:L], t[L:4 * L], t[4 * L:]
+        dy = _need(dy, "lstm grad").clone()
+        B, T = dy.shape[0], dy.shape[1]
+        N = B * T
+        l = lib()
+        xbuf, err = _lstm_ws(B, H)
+        dW = [None] * len(weights)
+        dx = None
+        for li in range(L - 1, -1, -1):
+            G, Cs, Y = saved[3 * li:3 * li + 3]
+            w = weights[8 * li:8 * li + 8]
+            xin = inputs[li]
+            din = xin.shape[-1]
+            check(l.mlvae_lstm_bwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(dy),
+                                   _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_bwd")
+            dx = torch.empty(B, T, din, device=dy.device, dtype=torch.float32)
+            for d in range(2):
+                wi = w[4 * d]
+                gemm(0, 0, N, din, 4 * H, _p(G, 4 * H * d), 8 * H, _p(wi), din, _p(dx), din,
+                     beta=1.0 if d else 0.0)
+                gwi = torch.empty_like(wi)
+                gemm(1, 0, 4 * H, din, N, _p(G, 4 * H * d), 8 * H, _p(xin), din, _p(gwi), din)
+                gwh = torch.empty_like(w[4 * d + 1])
+                gemm(1, 0, 4 * H, H, N, _p(G, 4 * H * d), 8 * H, _p(Y, H * d), 2 * H, _p(gwh), H,
+                     kshift_T=T, kshift=1 if d else -1)
+                gbi = torch.empty_like(w[4 * d + 2])
+                gbh = torch.empty_like(w[4 * d + 3])
+                colsum(N, 4 * H, _p(G, 4 * H * d), 8 * H, _p(gbi), _p(gbh))
+                base = 8 * li + 4 * d
+                dW[base:base + 4] = [gwi, gwh, gbi, gbh]
+            if li > 0 and ctx.seeds[li - 1] is not None:
+                _dropout(dx, dx, ctx.seeds[li - 1], ctx.dropout)
+            dy = dx
+        if int(err.item()) != 0:
+            raise RuntimeError("LSTM recurrence hand-off timed out")
+        return (dx, None, None, None, None, *dW)
+
+
+def bilstm(x, lstm_module, train):
+    """Run an nn.LSTM's parameters through the HIP recurrence (its own forward is not used)."""
+    H, L = lstm_module.hidden_size, lstm_module.num_layers
+    weights = []
+    for li in range(L):
+        for sfx in ("", "_reverse"):
+            for kind in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+                weights.append(getattr(lstm_module, f"{kind}_l{li}{sfx}"))
+    p = float(lstm_module.dropout) if train else 0.0
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+    return BiLSTMFn.apply(x, H, L, p, seed, *weights)
