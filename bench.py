@@ -3,10 +3,16 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--prec bf16|fp32] [--config c2]
 
 N=1 workload = BASELINE.json configs[1]: full ML-VAE enc/dec on 80-d log-mel, T=500, B=32
-per GPU, dropout 0.15 (train mode), Adam + clip 5.0 -- one step = one full fit_batch.
-For N>1 (launched by torch.distributed.run) every rank trains its own B=32 shard of the
-global batch (weak scaling; c3 = 8 x 32 = 256) and gradients are all-reduced over RCCL.
-Rank 0 prints ONE JSON line.
+per GPU, train mode (dropout 0.15), Adam + clip 5.0 -- one step = one full fit_batch of the
+fused HIP path.  For N>1 (torch.distributed.run) every rank trains its own B=32 shard
+(weak scaling; N=8 is configs[2]: global B=256) and the gradients are all-reduced over RCCL.
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+  roofline      the dominant kernel (the persistent BiLSTM BPTT recurrence), timed with HIP
+                events on its stream during the timed region; algorithmic bytes per launch;
+                traffic from the committed rocprofv3 PMC run (profiles/), or null
+  cpu_baseline  the CPU oracle (oracle/vae_cpu.py, pinned to reference fixtures) timed on
+                this host's cores on a bounded sample of the same workload (rank 0, N=1)
 """
 import argparse
 import json
@@ -20,22 +26,73 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+METRIC = "spectrogram frames/sec + ELBO; 80-d log-mel B=256 at 1/2/4/8 MI355X"
 CONFIGS = {
     # name: (F, E, Z, H, L, C, B_per_gpu, T)
     "c1": (64, 128, 16, 128, 2, 128, 8, 200),
     "c2": (80, 64, 32, 512, 2, 64, 32, 500),
     "c4": (80, 64, 32, 512, 2, 64, 64, 2000),
 }
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 
 
 def macs_per_frame(F, E, Z, H, L, C):
     enc = E * F + E * E + 2 * Z * E
-    lstm = 0
-    for l in range(L):
-        din = Z if l == 0 else 2 * H
-        lstm += 2 * (4 * H * din + 4 * H * H)
+    lstm = sum(2 * (4 * H * (Z if l == 0 else 2 * H) + 4 * H * H) for l in range(L))
     heads = 2 * (C * 2 * H + C * C + F * C)
     return enc + lstm + heads
+
+
+def lstm_launch_bytes(B, T, H):
+    """Algorithmic HBM bytes of one recurrence launch (both directions), fp32 tensors:
+    fwd: read G [N,8H] + write gates [N,8H] + write c [N,2H] + write h [N,2H]
+    bwd: read gates [N,8H] + read c [N,2H] + read dY [N,2H] + write dG [N,8H]
+    (= 20H*4 bytes per frame either way)."""
+    return B * T * (8 * H + 8 * H + 2 * H + 2 * H) * 4
+
+
+def lstm_launch_flops(B, T, H):
+    """Recurrent MACs: per frame and direction 4H x H (h W_hh^T, or dG W_hh in BPTT)."""
+    return 2 * B * T * 2 * 4 * H * H
+
+
+def cpu_baseline(cfg_name, prec, budget_s=12.0):
+    """The CPU oracle (torch CPU, ATen LSTM as the reference calls it) on this host."""
+    from oracle import vae_cpu as O
+    F, E, Z, H, L, C, B, T = CONFIGS[cfg_name]
+    threads = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", threads))
+    torch.set_num_threads(max(1, min(threads, cap)))
+    g = torch.Generator().manual_seed(1)
+    params = O.init_params(F, E, Z, H, L, C, seed=123456)
+    x = torch.randn(B, T, F, generator=g)
+    lens = torch.ones(B)
+    cfg = dict(L=L, loss_type="likelihood", kld_weight=1e-3)
+    state, steps, t0 = {}, 0, time.perf_counter()
+    masks_shape = (L - 1, B, T, 2 * H)
+    while True:
+        eps = torch.randn(B, T, Z, generator=g)
+        masks = (torch.rand(masks_shape, generator=g) > 0.15).float() / 0.85 if L > 1 else None
+        params, _ = O.train_step(params, state, x, lens, eps, cfg, masks, impl="aten")
+        steps += 1
+        dt = time.perf_counter() - t0
+        if dt > budget_s or steps >= 20:
+            break
+    return {"value": steps * B * T / dt, "unit": "frames/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{steps} full {cfg_name} train steps (B={B}, T={T}, fp32, ATen LSTM, clip+Adam) "
+                      f"in {dt:.1f} s on {torch.get_num_threads()} host threads"}
+
+
+def pmc_traffic(kernel):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -59,14 +116,13 @@ def main():
     from mlvae_hip.engine import VAEConfig, VAEEngine
     F, E, Z, H, L, C, B, T = CONFIGS[args.config]
     cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=args.prec)
-    eng = VAEEngine(cfg)
-    from oracle import vae_cpu as O  # only for the reference-default initial weights
-    eng.load_reference_params(O.init_params(F, E, Z, H, L, C, seed=123456))
+    eng = VAEEngine(cfg, device=f"cuda:{local}")
+    eng.init_default(seed=123456)
     if world > 1:
         from mlvae_hip import dist as mdist
         mdist.attach(eng, rank=rank, world=world, batch_per_rank=B)
     g = torch.Generator(device="cuda").manual_seed(123456 + rank)
-    x = torch.randn(B, T, F, device="cuda", generator=g)
+    x = torch.randn(B, T, F, device="cuda", generator=g)   # synthetic normalised log-mel
     lens = torch.ones(B, device="cuda")
 
     def barrier():
@@ -79,24 +135,31 @@ def main():
         eng.train_step(x, lens)
     barrier()
     eng.check_errors()
+    eng.kernel_timers = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = eng.train_step(x, lens)
     barrier()
     dt = time.perf_counter() - t0
     eng.check_errors()
+    timers, eng.kernel_timers = eng.kernel_timers, None
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = tt.item()
     ms = dt / args.steps * 1e3
-    frames = B * T * world * args.steps
-    value = frames / dt
+    value = B * T * world * args.steps / dt
     lv = loss.tolist()
+    kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
     if rank == 0:
+        dom = "lstm_bwd"
+        dur_s = kern[dom] * 1e-3
+        nbytes = lstm_launch_bytes(B, T, H)
+        achieved = nbytes / dur_s / 1e9
+        traffic = pmc_traffic(dom)
         out = {
-            "metric": "spectrogram frames/sec (VAE train step) + ELBO",
+            "metric": METRIC,
             "value": value,
             "unit": "frames/s",
             "n_gpus": world,
@@ -107,13 +170,27 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.prec,
-            "data": "synthetic N(0,1) 80-d frames, lens=1, random-init weights",
-            "config": {"workload": f"{args.config}: ML-VAE enc {E}x2, z={Z}, BiLSTM {L}x{H}, "
-                                   f"dec-FC {C}, F={F}, T={T}, B={B}/GPU, Adam+clip5, dropout 0.15",
+            "data": "synthetic N(0,1) 80-d frames (normalised log-mel stand-in), lens=1, "
+                    "random-init weights (PyTorch default init, seed 123456)",
+            "config": {"workload": f"{args.config}: VanillaVAE enc [{F},{E},{E}] z={Z}, BiLSTM "
+                                   f"{L}x{H} (dropout 0.15), dec-FC [{2 * H},{C},{C},{F}], T={T}, "
+                                   f"B={B}/GPU, Gaussian-NLL ELBO, clip 5.0 + Adam 1e-3",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "elbo": {"kld_loss": lv[0], "recon_loss": lv[1], "loss": lv[2]},
             "train_tflops": value * 6 * macs_per_frame(F, E, Z, H, L, C) / 1e12,
+            "roofline": {"kernel": "lstm_bwd_kernel (persistent BiLSTM BPTT, both directions)",
+                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": nbytes,
+                         "avg_launch_ms": kern[dom], "launches": len(timers[dom]),
+                         "mfma_frac": lstm_launch_flops(B, T, H) / dur_s / 1e12 /
+                         MFMA_PEAK_TFLOPS[args.prec]},
+            "kernel_ms": kern,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.config, args.prec)
+        else:
+            out["cpu_baseline"] = None
         print(json.dumps(out))
     if world > 1:
         import torch.distributed as dist

@@ -63,6 +63,10 @@ def lib():
     """Load libmlvae.so (once).  Raises if it is absent: the HIP path has no fallback."""
     global _lib
     if _lib is None:
+        # torch first: its bundled libamdhip64.so.7 then satisfies libmlvae.so's dependency,
+        # so torch (allocations, streams) and the kernels share ONE HIP runtime; loading
+        # libmlvae.so first would map /opt/rocm's runtime as a second, incompatible copy.
+        import torch  # noqa: F401
         if not os.path.exists(LIB_PATH):
             raise MlvaeError(
                 f"{LIB_PATH} is missing: build it with `python -m mlvae_hip.build` "

@@ -17,6 +17,7 @@ ref:src/models/test_vanilla_vae/model.py:19-55):
 Every tensor is row-major [B*T, C]; the flat parameter buffer keeps pairs that a fused
 launch reads as one matrix adjacent (mean/log_var heads, both LSTM directions).
 """
+import math
 from collections import OrderedDict
 from dataclasses import dataclass, field
 
@@ -221,6 +222,7 @@ class VAEEngine:
         self.overlap = True         # weight-gradient GEMMs on a side stream
         self.side_stream = torch.cuda.Stream(self.device)
         self._on_side = False
+        self.kernel_timers = None   # {name: [(start_event, end_event), ...]} when profiling
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
         self.global_offset = 0      # first global utterance index of this shard
@@ -264,6 +266,23 @@ class VAEEngine:
                 p.data = eng.view(pre + n)
                 p.grad = eng.view(pre + n, eng.grad)
         return eng
+
+    def init_default(self, seed=None):
+        """PyTorch-default initialisation, drawn on the device: U(-1/sqrt(fan_in), +) for
+        Linear weights and biases (nn.Linear.reset_parameters) and U(-1/sqrt(H), +) for every
+        LSTM tensor (nn.LSTM.reset_parameters) -- the distributions the reference's modules
+        get from their constructors (ref:src/modules/fc_block.py, src/modules/decoder.py)."""
+        g = torch.Generator(device=self.device).manual_seed(self.seed if seed is None else seed)
+        with torch.no_grad():
+            for name, shp in self.layout.shapes.items():
+                if ".rnn." in name:
+                    bound = 1.0 / math.sqrt(self.cfg.H)
+                else:
+                    wshape = self.layout.shapes[name[:-4] + "weight"] if name.endswith("bias") else shp
+                    bound = 1.0 / math.sqrt(wshape[1])
+                v = self.view(name)
+                v.uniform_(-bound, bound, generator=g)
+        return self
 
     def load_reference_params(self, params):
         with torch.no_grad():
@@ -310,6 +329,23 @@ class VAEEngine:
             fn()
         finally:
             self._on_side = False
+
+    def _timed(self, name):
+        """HIP events around one launch on the main stream (bench.py's roofline timing)."""
+        eng = self
+
+        class _T:
+            def __enter__(self_):
+                if eng.kernel_timers is not None:
+                    self_.a = torch.cuda.Event(enable_timing=True)
+                    self_.a.record(torch.cuda.current_stream(eng.device))
+
+            def __exit__(self_, *exc):
+                if eng.kernel_timers is not None:
+                    b = torch.cuda.Event(enable_timing=True)
+                    b.record(torch.cuda.current_stream(eng.device))
+                    eng.kernel_timers.setdefault(name, []).append((self_.a, b))
+        return _T()
 
     def _join_side(self):
         if self.overlap:
@@ -361,10 +397,11 @@ class VAEEngine:
                        self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
                        bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
                        bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
-            check(l.mlvae_lstm_fwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                   self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                   _p(w.Cs[li]), _p(w.Y[li]), _p(w.xbuf), w.xbuf.numel(),
-                                   _p(w.err), s), "lstm_fwd")
+            with self._timed("lstm_fwd"):
+                check(l.mlvae_lstm_fwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                       self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                       _p(w.Cs[li]), _p(w.Y[li]), _p(w.xbuf), w.xbuf.numel(),
+                                       _p(w.err), s), "lstm_fwd")
             xin, din = w.Y[li], 2 * H
             if li < cfg.L - 1 and train and cfg.dropout > 0:
                 xin = w.Yd[li]
@@ -461,10 +498,11 @@ class VAEEngine:
         for li in range(cfg.L - 1, -1, -1):
             xin, din = w.layer_in[li]
             Gl = w.G[li]
-            check(l.mlvae_lstm_bwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                   self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                   _p(w.Cs[li]), _p(w.dY[li]), _p(w.xbuf), w.xbuf.numel(),
-                                   _p(w.err), s), "lstm_bwd")
+            with self._timed("lstm_bwd"):
+                check(l.mlvae_lstm_bwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                       self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
+                                       _p(w.Cs[li]), _p(w.dY[li]), _p(w.xbuf), w.xbuf.numel(),
+                                       _p(w.err), s), "lstm_bwd")
 
             def wgl(li=li, Gl=Gl, xin=xin, din=din):
                 self._gemm(w, 1, 0, 8 * H, din, N, _p(Gl), 8 * H, _p(xin), din,
