@@ -84,6 +84,12 @@ __device__ __forceinline__ int valid_frames(float rel_len, int T) {
   return c >= (float)T ? T : (int)c;
 }
 
+// DPP lane move of a float (row_mask = bank_mask = 0xf, bound_ctrl: out-of-row lanes read 0)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+
 // Wave-level sum (64 lanes) with a fixed butterfly order (deterministic).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -77,6 +77,9 @@ def lib():
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, I)
         _lib = h
+        mode = os.environ.get("MLVAE_LSTM_DEBUG_MODE")
+        if mode:  # diagnostics / A-B timing switches of the recurrence (lstm.hip)
+            h.mlvae_lstm_set_debug_mode(int(mode))
     return _lib
 
 

@@ -20,7 +20,7 @@ def main(prec=1, B=32, T=500, H=512, bwd=False):
     check(lib().mlvae_lstm_workspace_size(B, H, prec, ctypes.byref(xb)))
     xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
-    dbg = torch.zeros(T * 8, device="cuda", dtype=torch.int64)
+    dbg = torch.zeros(T * 16, device="cuda", dtype=torch.int64)
     s = torch.cuda.current_stream().cuda_stream
     lib().mlvae_lstm_set_debug_mode(int(os.environ.get("LSTM_DBG_MODE", "0")))
     for it in range(3):
@@ -40,7 +40,7 @@ def main(prec=1, B=32, T=500, H=512, bwd=False):
         torch.cuda.synchronize()
         print(f"{'bwd' if bwd else 'fwd'} launch {ev0.elapsed_time(ev1):.3f} ms ({ev0.elapsed_time(ev1) / T * 1e3:.2f} us/step)")
     lib().mlvae_lstm_set_debug(None)
-    d = dbg.view(T, 8).cpu().double()
+    d = dbg.view(T, 16).cpu().double()
     names = (["poll+load", "mfma", "barrier", "cell+publish"] if bwd else
              ["poll+load", "mfma", "reduce", "cell+publish"])
     ph = [(1, 0), (2, 1), (3, 2), (4, 3)]
@@ -53,6 +53,12 @@ def main(prec=1, B=32, T=500, H=512, bwd=False):
     print(f"{'last poll RT':14s} median {rt.median().item():8.0f}")
     sp = d[2:, 6]
     print(f"{'spins':14s} median {sp.median().item():8.0f} mean {sp.mean().item():6.2f}")
+    print(f"placement flags (bit0 plain same-XCD stores, bit1 xcd-local grid): {int(d[0, 7])}")
+    if bwd:
+        for w in range(4):
+            pd = d[2:, 8 + w] - d[2:, 0]
+            pb = d[2:, 12 + w] - d[2:, 0]
+            print(f"wave {w}: poll done +{pd.median().item():6.0f}  at barrier +{pb.median().item():6.0f}")
     tot = d[3:, 0] - d[2:-1, 0]
     print(f"{'step total':14s} median {tot.median().item():8.0f}")
 
