@@ -221,6 +221,10 @@ class VAEEngine:
         self._work = {}
         self.overlap = True         # weight-gradient GEMMs on a side stream
         self.side_stream = torch.cuda.Stream(self.device)
+        # the step's critical path (recurrences, dgrads) runs on a high-priority stream so the
+        # dispatcher prefers its workgroups over the side stream's weight-gradient GEMMs
+        self.prioritize = False   # measured no gain at c2 (8.44 vs 8.39 ms); kept as an option
+        self.main_stream = torch.cuda.Stream(self.device, priority=-1)
         self._on_side = False
         self.kernel_timers = None   # {name: [(start_event, end_event), ...]} when profiling
         self.process_group = None   # set by mlvae_hip.dist for data parallel
@@ -561,12 +565,34 @@ class VAEEngine:
         from . import dist as mdist
         mdist.allreduce_step(self.grad, w.loss, self.process_group)
 
+    def _main(self):
+        """Context: run on the high-priority main stream, ordered after (and before) the
+        caller's current stream."""
+        eng = self
+
+        class _M:
+            def __enter__(self_):
+                if not eng.prioritize:
+                    return
+                self_.caller = torch.cuda.current_stream(eng.device)
+                eng.main_stream.wait_stream(self_.caller)
+                self_.ctx = torch.cuda.stream(eng.main_stream)
+                self_.ctx.__enter__()
+
+            def __exit__(self_, *exc):
+                if not eng.prioritize:
+                    return
+                self_.ctx.__exit__(*exc)
+                self_.caller.wait_stream(eng.main_stream)
+        return _M()
+
     def train_step(self, x, lens, eps=None, dropout_masks=None):
         """One fit_batch: forward, backward, clip + Adam.  Returns the device tensor
         [kld_loss, recon_loss, loss] (no host synchronisation)."""
-        w = self.forward(x, lens, eps=eps, train=True, dropout_masks=dropout_masks)
-        self.backward(w)
-        self.optimizer_step(w)
+        with self._main():
+            w = self.forward(x, lens, eps=eps, train=True, dropout_masks=dropout_masks)
+            self.backward(w)
+            self.optimizer_step(w)
         self.rng_step += 1
         return w.loss
 

@@ -1,0 +1,52 @@
+"""Per-kernel HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+usage: python tools/pmc_summary.py <fetch counter_collection.csv> <write counter_collection.csv> <out.json>
+
+Both counters are reported in KB.  MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE
+counts exactly half of the bytes of wide coalesced streaming reads, so the read bytes are
+taken as 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B streaming stores.  hbm_bytes_per_launch =
+2*FETCH + WRITE (the raw values are kept next to it)."""
+import collections
+import csv
+import json
+import sys
+
+
+def per_kernel(path):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+    return agg
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "")
+    if "lstm_bwd_rs_kernel" in n or "lstm_bwd_kernel" in n:
+        return "lstm_bwd"
+    if "lstm_fwd_kernel" in n:
+        return "lstm_fwd"
+    return n.split("(")[0]
+
+
+def main(fetch_csv, write_csv, out):
+    f, w = per_kernel(fetch_csv), per_kernel(write_csv)
+    res = {}
+    for name in set(f) | set(w):
+        fv, wv = f.get(name, [0.0]), w.get(name, [0.0])
+        fetch = sum(fv) / len(fv)
+        write = sum(wv) / len(wv)
+        key = short(name)
+        if key in res and res[key]["launches"] >= len(fv):
+            continue
+        res[key] = {"kernel": name, "launches": len(fv), "fetch_size_bytes_raw": fetch,
+                    "write_size_bytes": write, "read_bytes_corrected": 2 * fetch,
+                    "hbm_bytes_per_launch": 2 * fetch + write}
+    res = dict(sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]))
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in list(res.items())[:10]:
+        print(f"{k:40s} launches {v['launches']:3d}  read {v['read_bytes_corrected'] / 1e6:9.1f} MB  "
+              f"write {v['write_size_bytes'] / 1e6:9.1f} MB")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
