@@ -36,6 +36,18 @@ int mlvae_gemm(int prec, int trans_a, int trans_b, int M, int N, int K, float al
                const float* bias1, const float* bias2, int epi, const float* aux, int ldaux,
                int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream);
 
+/* bf16-MFMA GEMM over bf16 or fp32 operands (a_bf16 / b_bf16: operand stored as bf16),
+ * fp32 C, same epilogues / kshift / split-K as mlvae_gemm.  The bf16 precision mode's GEMMs:
+ * the step keeps bf16 copies of its GEMM operands (h, dropout output, dG, weights).  Operand
+ * rows along the contiguous dimension must be 16-byte aligned. */
+size_t mlvae_gemm_ex_workspace_size(int M, int N, int K);
+int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, float alpha, const void* A,
+                  int a_bf16, int lda, const void* B, int b_bf16, int ldb, float beta, float* C,
+                  int ldc, const float* bias1, const float* bias2, int epi, const float* aux,
+                  int ldaux, int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream);
+/* y (bf16) = round-to-nearest-even(x), n elements. */
+int mlvae_cast_bf16(size_t n, const float* x, void* y, void* stream);
+
 /* Bidirectional LSTM layer recurrence, both directions in one persistent launch.
  * gates [B*T, 8H]: in = x W_ih^T + b_ih + b_hh (cols [0,4H) forward, [4H,8H) reverse);
  *                  out = activated gates i,f,g,o (saved for the backward).
@@ -52,6 +64,15 @@ int mlvae_lstm_fwd(int prec, int B, int T, int H, const float* w_hh_fwd, const f
 int mlvae_lstm_bwd(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                    float* gates, const float* cells, const float* dy, void* xbuf, size_t xbytes,
                    int* err, void* stream);
+/* _ex variants: the forward also writes h as bf16 (y_bf16 [B*T, 2H], may be NULL); the
+ * backward writes dG as bf16 into dg_bf16 [B*T, 8H] instead of into gates (NULL: into gates).
+ * The bf16 copies are the operands of the bf16-mode GEMMs (mlvae_gemm_ex). */
+int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                      float* gates, float* cells, float* y, void* y_bf16, void* xbuf,
+                      size_t xbytes, int* err, void* stream);
+int mlvae_lstm_bwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                      float* gates, const float* cells, const float* dy, void* dg_bf16,
+                      void* xbuf, size_t xbytes, int* err, void* stream);
 /* Diagnostics: record per-step phase stamps of workgroup 0 into buf (NULL disables). */
 int mlvae_lstm_set_debug(void* buf);
 
@@ -114,11 +135,17 @@ int mlvae_masked_mean_bwd(int B, int T, int C, const float* lens, int reduction,
 size_t mlvae_colsum_workspace_size(int N, int C);
 int mlvae_colsum(int N, int C, const float* in, int ld, float* out, float* out2, float beta,
                  float* ws, size_t ws_bytes, void* stream);
+/* the same over an fp32 (in_bf16 = 0) or bf16 (in_bf16 = 1) input */
+int mlvae_colsum_ex(int N, int C, const void* in, int in_bf16, int ld, float* out, float* out2,
+                    float beta, float* ws, size_t ws_bytes, void* stream);
 
 /* y = x * mask; mask = given (already scaled) or Philox(seed, i) keep-prob 1-p scaled 1/(1-p).
  * Inter-layer dropout of nn.LSTM in train mode (ref:src/modules/decoder.py:14). */
 int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
                   unsigned long long seed, float p, void* stream);
+/* the same writing y (fp32, may be NULL) and/or y_bf16 (bf16, may be NULL) */
+int mlvae_dropout_ex(size_t n, const float* x, float* y, void* y_bf16, const float* mask,
+                     unsigned long long seed, float p, void* stream);
 
 #ifdef __cplusplus
 }

@@ -53,6 +53,8 @@ struct LstmArgs {
   int xcd_local;            // group g = blocks b with b % 8 == g (one XCD each, when the
                             // dispatcher deals round-robin); others exit at once
   unsigned* xtab;           // [ngroups][NJ] XCC id + 1 of every member (zeroed per launch)
+  unsigned short* Yb;       // optional bf16 copy of h [B*T, 2H] (fwd; GEMM operand)
+  unsigned short* dGb;      // optional: bwd writes dG as bf16 [B*T, 8H] here instead of into G
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -305,6 +307,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
       gp[0] = ig; gp[H] = fg; gp[2 * H] = gg; gp[3 * H] = og;
       a.Cs[n * 2 * H + dir * H + j0 + jj] = c;
       a.Y[n * 2 * H + dir * H + j0 + jj] = hv;
+      if (a.Yb) a.Yb[n * 2 * H + dir * H + j0 + jj] = (unsigned short)f2bf(hv);
     }
   }
 }
@@ -529,8 +532,15 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
       for (int u = 0; u < UPT; ++u) {
         const int uu = cj + 16 * u;
         if (uu < HJ) {
-          float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + uu;
-          gp[0] = dG[u][0]; gp[H] = dG[u][1]; gp[2 * H] = dG[u][2]; gp[3 * H] = dG[u][3];
+          const size_t o = n * 8 * H + dir * 4 * H + j0 + uu;
+          if (a.dGb) {
+            unsigned short* gb = a.dGb + o;
+            gb[0] = (unsigned short)f2bf(dG[u][0]); gb[H] = (unsigned short)f2bf(dG[u][1]);
+            gb[2 * H] = (unsigned short)f2bf(dG[u][2]); gb[3 * H] = (unsigned short)f2bf(dG[u][3]);
+          } else {
+            float* gp = a.G + o;
+            gp[0] = dG[u][0]; gp[H] = dG[u][1]; gp[2 * H] = dG[u][2]; gp[3 * H] = dG[u][3];
+          }
         }
       }
     }
@@ -741,8 +751,15 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
     }
     STAMP(4);
     if (bvalid && !(a.dbg_mode & 1)) {  // dG for the weight-gradient GEMMs: plain stores
-      float* gp = a.G + n * 8 * H + dir * 4 * H + j;
-      gp[0] = dG0; gp[H] = dG1; gp[2 * H] = dG2; gp[3 * H] = dG3;
+      const size_t o = n * 8 * H + dir * 4 * H + j;
+      if (a.dGb) {
+        unsigned short* gb = a.dGb + o;
+        gb[0] = (unsigned short)f2bf(dG0); gb[H] = (unsigned short)f2bf(dG1);
+        gb[2 * H] = (unsigned short)f2bf(dG2); gb[3 * H] = (unsigned short)f2bf(dG3);
+      } else {
+        float* gp = a.G + o;
+        gp[0] = dG0; gp[H] = dG1; gp[2 * H] = dG2; gp[3 * H] = dG3;
+      }
     }
     return true;
   };
@@ -863,7 +880,8 @@ unsigned long long* g_dbg = nullptr;
 int g_dbg_mode = 0;
 
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
-        float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st) {
+        float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
+        unsigned short* yb = nullptr, unsigned short* dgb = nullptr) {
   if (B <= 0 || T <= 0) return 0;
   if (H <= 0 || H % 4 != 0) { mlvae_set_error("lstm: H=%d must be a positive multiple of 4", H); return 1; }
   if (prec != PREC_F32 && prec != PREC_BF16) { mlvae_set_error("lstm: bad prec %d", prec); return 1; }
@@ -886,6 +904,8 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     a.Cs = Cs + (size_t)b0 * T * 2 * H;
     a.Y = Y + (size_t)b0 * T * 2 * H;
     a.xbuf = xbuf; a.err = err; a.dbg = g_dbg; a.dbg_mode = g_dbg_mode;
+    a.Yb = yb ? yb + (size_t)b0 * T * 2 * H : nullptr;
+    a.dGb = dgb ? dgb + (size_t)b0 * T * 8 * H : nullptr;
     a.xcd_local = p.xcd && (g_dbg_mode & 2) && device_cus() == 256;
     a.xtab = p.rs ? reinterpret_cast<unsigned*>(static_cast<char*>(xbuf) +
                                                 (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * 256 * sizeof(short))
@@ -923,18 +943,34 @@ extern "C" int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes)
   return 0;
 }
 
+extern "C" int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd,
+                                 const float* w_hh_rev, float* gates, float* cells, float* y,
+                                 void* y_bf16, void* xbuf, size_t xbytes, int* err, void* stream) {
+  return run(true, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, cells, y, xbuf, xbytes, err,
+             (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr);
+}
+
 extern "C" int mlvae_lstm_fwd(int prec, int B, int T, int H, const float* w_hh_fwd,
                               const float* w_hh_rev, float* gates, float* cells, float* y,
                               void* xbuf, size_t xbytes, int* err, void* stream) {
-  return run(true, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, cells, y, xbuf, xbytes, err,
-             (hipStream_t)stream);
+  return mlvae_lstm_fwd_ex(prec, B, T, H, w_hh_fwd, w_hh_rev, gates, cells, y, nullptr, xbuf,
+                           xbytes, err, stream);
+}
+
+extern "C" int mlvae_lstm_bwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd,
+                                 const float* w_hh_rev, float* gates, const float* cells,
+                                 const float* dy, void* dg_bf16, void* xbuf, size_t xbytes,
+                                 int* err, void* stream) {
+  return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, const_cast<float*>(cells),
+             const_cast<float*>(dy), xbuf, xbytes, err, (hipStream_t)stream, nullptr,
+             static_cast<unsigned short*>(dg_bf16));
 }
 
 extern "C" int mlvae_lstm_bwd(int prec, int B, int T, int H, const float* w_hh_fwd,
                               const float* w_hh_rev, float* gates, const float* cells,
                               const float* dy, void* xbuf, size_t xbytes, int* err, void* stream) {
-  return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, gates, const_cast<float*>(cells),
-             const_cast<float*>(dy), xbuf, xbytes, err, (hipStream_t)stream);
+  return mlvae_lstm_bwd_ex(prec, B, T, H, w_hh_fwd, w_hh_rev, gates, cells, dy, nullptr, xbuf,
+                           xbytes, err, stream);
 }
 
 // Diagnostics: when set, the next recurrence launches record per-step phase stamps of

@@ -133,7 +133,25 @@ __global__ __launch_bounds__(256) void clip_scale_kernel(float* __restrict__ g, 
 // ---------------------------------------------------------------- column sums
 // Block = 64 columns x a chunk of rows; 256 threads = 16 column quads x 16 row lanes, float4
 // loads, fixed-order LDS fold -> part[chunk][c]; colsum_final folds the chunks in order.
-__global__ __launch_bounds__(256) void colsum_partial(int N, int C, const float* __restrict__ in,
+template <bool BF>
+__device__ __forceinline__ f32x4 load4(const void* in, size_t off) {
+  if constexpr (BF) {
+    const u32x2 v = *reinterpret_cast<const u32x2*>(static_cast<const unsigned short*>(in) + off);
+    return f32x4{__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u),
+                 __uint_as_float(v[1] << 16), __uint_as_float(v[1] & 0xffff0000u)};
+  } else {
+    return *reinterpret_cast<const f32x4*>(static_cast<const float*>(in) + off);
+  }
+}
+template <bool BF>
+__device__ __forceinline__ float load1(const void* in, size_t off) {
+  if constexpr (BF) return __uint_as_float((unsigned)static_cast<const unsigned short*>(in)[off] << 16);
+  else return static_cast<const float*>(in)[off];
+}
+
+// in: fp32, or bf16 (the bf16 mode's dG copy)
+template <bool BF>
+__global__ __launch_bounds__(256) void colsum_partial(int N, int C, const void* __restrict__ in,
                                                       int ld, int rows_per, int vec,
                                                       float* __restrict__ part) {
   __shared__ f32x4 red[16][16];
@@ -143,11 +161,11 @@ __global__ __launch_bounds__(256) void colsum_partial(int N, int C, const float*
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     if (vec && c + 3 < C) {
-      for (int r = r0 + rl; r < r1; r += 16) acc += *reinterpret_cast<const f32x4*>(in + (size_t)r * ld + c);
+      for (int r = r0 + rl; r < r1; r += 16) acc += load4<BF>(in, (size_t)r * ld + c);
     } else {
       for (int r = r0 + rl; r < r1; r += 16)
         for (int e = 0; e < 4; ++e)
-          if (c + e < C) acc[e] += in[(size_t)r * ld + c + e];
+          if (c + e < C) acc[e] += load1<BF>(in, (size_t)r * ld + c + e);
     }
   }
   red[rl][cq] = acc;
@@ -160,6 +178,7 @@ __global__ __launch_bounds__(256) void colsum_partial(int N, int C, const float*
     if (cc < C) part[(size_t)blockIdx.y * C + cc] = s;
   }
 }
+
 __global__ __launch_bounds__(256) void colsum_final(int C, int R, const float* __restrict__ part,
                                                     float* __restrict__ out, float* __restrict__ out2,
                                                     float beta) {
@@ -205,6 +224,7 @@ __device__ __forceinline__ unsigned philox_u32(unsigned long long seed, unsigned
 
 __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __restrict__ x,
                                                       float* __restrict__ y,
+                                                      unsigned short* __restrict__ ybf,
                                                       const float* __restrict__ mask,
                                                       unsigned long long seed, float p) {
   const float keep = 1.f - p, scale = 1.f / keep;
@@ -212,7 +232,9 @@ __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __r
     float m;
     if (mask) m = mask[i];
     else m = ((philox_u32(seed, i) >> 8) * (1.f / 16777216.f)) < keep ? scale : 0.f;
-    y[i] = x[i] * m;
+    const float v = x[i] * m;
+    if (y) y[i] = v;
+    if (ybf) ybf[i] = (unsigned short)f2bf(v);
   }
 }
 
@@ -271,24 +293,39 @@ extern "C" size_t mlvae_colsum_workspace_size(int N, int C) {
 }
 
 // out[c] (+= if beta) = sum_n in[n][c]; out2 (optional) receives a copy (b_ih / b_hh pairs)
-extern "C" int mlvae_colsum(int N, int C, const float* in, int ld, float* out, float* out2,
-                            float beta, float* ws, size_t ws_bytes, void* stream) {
+extern "C" int mlvae_colsum_ex(int N, int C, const void* in, int in_bf16, int ld, float* out,
+                               float* out2, float beta, float* ws, size_t ws_bytes, void* stream) {
   if (C == 0) return 0;
   const int R = colsum_chunks(N, C);
   if (!ws || ws_bytes < (size_t)R * C * sizeof(float)) { mlvae_set_error("colsum: workspace too small"); return 1; }
   const int rows_per = (N + R - 1) / R;
-  const int vec = (((uintptr_t)in & 15) == 0) && (ld % 4 == 0);
+  const int vec = in_bf16 ? ((((uintptr_t)in & 7) == 0) && (ld % 4 == 0))
+                          : ((((uintptr_t)in & 15) == 0) && (ld % 4 == 0));
   hipStream_t s = (hipStream_t)stream;
-  colsum_partial<<<dim3((C + 63) / 64, R), 256, 0, s>>>(N, C, in, ld, rows_per, vec, ws);
+  if (in_bf16) colsum_partial<true><<<dim3((C + 63) / 64, R), 256, 0, s>>>(N, C, in, ld, rows_per, vec, ws);
+  else colsum_partial<false><<<dim3((C + 63) / 64, R), 256, 0, s>>>(N, C, in, ld, rows_per, vec, ws);
   colsum_final<<<(C + 255) / 256, 256, 0, s>>>(C, R, ws, out, out2, beta);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_colsum(int N, int C, const float* in, int ld, float* out, float* out2,
+                            float beta, float* ws, size_t ws_bytes, void* stream) {
+  return mlvae_colsum_ex(N, C, in, 0, ld, out, out2, beta, ws, ws_bytes, stream);
+}
+
+extern "C" int mlvae_dropout_ex(size_t n, const float* x, float* y, void* y_bf16,
+                                const float* mask, unsigned long long seed, float p,
+                                void* stream) {
+  if (p < 0.f || p >= 1.f) { mlvae_set_error("dropout: p=%f out of range", p); return 1; }
+  if (!y && !y_bf16) { mlvae_set_error("dropout: no output"); return 1; }
+  dropout_kernel<<<grid_for(n, 2048), 256, 0, (hipStream_t)stream>>>(
+      n, x, y, static_cast<unsigned short*>(y_bf16), mask, seed, p);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
                              unsigned long long seed, float p, void* stream) {
-  if (p < 0.f || p >= 1.f) { mlvae_set_error("dropout: p=%f out of range", p); return 1; }
-  dropout_kernel<<<grid_for(n, 2048), 256, 0, (hipStream_t)stream>>>(n, x, y, mask, seed, p);
-  MLVAE_CHECK_LAUNCH();
-  return 0;
+  return mlvae_dropout_ex(n, x, y, nullptr, mask, seed, p, stream);
 }

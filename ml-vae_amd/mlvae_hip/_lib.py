@@ -23,9 +23,14 @@ _SIGS = {
     "mlvae_device_check": [C.c_char_p, I],
     "mlvae_gemm_workspace_size": [I, I, I],
     "mlvae_gemm": [I, I, I, I, I, I, F, P, I, P, I, F, P, I, P, P, I, P, I, I, I, P, SZ, P],
+    "mlvae_gemm_ex_workspace_size": [I, I, I],
+    "mlvae_gemm_ex": [I, I, I, I, I, F, P, I, I, P, I, I, F, P, I, P, P, I, P, I, I, I, P, SZ, P],
+    "mlvae_cast_bf16": [SZ, P, P, P],
     "mlvae_lstm_workspace_size": [I, I, I, C.POINTER(SZ)],
     "mlvae_lstm_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_lstm_fwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_lstm_bwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_elbo_partials_count": [I, I, I],
     "mlvae_reparam_kl_fwd": [I, I, I, P, I, P, P, P, P, P, P],
     "mlvae_reparam_kl_bwd": [I, I, I, P, I, P, P, P, P, P, F, P, I, P],
@@ -39,7 +44,9 @@ _SIGS = {
     "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P, I, P],
     "mlvae_colsum_workspace_size": [I, I],
     "mlvae_colsum": [I, I, P, I, P, P, F, P, SZ, P],
+    "mlvae_colsum_ex": [I, I, P, I, I, P, P, F, P, SZ, P],
     "mlvae_dropout": [SZ, P, P, P, U64, F, P],
+    "mlvae_dropout_ex": [SZ, P, P, P, P, U64, F, P],
     "mlvae_lrelu_bwd": [SZ, P, P, P, P],
     "mlvae_clip_scale": [P, SZ, P, I, F, P, P],
     "mlvae_masked_mean_bwd": [I, I, I, P, I, P, P, P],
@@ -49,6 +56,7 @@ _SIGS = {
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
     "mlvae_gemm_workspace_size": SZ,
+    "mlvae_gemm_ex_workspace_size": SZ,
     "mlvae_colsum_workspace_size": SZ,
 }
 

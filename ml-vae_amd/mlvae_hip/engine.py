@@ -149,6 +149,15 @@ class _Work:
         self.Cs = [torch.empty(N, 2 * H, **f) for _ in range(L)]
         self.Y = [torch.empty(N, 2 * H, **f) for _ in range(L)]
         self.Yd = [torch.empty(N, 2 * H, **f) if cfg.dropout > 0 else None for _ in range(L - 1)]
+        # bf16 mode: bf16 copies of the big GEMM operands (h, dropout output, dG)
+        self.bf = cfg.prec == "bf16"
+        b16 = dict(device=device, dtype=torch.bfloat16)
+        self.Yb = [torch.empty(N, 2 * H, **b16) for _ in range(L)] if self.bf else None
+        self.Ydb = ([torch.empty(N, 2 * H, **b16) if cfg.dropout > 0 else None for _ in range(L - 1)]
+                    if self.bf else None)
+        self.dGb = [torch.empty(N, 8 * H, **b16) for _ in range(L)] if self.bf else None
+        if self.bf:
+            self.Yd = [None] * (L - 1)  # the dropout output exists as bf16 only
         self.P1 = torch.empty(N, 2 * C, **f)
         self.P2m = torch.empty(N, C, **f)
         self.P2v = torch.empty(N, C, **f)
@@ -179,7 +188,8 @@ class _Work:
         for li in range(L):
             din = Z if li == 0 else 2 * H
             shapes += [(N, 8 * H, din), (8 * H, din, N)]
-        ws = max(l.mlvae_gemm_workspace_size(m, n, k) for m, n, k in shapes)
+        ws = max(max(l.mlvae_gemm_workspace_size(m, n, k), l.mlvae_gemm_ex_workspace_size(m, n, k))
+                 for m, n, k in shapes)
         cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
         self.gws = torch.empty(max(ws, cs, 16) // 4 + 1, **f)
         self.gws_side = torch.empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
@@ -188,6 +198,15 @@ class _Work:
         check(l.mlvae_lstm_workspace_size(B, H, PREC[cfg.prec], _lib.C.byref(xb)), "lstm_workspace_size")
         self.xbuf = torch.empty(max(xb.value, 16), device=device, dtype=torch.uint8)
         self.err = torch.zeros(1, device=device, dtype=torch.int32)
+
+
+def _aligned(ptr, ld, bf):
+    return ptr is not None and ptr % 16 == 0 and ld % (8 if bf else 4) == 0
+
+
+def _pb(t, off=0):
+    """address of element off of a bf16 tensor"""
+    return t.data_ptr() + 2 * off
 
 
 def _p(t, off=0):
@@ -214,6 +233,8 @@ class VAEEngine:
         self.nonfinite_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.grad_norm = torch.zeros(1, **f)
         self.hyp = torch.zeros(4, **f)
+        # bf16 mode: bf16 copy of the weights, refreshed at the start of every forward
+        self.flat_bf = torch.empty(n, device=self.device, dtype=torch.bfloat16) if cfg.prec == "bf16" else None
         self.nparts = lib().mlvae_sumsq_partials_count(n)
         self.sq_parts = torch.zeros(self.nparts, device=self.device, dtype=torch.float64)
         self.seed = seed
@@ -296,6 +317,12 @@ class VAEEngine:
     def _ptr(self, name, buf=None):
         return _p(self.flat if buf is None else buf, self.layout.offsets[name])
 
+    def _wb(self, name):
+        """bf16 copy of a weight (bf16 mode), else None."""
+        if self.flat_bf is None:
+            return None
+        return _pb(self.flat_bf, self.layout.offsets[name])
+
     def work(self, B, T):
         key = (B, T)
         if key not in self._work:
@@ -314,6 +341,24 @@ class VAEEngine:
         check(lib().mlvae_gemm(PREC[self.cfg.prec], ta, tb, M, N, K, 1.0, A, lda, B, ldb, beta, C,
                                ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift,
                                _p(ws), w.gws_bytes, self._stream()), "mlvae_gemm")
+
+    def _mm(self, w, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, A_bf=None, B_bf=None, bias1=None,
+            bias2=None, epi=0, aux=None, ldaux=0, kshift_T=0, kshift=0, beta=0.0):
+        """GEMM with each operand given as fp32 (A, B) and/or bf16 (A_bf, B_bf) pointer.
+        bf16 mode runs mlvae_gemm_ex (bf16 operands preferred); fp32 mode the exact kernel."""
+        if self.cfg.prec == "bf16":
+            a, abf = (A_bf, 1) if A_bf is not None else (A, 0)
+            b, bbf = (B_bf, 1) if B_bf is not None else (B, 0)
+            if _aligned(a, lda, abf) and _aligned(b, ldb, bbf):
+                ws = w.gws_side if self._on_side else w.gws
+                check(lib().mlvae_gemm_ex(ta, tb, M, N, K, 1.0, a, abf, lda, b, bbf, ldb, beta, C,
+                                          ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift,
+                                          _p(ws), w.gws_bytes, self._stream()), "mlvae_gemm_ex")
+                return
+        if A is None or B is None:
+            raise RuntimeError("GEMM operand exists only as bf16 but is not 16-byte aligned")
+        self._gemm(w, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, bias1=bias1, bias2=bias2, epi=epi,
+                   aux=aux, ldaux=ldaux, kshift_T=kshift_T, kshift=kshift, beta=beta)
 
     def _colsum(self, w, N, Cn, src, ld, out, out2=None):
         ws = w.gws_side if self._on_side else w.gws
@@ -372,6 +417,9 @@ class VAEEngine:
         N, E, Z, H, C, Fd = w.N, cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
         X = _p(x)
+        if self.flat_bf is not None:  # this step's weights as bf16 GEMM operands
+            check(l.mlvae_cast_bf16(self.layout.total, _p(self.flat), _pb(self.flat_bf), s), "cast_bf16")
+        wb = self._wb
         count = None
         if self.world > 1:
             count = self._global_count(w)
@@ -384,45 +432,54 @@ class VAEEngine:
             eps_t = eps.to(self.device, torch.float32).contiguous().view(N, Z)
         w.eps_used = eps_t
         # ---- encoder (ref:src/modules/vanilla_vae.py:21-28)
-        self._gemm(w, 0, 1, N, E, Fd, X, Fd, self._ptr("encoder.fc.0.blocks.0.weight"), Fd,
-                   _p(w.E1), E, bias1=self._ptr("encoder.fc.0.blocks.0.bias"), epi=EPI_LRELU)
-        self._gemm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
-                   _p(w.E2), E, bias1=self._ptr("encoder.fc.0.blocks.2.bias"), epi=EPI_LRELU)
-        self._gemm(w, 0, 1, N, 2 * Z, E, _p(w.E2), E, self._ptr("encoder.mean_fc.weight"), E,
-                   _p(w.ML), 2 * Z, bias1=self._ptr("encoder.mean_fc.bias"))
+        self._mm(w, 0, 1, N, E, Fd, X, Fd, self._ptr("encoder.fc.0.blocks.0.weight"), Fd,
+                 _p(w.E1), E, B_bf=wb("encoder.fc.0.blocks.0.weight"),
+                 bias1=self._ptr("encoder.fc.0.blocks.0.bias"), epi=EPI_LRELU)
+        self._mm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
+                 _p(w.E2), E, B_bf=wb("encoder.fc.0.blocks.2.weight"),
+                 bias1=self._ptr("encoder.fc.0.blocks.2.bias"), epi=EPI_LRELU)
+        self._mm(w, 0, 1, N, 2 * Z, E, _p(w.E2), E, self._ptr("encoder.mean_fc.weight"), E,
+                 _p(w.ML), 2 * Z, B_bf=wb("encoder.mean_fc.weight"), bias1=self._ptr("encoder.mean_fc.bias"))
         check(l.mlvae_reparam_kl_fwd(B, T, Z, _p(w.ML), 2 * Z, _p(eps_t), _p(lens), _p(w.Zs),
                                      None, _p(w.pk), s), "reparam_kl_fwd")
         # ---- decoder BiLSTM (ref:src/modules/decoder.py:22)
-        xin, din = w.Zs, Z
+        # layer input as (fp32 tensor or None, bf16 tensor or None, width)
+        xin, xin_bf, din = w.Zs, None, Z
         w.layer_in = []
         for li in range(cfg.L):
-            w.layer_in.append((xin, din))
-            self._gemm(w, 0, 1, N, 8 * H, din, _p(xin), din,
-                       self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
-                       bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
-                       bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+            w.layer_in.append((xin, xin_bf, din))
+            self._mm(w, 0, 1, N, 8 * H, din, _p(xin) if xin is not None else None, din,
+                     self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
+                     A_bf=_pb(xin_bf) if xin_bf is not None else None,
+                     B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
+                     bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                     bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
             with self._timed("lstm_fwd"):
-                check(l.mlvae_lstm_fwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                       self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                       _p(w.Cs[li]), _p(w.Y[li]), _p(w.xbuf), w.xbuf.numel(),
-                                       _p(w.err), s), "lstm_fwd")
-            xin, din = w.Y[li], 2 * H
+                check(l.mlvae_lstm_fwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                          self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                          _p(w.Cs[li]), _p(w.Y[li]), _pb(w.Yb[li]) if w.bf else None,
+                                          _p(w.xbuf), w.xbuf.numel(), _p(w.err), s), "lstm_fwd")
+            xin, xin_bf, din = w.Y[li], (w.Yb[li] if w.bf else None), 2 * H
             if li < cfg.L - 1 and train and cfg.dropout > 0:
-                xin = w.Yd[li]
+                xin, xin_bf = w.Yd[li], (w.Ydb[li] if w.bf else None)
                 self._dropout(w, li, w.Y[li], xin, dropout_masks)
         w.rnn_out = w.Y[cfg.L - 1]
+        w.rnn_out_bf = w.Yb[cfg.L - 1] if w.bf else None
         # ---- heads (ref:src/modules/decoder.py:24-25, FCBlock ref:src/modules/fc_block.py:9-16)
         R = _p(w.rnn_out)
-        self._gemm(w, 0, 1, N, 2 * C, 2 * H, R, 2 * H, self._ptr("decoder.mean_fc.blocks.0.weight"),
-                   2 * H, _p(w.P1), 2 * C, bias1=self._ptr("decoder.mean_fc.blocks.0.bias"),
-                   epi=EPI_LRELU)
+        self._mm(w, 0, 1, N, 2 * C, 2 * H, R, 2 * H, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                 2 * H, _p(w.P1), 2 * C, A_bf=_pb(w.rnn_out_bf) if w.bf else None,
+                 B_bf=wb("decoder.mean_fc.blocks.0.weight"),
+                 bias1=self._ptr("decoder.mean_fc.blocks.0.bias"), epi=EPI_LRELU)
         for hd, P2, out in (("mean_fc", w.P2m, w.MUX), ("log_var_fc", w.P2v, w.LVX)):
             off = 0 if hd == "mean_fc" else C
-            self._gemm(w, 0, 1, N, C, C, _p(w.P1, off), 2 * C,
-                       self._ptr(f"decoder.{hd}.blocks.2.weight"), C, _p(P2), C,
-                       bias1=self._ptr(f"decoder.{hd}.blocks.2.bias"), epi=EPI_LRELU)
-            self._gemm(w, 0, 1, N, Fd, C, _p(P2), C, self._ptr(f"decoder.{hd}.blocks.4.weight"), C,
-                       _p(out), Fd, bias1=self._ptr(f"decoder.{hd}.blocks.4.bias"))
+            self._mm(w, 0, 1, N, C, C, _p(w.P1, off), 2 * C,
+                     self._ptr(f"decoder.{hd}.blocks.2.weight"), C, _p(P2), C,
+                     B_bf=wb(f"decoder.{hd}.blocks.2.weight"),
+                     bias1=self._ptr(f"decoder.{hd}.blocks.2.bias"), epi=EPI_LRELU)
+            self._mm(w, 0, 1, N, Fd, C, _p(P2), C, self._ptr(f"decoder.{hd}.blocks.4.weight"), C,
+                     _p(out), Fd, B_bf=wb(f"decoder.{hd}.blocks.4.weight"),
+                     bias1=self._ptr(f"decoder.{hd}.blocks.4.bias"))
         # ---- ELBO part 2 (+ its gradient when training)
         lt = LOSS[cfg.loss_type]
         w_kl, w_rec = self.loss_weights()
@@ -447,8 +504,10 @@ class VAEEngine:
             w.__dict__.setdefault("_masks", {})[li] = m
             mask_ptr = _p(m)
         seed = (self.seed * 1000003 + self.rng_step * 131 + li) & ((1 << 63) - 1)
-        check(lib().mlvae_dropout(src.numel(), _p(src), _p(dst), mask_ptr, seed, self.cfg.dropout,
-                                  self._stream()), "dropout")
+        dst_bf = w.Ydb[li] if w.bf else None
+        check(lib().mlvae_dropout_ex(src.numel(), _p(src), _p(dst) if dst is not None else None,
+                                     _pb(dst_bf) if dst_bf is not None else None, mask_ptr, seed,
+                                     self.cfg.dropout, self._stream()), "dropout")
         w.__dict__.setdefault("_drop_seed", {})[li] = (seed, mask_ptr)
 
     def _global_count(self, w):
@@ -471,56 +530,74 @@ class VAEEngine:
         heads = [("mean_fc", w.P2m, w.dMUX, w.dP2m, 0)]
         if not mse:
             heads.append(("log_var_fc", w.P2v, w.dLVX, w.dP2v, C))
+        wb = self._wb
         for hd, P2, dOut, dP2, off in heads:
             W3, W2 = self._ptr(f"decoder.{hd}.blocks.4.weight"), self._ptr(f"decoder.{hd}.blocks.2.weight")
 
             def wg3(hd=hd, dOut=dOut, P2=P2):
-                self._gemm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
+                self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
                 self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
             self._side(wg3)
-            self._gemm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C, epi=EPI_DLRELU,
-                       aux=_p(P2), ldaux=C)
+            self._mm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C,
+                     B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
 
             def wg2(hd=hd, dP2=dP2, off=off):
-                self._gemm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
-                           gp(f"decoder.{hd}.blocks.2.weight"), C)
+                self._mm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
+                         gp(f"decoder.{hd}.blocks.2.weight"), C)
                 self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
             self._side(wg2)
-            self._gemm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C, epi=EPI_DLRELU,
-                       aux=_p(w.P1, off), ldaux=2 * C)
+            self._mm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C,
+                     B_bf=wb(f"decoder.{hd}.blocks.2.weight"), epi=EPI_DLRELU,
+                     aux=_p(w.P1, off), ldaux=2 * C)
         K1 = C if mse else 2 * C  # mse: the log_var head gets no gradient (torch: grad None)
         R = _p(w.rnn_out)
+        R_bf = _pb(w.rnn_out_bf) if w.bf else None
 
         def wg1():
-            self._gemm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
-                       gp("decoder.mean_fc.blocks.0.weight"), 2 * H)
+            self._mm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
+                     gp("decoder.mean_fc.blocks.0.weight"), 2 * H, B_bf=R_bf)
             self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
         self._side(wg1)
-        self._gemm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
-                   2 * H, _p(w.dY[cfg.L - 1]), 2 * H)
+        self._mm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                 2 * H, _p(w.dY[cfg.L - 1]), 2 * H, B_bf=wb("decoder.mean_fc.blocks.0.weight"))
         # ---- BiLSTM layers, top to bottom
         for li in range(cfg.L - 1, -1, -1):
-            xin, din = w.layer_in[li]
+            xin, xin_bf, din = w.layer_in[li]
             Gl = w.G[li]
+            dGb = w.dGb[li] if w.bf else None
             with self._timed("lstm_bwd"):
-                check(l.mlvae_lstm_bwd(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                       self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                       _p(w.Cs[li]), _p(w.dY[li]), _p(w.xbuf), w.xbuf.numel(),
-                                       _p(w.err), s), "lstm_bwd")
+                check(l.mlvae_lstm_bwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                          self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
+                                          _p(w.Cs[li]), _p(w.dY[li]), _pb(dGb) if dGb is not None else None,
+                                          _p(w.xbuf), w.xbuf.numel(), _p(w.err), s), "lstm_bwd")
+            # dG: fp32 in G (fp32 mode) or bf16 in dGb (bf16 mode)
+            dG, dG_bf = (None, dGb) if dGb is not None else (Gl, None)
+            pg = lambda t, off=0: None if t is None else _p(t, off)
+            pgb = lambda t, off=0: None if t is None else _pb(t, off)
+            Ybl = w.Yb[li] if w.bf else None
 
-            def wgl(li=li, Gl=Gl, xin=xin, din=din):
-                self._gemm(w, 1, 0, 8 * H, din, N, _p(Gl), 8 * H, _p(xin), din,
-                           gp(f"decoder.rnn.weight_ih_l{li}"), din)
-                self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl), 8 * H, _p(w.Y[li]), 2 * H,
-                           gp(f"decoder.rnn.weight_hh_l{li}"), H, kshift_T=T, kshift=-1)
-                self._gemm(w, 1, 0, 4 * H, H, N, _p(Gl, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
-                           gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, kshift_T=T, kshift=1)
-                self._colsum(w, N, 8 * H, _p(Gl), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
-                             gp(f"decoder.rnn.bias_hh_l{li}"))
+            def wgl(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, Ybl=Ybl):
+                self._mm(w, 1, 0, 8 * H, din, N, pg(dG), 8 * H, pg(xin), din,
+                         gp(f"decoder.rnn.weight_ih_l{li}"), din, A_bf=pgb(dG_bf), B_bf=pgb(xin_bf))
+                self._mm(w, 1, 0, 4 * H, H, N, pg(dG), 8 * H, _p(w.Y[li]), 2 * H,
+                         gp(f"decoder.rnn.weight_hh_l{li}"), H, A_bf=pgb(dG_bf), B_bf=pgb(Ybl),
+                         kshift_T=T, kshift=-1)
+                self._mm(w, 1, 0, 4 * H, H, N, pg(dG, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
+                         gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, A_bf=pgb(dG_bf, 4 * H),
+                         B_bf=pgb(Ybl, H), kshift_T=T, kshift=1)
+                if dG_bf is not None:
+                    ws = w.gws_side if self._on_side else w.gws
+                    check(lib().mlvae_colsum_ex(N, 8 * H, _pb(dG_bf), 1, 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
+                                                gp(f"decoder.rnn.bias_hh_l{li}"), 0.0, _p(ws), w.gws_bytes,
+                                                self._stream()), "colsum")
+                else:
+                    self._colsum(w, N, 8 * H, _p(dG), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
+                                 gp(f"decoder.rnn.bias_hh_l{li}"))
             self._side(wgl)
             dx = w.dZs if li == 0 else w.dY[li - 1]
-            self._gemm(w, 0, 0, N, din, 8 * H, _p(Gl), 8 * H,
-                       self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din)
+            self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
+                     self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din, A_bf=pgb(dG_bf),
+                     B_bf=wb(f"decoder.rnn.weight_ih_l{li}"))
             if li > 0 and xin is not w.Y[li - 1]:  # dropout between layers li-1 and li
                 seed, mask_ptr = w._drop_seed[li - 1]
                 check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
@@ -531,19 +608,20 @@ class VAEEngine:
                                      _p(w.dZs), None, w_kl, _p(w.dML), 2 * Z, s), "reparam_kl_bwd")
 
         def wge2():
-            self._gemm(w, 1, 0, 2 * Z, E, N, _p(w.dML), 2 * Z, _p(w.E2), E, gp("encoder.mean_fc.weight"), E)
+            self._mm(w, 1, 0, 2 * Z, E, N, _p(w.dML), 2 * Z, _p(w.E2), E, gp("encoder.mean_fc.weight"), E)
             self._colsum(w, N, 2 * Z, _p(w.dML), 2 * Z, gp("encoder.mean_fc.bias"))
         self._side(wge2)
-        self._gemm(w, 0, 0, N, E, 2 * Z, _p(w.dML), 2 * Z, self._ptr("encoder.mean_fc.weight"), E,
-                   _p(w.dE2), E, epi=EPI_DLRELU, aux=_p(w.E2), ldaux=E)
+        self._mm(w, 0, 0, N, E, 2 * Z, _p(w.dML), 2 * Z, self._ptr("encoder.mean_fc.weight"), E,
+                 _p(w.dE2), E, B_bf=wb("encoder.mean_fc.weight"), epi=EPI_DLRELU, aux=_p(w.E2), ldaux=E)
 
         def wge1():
-            self._gemm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp("encoder.fc.0.blocks.2.weight"), E)
+            self._mm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp("encoder.fc.0.blocks.2.weight"), E)
             self._colsum(w, N, E, _p(w.dE2), E, gp("encoder.fc.0.blocks.2.bias"))
         self._side(wge1)
-        self._gemm(w, 0, 0, N, E, E, _p(w.dE2), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
-                   _p(w.dE1), E, epi=EPI_DLRELU, aux=_p(w.E1), ldaux=E)
-        self._gemm(w, 1, 0, E, Fd, N, _p(w.dE1), E, _p(w.x), Fd, gp("encoder.fc.0.blocks.0.weight"), Fd)
+        self._mm(w, 0, 0, N, E, E, _p(w.dE2), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
+                 _p(w.dE1), E, B_bf=wb("encoder.fc.0.blocks.2.weight"), epi=EPI_DLRELU,
+                 aux=_p(w.E1), ldaux=E)
+        self._mm(w, 1, 0, E, Fd, N, _p(w.dE1), E, _p(w.x), Fd, gp("encoder.fc.0.blocks.0.weight"), Fd)
         self._colsum(w, N, E, _p(w.dE1), E, gp("encoder.fc.0.blocks.0.bias"))
         self._join_side()
 

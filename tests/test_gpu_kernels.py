@@ -69,6 +69,83 @@ def test_gemm_epilogues_and_shift(prec, tol):
         assert rel_err(C, ref) < tol, (epi, shift)
 
 
+def _as_bf16(t, on):
+    """(device tensor handed to the kernel, fp64 values the kernel sees)."""
+    if on:
+        b = t.to(torch.bfloat16)
+        return b.cuda(), b.double()
+    return t.cuda(), t.double()
+
+
+@pytest.mark.parametrize("abf,bbf", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(200, 136, 72), (40, 24, 8), (136, 264, 1000), (64, 80, 4000)])
+def test_gemm_ex_bf16_operands(abf, bbf, ta, tb, M, N, K):
+    """mlvae_gemm_ex: bf16 MFMA over bf16- or fp32-stored operands, every transpose."""
+    need_gpu()
+    torch.manual_seed(M + 3 * N + K)
+    A = torch.randn(K, M) if ta else torch.randn(M, K)
+    B = torch.randn(N, K) if tb else torch.randn(K, N)
+    bias1 = torch.randn(N)
+    dA, A64 = _as_bf16(A, abf)
+    dB, B64 = _as_bf16(B, bbf)
+    a = A64.t() if ta else A64
+    b = B64.t() if tb else B64
+    # fp32 operands are rounded to bf16 while staging: compare against the rounded product
+    if not abf:
+        a = a.to(torch.bfloat16).double()
+    if not bbf:
+        b = b.to(torch.bfloat16).double()
+    ref = a @ b + bias1.double()
+    C = torch.empty(M, N, device="cuda")
+    l = lib()
+    ws = torch.empty(l.mlvae_gemm_ex_workspace_size(M, N, K) // 4 + 1, device="cuda")
+    check(l.mlvae_gemm_ex(ta, tb, M, N, K, 1.0, P(dA), abf, dA.shape[1], P(dB), bbf, dB.shape[1],
+                          0.0, P(C), N, P(bias1.cuda()), None, 0, None, 0, 0, 0, P(ws),
+                          ws.numel() * 4, stream()))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 1e-4
+
+
+@pytest.mark.parametrize("bf", [0, 1])
+def test_gemm_ex_epilogues_and_shift(bf):
+    need_gpu()
+    torch.manual_seed(4)
+    M, N, K, T = 96, 48, 304, 19
+    A = torch.randn(K, M)
+    B = torch.randn(K, N)
+    aux = torch.randn(M, N)
+    Cin = torch.randn(M, N)
+    dA, A64 = _as_bf16(A, bf)
+    dB, B64 = _as_bf16(B, bf)
+    A64, B64 = A64.to(torch.bfloat16).double(), B64.to(torch.bfloat16).double()
+    l = lib()
+    ws = torch.empty(l.mlvae_gemm_ex_workspace_size(M, N, K) // 4 + 1, device="cuda")
+    daux = aux.cuda()
+    for epi, shift in [(1, 0), (2, 0), (0, -1), (0, 1)]:
+        C = Cin.cuda()
+        check(l.mlvae_gemm_ex(1, 0, M, N, K, 0.5, P(dA), bf, M, P(dB), bf, N, 2.0, P(C), N, None,
+                              None, epi, P(daux), N, T if shift else 0, shift, P(ws),
+                              ws.numel() * 4, stream()))
+        torch.cuda.synchronize()
+        ref = 0.5 * _ref_gemm(A64, B64, 1, 0, T, shift) + 2.0 * Cin.double()
+        if epi == 1:
+            ref = torch.nn.functional.leaky_relu(ref, 0.01)
+        if epi == 2:
+            ref = ref * torch.where(aux > 0, 1.0, 0.01).double()
+        assert rel_err(C, ref) < 1e-4, (epi, shift)
+
+
+def test_cast_bf16():
+    need_gpu()
+    x = torch.randn(1003) * 100
+    y = torch.empty(1003, dtype=torch.bfloat16, device="cuda")
+    xd = x.cuda()
+    check(lib().mlvae_cast_bf16(x.numel(), P(xd), P(y), stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), x.to(torch.bfloat16))
+
+
 def _lstm_ref(x, p, H):
     """One bidirectional layer from the oracle's explicit loop; returns y and autograd fn."""
     outs = []
