@@ -45,6 +45,33 @@ int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, float alpha, co
                   int a_bf16, int lda, const void* B, int b_bf16, int ldb, float beta, float* C,
                   int ldc, const float* bias1, const float* bias2, int epi, const float* aux,
                   int ldaux, int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream);
+/* The same with epilogue 3 = inter-layer dropout backward: C *= mask(drop_seed, row*ldc + col)
+ * with the mask of mlvae_dropout_ex (keep prob 1 - drop_p, scale 1/(1 - drop_p)), so the dgrad
+ * of the layer above writes the gradient of the dropout input directly
+ * (ref:src/modules/decoder.py:14, nn.LSTM dropout between layers in train mode). */
+int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K, float alpha,
+                       const void* A, int a_bf16, int lda, const void* B, int b_bf16, int ldb,
+                       float beta, float* C, int ldc, const float* bias1, const float* bias2,
+                       int epi, const float* aux, int ldaux, int kshift_T, int kshift,
+                       unsigned long long drop_seed, float drop_p, float* ws, size_t ws_bytes,
+                       void* stream);
+/* Large bf16 GEMMs (256 x 256 tiles, LDS-DMA staging, bf16 operands only, fp32 C):
+ *   C_b = epi( op(A_b) op(B_b) + bias1 + bias2 + beta C_b ),  b = 0 .. batch-1
+ * A_b = A + b*a_bstride (elements), likewise B_b, C_b.  trans_a = 0: A [M,K] k-contiguous;
+ * trans_a = 1: A stored [K,M].  trans_b = 1: B stored [N,K]; trans_b = 0: B stored [K,N].
+ * kshift (+ b*kshift_bstep) time-shifts the rows of a [K,N] B operand as mlvae_gemm does.
+ * epi as mlvae_gemm_ex_drop (3 = dropout mask of (drop_seed, row*ldc + col)).  Operands need
+ * 16-byte aligned bases, lda/ldb and the contiguous extent multiples of 8.  Long-K products
+ * split K into fp32 partial slabs (workspace: mlvae_gemm_bf16_workspace_size) reduced in a fixed
+ * order.  Replaces the LSTM input projection, its dgrad and the weight gradients
+ * (ref:src/modules/decoder.py:14-15,22). */
+size_t mlvae_gemm_bf16_workspace_size(int M, int N, int K, int batch);
+int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch, const void* A,
+                    int lda, long long a_bstride, const void* B, int ldb, long long b_bstride,
+                    float* C, int ldc, long long c_bstride, float beta, const float* bias1,
+                    const float* bias2, int epi, const float* aux, int ldaux, int kshift_T,
+                    int kshift, int kshift_bstep, unsigned long long drop_seed, float drop_p,
+                    float* ws, size_t ws_bytes, void* stream);
 /* y (bf16) = round-to-nearest-even(x), n elements. */
 int mlvae_cast_bf16(size_t n, const float* x, void* y, void* stream);
 

@@ -101,3 +101,34 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// Counter-based Philox-4x32-10 (four 32-bit words per counter), keyed by a 64-bit seed.
+__device__ __forceinline__ void philox4(unsigned long long seed, unsigned long long ctr,
+                                        unsigned out[4]) {
+  unsigned c0 = (unsigned)ctr, c1 = (unsigned)(ctr >> 32), c2 = 0x243F6A88u, c3 = 0x85A308D3u;
+  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+    const unsigned n0 = (unsigned)(p1 >> 32) ^ c1 ^ k0, n2 = (unsigned)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0; c1 = (unsigned)p1; c2 = n2; c3 = (unsigned)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// Inter-layer LSTM dropout mask of flat element i (train mode, ref:src/modules/decoder.py:14):
+// keep iff u < 1-p with u = 24-bit uniform from word (i & 3) of Philox(seed, i >> 2); kept
+// elements are scaled by 1/(1-p) (nn.Dropout).  The forward (dropout kernel / recurrence store
+// path) and the backward (dgrad GEMM epilogue) evaluate the same function: no stored mask.
+__device__ __forceinline__ float dropout_word_scale(unsigned w, float keep, float scale) {
+  return ((w >> 8) * (1.f / 16777216.f)) < keep ? scale : 0.f;
+}
+__device__ __forceinline__ float dropout_scale(unsigned long long seed, unsigned long long i,
+                                               float keep, float scale) {
+  unsigned r[4];
+  philox4(seed, i >> 2, r);
+  const unsigned w = (i & 2) ? ((i & 1) ? r[3] : r[2]) : ((i & 1) ? r[1] : r[0]);
+  return dropout_word_scale(w, keep, scale);
+}

@@ -204,23 +204,9 @@ __global__ void count_frames_kernel(const float* lens, int B, int T, int* out) {
   *out = total_frames(lens, B, T);
 }
 
-// Counter-based standard normals: Philox-4x32-10 keyed by seed, counter = global element index
-// (so a data-parallel shard that passes its global offset draws the same eps as one GPU would).
-__device__ __forceinline__ void philox4(unsigned long long seed, unsigned long long ctr,
-                                        unsigned out[4]) {
-  unsigned c0 = (unsigned)ctr, c1 = (unsigned)(ctr >> 32), c2 = 0x243F6A88u, c3 = 0x85A308D3u;
-  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
-    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
-    const unsigned n0 = (unsigned)(p1 >> 32) ^ c1 ^ k0, n2 = (unsigned)(p0 >> 32) ^ c3 ^ k1;
-    c0 = n0; c1 = (unsigned)p1; c2 = n2; c3 = (unsigned)p0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
-}
-
+// Counter-based standard normals: Philox-4x32-10 (common.h) keyed by seed, counter = global
+// element index (so a data-parallel shard that passes its global offset draws the same eps as
+// one GPU would).
 __global__ __launch_bounds__(256) void randn_kernel(size_t n, unsigned long long seed,
                                                     unsigned long long offset, float* out) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {

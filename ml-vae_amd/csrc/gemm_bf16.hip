@@ -33,9 +33,20 @@ struct G2Args {
   int kshiftT, kshift;
   int splits, kchunk;
   float* ws;
+  unsigned long long dseed;   // EPI_DROPOUT: mask of flat element row*ldc + col
+  float dkeep, dscale;
 };
 
-enum { EPI_NONE = 0, EPI_LRELU = 1, EPI_DLRELU = 2 };
+enum { EPI_NONE = 0, EPI_LRELU = 1, EPI_DLRELU = 2, EPI_DROPOUT = 3 };
+
+// shared epilogue: bias already added; beta * C, then the activation / mask
+__device__ __forceinline__ float epi_apply(const G2Args& g, float val, int row, int col, float* cp) {
+  if (g.beta != 0.f) val += g.beta * *cp;
+  if (g.epi == EPI_LRELU) val = lrelu(val);
+  else if (g.epi == EPI_DLRELU) val *= lrelu_d(g.aux[(size_t)row * g.ldaux + col]);
+  else if (g.epi == EPI_DROPOUT) val *= dropout_scale(g.dseed, (size_t)row * g.ldc + col, g.dkeep, g.dscale);
+  return val;
+}
 
 __device__ __forceinline__ unsigned short bf_bits(float x) { return (unsigned short)f2bf(x); }
 
@@ -285,12 +296,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(G2Args g) {
           wsz[(size_t)row * g.N + col] = acc[i][j][v];
           continue;
         }
-        float val = g.alpha * acc[i][j][v] + b;
         float* cp = g.C + (size_t)row * g.ldc + col;
-        if (g.beta != 0.f) val += g.beta * *cp;
-        if (g.epi == EPI_LRELU) val = lrelu(val);
-        else if (g.epi == EPI_DLRELU) val *= lrelu_d(g.aux[(size_t)row * g.ldaux + col]);
-        *cp = val;
+        *cp = epi_apply(g, g.alpha * acc[i][j][v] + b, row, col, cp);
       }
     }
 }
@@ -305,10 +312,7 @@ __global__ __launch_bounds__(256) void splitk_reduce2(G2Args g) {
     if (g.bias1) val += g.bias1[col];
     if (g.bias2) val += g.bias2[col];
     float* cp = g.C + (size_t)row * g.ldc + col;
-    if (g.beta != 0.f) val += g.beta * *cp;
-    if (g.epi == EPI_LRELU) val = lrelu(val);
-    else if (g.epi == EPI_DLRELU) val *= lrelu_d(g.aux[(size_t)row * g.ldaux + col]);
-    *cp = val;
+    *cp = epi_apply(g, val, row, col, cp);
   }
 }
 
@@ -363,17 +367,23 @@ extern "C" size_t mlvae_gemm_ex_workspace_size(int M, int N, int K) {
   return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
 }
 
-extern "C" int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, float alpha,
-                             const void* A, int a_bf16, int lda, const void* B, int b_bf16,
-                             int ldb, float beta, float* C, int ldc, const float* bias1,
-                             const float* bias2, int epi, const float* aux, int ldaux,
-                             int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream) {
+extern "C" int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K, float alpha,
+                                  const void* A, int a_bf16, int lda, const void* B, int b_bf16,
+                                  int ldb, float beta, float* C, int ldc, const float* bias1,
+                                  const float* bias2, int epi, const float* aux, int ldaux,
+                                  int kshift_T, int kshift, unsigned long long drop_seed,
+                                  float drop_p, float* ws, size_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0 || !C || (K > 0 && (!A || !B))) {
     mlvae_set_error("mlvae_gemm_ex: bad shape/ptr");
     return 1;
   }
   if (M == 0 || N == 0) return 0;
   if (epi == EPI_DLRELU && !aux) { mlvae_set_error("mlvae_gemm_ex: DLRELU needs aux"); return 1; }
+  if (epi == EPI_DROPOUT && !(drop_p >= 0.f && drop_p < 1.f)) {
+    mlvae_set_error("mlvae_gemm_ex: dropout p=%f out of range", drop_p);
+    return 1;
+  }
+  if (epi < EPI_NONE || epi > EPI_DROPOUT) { mlvae_set_error("mlvae_gemm_ex: bad epilogue %d", epi); return 1; }
   if (kshift != 0 && (trans_b || kshift_T <= 0)) {
     mlvae_set_error("mlvae_gemm_ex: kshift needs trans_b = 0, T > 0");
     return 1;
@@ -389,6 +399,7 @@ extern "C" int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, floa
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
   g.alpha = alpha; g.beta = beta; g.bias1 = bias1; g.bias2 = bias2; g.epi = epi; g.aux = aux;
   g.ldaux = ldaux; g.kshiftT = kshift_T; g.kshift = kshift; g.ws = ws;
+  g.dseed = drop_seed; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
   int s, kc;
   gemm2_plan(M, N, K, &s, &kc);
   if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * sizeof(float))) {
@@ -414,6 +425,17 @@ extern "C" int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, floa
     MLVAE_CHECK_LAUNCH();
   }
   return 0;
+}
+
+extern "C" int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, float alpha,
+                             const void* A, int a_bf16, int lda, const void* B, int b_bf16,
+                             int ldb, float beta, float* C, int ldc, const float* bias1,
+                             const float* bias2, int epi, const float* aux, int ldaux,
+                             int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream) {
+  if (epi == EPI_DROPOUT) { mlvae_set_error("mlvae_gemm_ex: dropout epilogue needs mlvae_gemm_ex_drop"); return 1; }
+  return mlvae_gemm_ex_drop(trans_a, trans_b, M, N, K, alpha, A, a_bf16, lda, B, b_bf16, ldb, beta,
+                            C, ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift, 0ull, 0.f, ws,
+                            ws_bytes, stream);
 }
 
 // fp32 -> bf16 (round to nearest even), n elements, 16-byte aligned buffers.

@@ -1,0 +1,333 @@
+// Large bf16 GEMMs of the bf16 train step on gfx950: 256 x 256 tiles, LDS-DMA staging.
+//
+//   C[M,N] = epi( op(A)[M,K] . op(B)[K,N] + bias1[N] + bias2[N] + beta * C )     (C fp32)
+//
+// The products this serves (bf16 operands in HBM, written by the step itself):
+//   input projection  G = X W_ih^T      A [N_fr, din] k-contig, B = W_ih [8H, din] k-contig
+//                     (ref:src/modules/decoder.py:14-15,22, nn.LSTM input part)
+//   dgrad             dX = dG W_ih      A = dG [N_fr, 8H] k-contig, B = W_ih [8H, din] n-contig
+//   weight gradients  dW = dG^T X       A = dG [N_fr, 8H] m-contig, B = X [N_fr, din] n-contig
+//                     (K = B*T frames: split-K; the recurrent dW_hh reads B time-shifted)
+//
+// Structure (cdna_hip_programming.md §5: 256² tile, BK = 64, 8 waves as 2 (M) x 4 (N), each wave
+// 128 x 64 as 8 x 4 v_mfma_f32_16x16x32_bf16 tiles):
+//   * operands go HBM -> LDS with buffer_load ... lds (16 B per lane; the LDS image is lane-linear,
+//     so the bank swizzle is applied to the per-lane SOURCE address); out-of-range chunks read as
+//     zero through the buffer descriptor's range check (offset 0x80000000);
+//   * two LDS buffers (2 x 64 KB): tile k+1 streams in while tile k feeds the MFMAs; one
+//     vmcnt(0) + barrier per K-step;
+//   * k-contiguous operands: [rows][64 k] image (128-B rows), 16-B chunk c of row r stored at slot
+//     c ^ (r & 7); fragments by ds_read_b128;
+//   * m/n-contiguous operands: [64 k][256 m] image (512-B rows), chunk c of k-row r at slot
+//     c ^ f(r), f(r) = 2 * ((r & 3) | ((r >> 3) & 1) << 2); fragments by ds_read_b64_tr_b16 (the
+//     hardware transpose read): conflict-free per 32-lane half;
+//   * XCD-aware bijective tile order; optional batch (gridDim.y) and split-K (gridDim.z, fp32
+//     partial slabs + a fixed-order reduce: deterministic).
+#include "common.h"
+
+namespace {
+
+constexpr int TBM = 256, TBN = 256, TBK = 64;
+constexpr int IMG = TBM * TBK;                               // elements per operand image
+constexpr size_t FAST_LDS = (size_t)2 * 2 * IMG * sizeof(short);  // 128 KB
+constexpr unsigned OOB = 0x80000000u;
+
+struct GFArgs {
+  int M, N, K;
+  const short* A; int lda; long long a_bs;
+  const short* B; int ldb; long long b_bs;
+  float* C; int ldc; long long c_bs;
+  float beta;
+  const float* bias1; const float* bias2;
+  int epi;
+  const float* aux; int ldaux;
+  int kshiftT, kshift, kshift_bstep;
+  unsigned long long dseed; float dkeep, dscale;
+  int splits, kchunk;
+  float* ws;
+};
+
+enum { EPI_NONE = 0, EPI_LRELU = 1, EPI_DLRELU = 2, EPI_DROPOUT = 3 };
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) bf16x4* lds_b4_t;
+
+__device__ __forceinline__ unsigned mc_swz(int r) { return 2u * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+// Issue this wave's 4 LDS-DMA pieces (1 KB each) of one 256 x 64 operand tile.
+//   KC: element (row, k) at p[row * ld + k];   MC: element (row, k) at p[k * ld + row]
+// rows [r0, r0 + 256) bounded by R; k [k0, k0 + 64) bounded by kend (and by the time shift).
+template <bool KC>
+__device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
+                                      int k0, int kend, int shT, int sh, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int piece = wave * 4 + j;
+    const int p = piece * 64 + lane;
+    unsigned off;
+    if constexpr (KC) {
+      const int row = p >> 3, c = (p & 7) ^ (row & 7);
+      const int gr = r0 + row, gk = k0 + 8 * c;
+      off = (gr < R && gk < kend) ? (unsigned)(((size_t)gr * ld + gk) * 2) : OOB;
+    } else {
+      const int kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr);
+      int gk = k0 + kr;
+      const int gr = r0 + 8 * c;
+      bool ok = gk < kend && gr < R;
+      if (sh != 0 && ok) {
+        const int t = gk % shT + sh;
+        ok = t >= 0 && t < shT;
+        gk += sh;
+      }
+      off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+  }
+}
+
+// MFMA 16x16x32 operand fragment: lane l gets rows/cols (base + (l & 15)), k = kk + 8 (l >> 4) + j.
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const short* img, int base, int kk, int lane) {
+  if constexpr (KC) {
+    const int row = base + (lane & 15), c = (kk >> 3) + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * TBK + ((c ^ (row & 7)) << 3));
+  } else {
+    const int g = lane >> 4, i4 = lane & 15, q = i4 >> 2, pp = i4 & 3;
+    const int r1 = kk + 8 * g + q, r2 = r1 + 4;
+    const int c = (base >> 3) + (pp >> 1);
+    const short* a1 = img + r1 * TBM + ((c ^ (int)mc_swz(r1)) << 3) + 4 * (pp & 1);
+    const short* a2 = img + r2 * TBM + ((c ^ (int)mc_swz(r2)) << 3) + 4 * (pp & 1);
+    const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_t)a1);
+    const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_t)a2);
+    return bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
+__device__ __forceinline__ float epi_apply(const GFArgs& g, float val, int row, int col, float* cp) {
+  if (g.beta != 0.f) val += g.beta * *cp;
+  if (g.epi == EPI_LRELU) val = lrelu(val);
+  else if (g.epi == EPI_DLRELU) val *= lrelu_d(g.aux[(size_t)row * g.ldaux + col]);
+  else if (g.epi == EPI_DROPOUT) val *= dropout_scale(g.dseed, (size_t)row * g.ldc + col, g.dkeep, g.dscale);
+  return val;
+}
+
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  short* lds = reinterpret_cast<short*>(smem);   // [buf][A image, B image]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int TM = (g.M + TBM - 1) / TBM, TN = (g.N + TBN - 1) / TBN, ntiles = TM * TN;
+  int tile;
+  {  // XCD-aware bijective order: each XCD works a contiguous run of tiles (shared A panels)
+    const int b = blockIdx.x, xcd = b % 8, local = b / 8, q = ntiles / 8, r = ntiles % 8;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  }
+  const int m0 = (tile / TN) * TBM, n0 = (tile % TN) * TBN;
+  const int bz = blockIdx.y;
+  const short* Ap = g.A + bz * g.a_bs;
+  const short* Bp = g.B + bz * g.b_bs;
+  const int sh = g.kshift + bz * g.kshift_bstep;
+  const auto ra = make_rsrc(Ap, OOB);
+  const auto rb = make_rsrc(Bp, OOB);
+  const int kbeg = blockIdx.z * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage_both = [&](int buf, int k0) {
+    stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+    stage<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+  };
+  if (nk > 0) {
+    stage_both(0, kbeg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
+    const short* As = lds + (cur * 2 + 0) * IMG;
+    const short* Bs = lds + (cur * 2 + 1) * IMG;
+#pragma unroll
+    for (int kk = 0; kk < TBK; kk += 32) {
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = frag<AKC>(As, wm * 128 + i * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile it+1 has landed (this wave's pieces)
+    __syncthreads();                                 // ... everyone's; buffer cur is free
+  }
+
+  // epilogue: lane holds C[m0 + wm*128 + i*16 + 4*(lane>>4) + r][n0 + wn*64 + j*16 + (lane&15)]
+  const bool split = g.splits > 1;
+  float* Cb = g.C + bz * g.c_bs;
+  float* wsz = split ? g.ws + ((size_t)bz * g.splits + blockIdx.z) * (size_t)g.M * g.N : nullptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+    if (col >= g.N) continue;
+    float b = 0.f;
+    if (!split) {
+      if (g.bias1) b += g.bias1[col];
+      if (g.bias2) b += g.bias2[col];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (row >= g.M) continue;
+        if (split) {
+          wsz[(size_t)row * g.N + col] = acc[i][j][r];
+        } else {
+          float* cp = Cb + (size_t)row * g.ldc + col;
+          *cp = epi_apply(g, acc[i][j][r] + b, row, col, cp);
+        }
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
+  const size_t MN = (size_t)g.M * g.N;
+  const int bz = blockIdx.y;
+  const float* ws = g.ws + (size_t)bz * g.splits * MN;
+  float* Cb = g.C + bz * g.c_bs;
+  for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < MN; idx += (size_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < g.splits; ++z) s += ws[z * MN + idx];
+    const int row = (int)(idx / g.N), col = (int)(idx % g.N);
+    if (g.bias1) s += g.bias1[col];
+    if (g.bias2) s += g.bias2[col];
+    float* cp = Cb + (size_t)row * g.ldc + col;
+    *cp = epi_apply(g, s, row, col, cp);
+  }
+}
+
+template <bool AKC, bool BKC>
+int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s) {
+  auto k = gemm256_kernel<AKC, BKC>;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)FAST_LDS) != hipSuccess) {
+      mlvae_set_error("gemm_bf16: cannot reserve %zu B LDS", FAST_LDS);
+      return 2;
+    }
+    attr = true;
+  }
+  k<<<grid, 512, FAST_LDS, s>>>(g);
+  return 0;
+}
+
+// split-K: long-K products (weight gradients over B*T frames) until ~1 workgroup per CU,
+// keeping >= 8 K-steps per split
+void fast_plan(int M, int N, int K, int batch, int* splits, int* kchunk) {
+  const long tiles = (long)((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN) * batch;
+  int s = 1;
+  if (tiles < 256 && K >= TBK * 16) {
+    s = (int)((256 + tiles - 1) / tiles);
+    const int maxs = K / (TBK * 8);
+    if (s > maxs) s = maxs;
+    if (s > 32) s = 32;
+    if (s < 1) s = 1;
+  }
+  int kc = (K + s - 1) / s;
+  kc = (kc + TBK - 1) / TBK * TBK;
+  s = kc > 0 ? (K + kc - 1) / kc : 1;
+  *splits = s < 1 ? 1 : s;
+  *kchunk = kc > 0 ? kc : TBK;
+}
+
+}  // namespace
+
+extern "C" size_t mlvae_gemm_bf16_workspace_size(int M, int N, int K, int batch) {
+  int s, kc;
+  fast_plan(M, N, K, batch < 1 ? 1 : batch, &s, &kc);
+  return s > 1 ? (size_t)s * M * N * (batch < 1 ? 1 : batch) * sizeof(float) : 0;
+}
+
+extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch,
+                               const void* A, int lda, long long a_bstride, const void* B, int ldb,
+                               long long b_bstride, float* C, int ldc, long long c_bstride,
+                               float beta, const float* bias1, const float* bias2, int epi,
+                               const float* aux, int ldaux, int kshift_T, int kshift,
+                               int kshift_bstep, unsigned long long drop_seed, float drop_p,
+                               float* ws, size_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || batch < 1 || !C || (K > 0 && (!A || !B))) {
+    mlvae_set_error("mlvae_gemm_bf16: bad shape/ptr");
+    return 1;
+  }
+  if (M == 0 || N == 0) return 0;
+  if (epi < EPI_NONE || epi > EPI_DROPOUT) { mlvae_set_error("mlvae_gemm_bf16: bad epilogue %d", epi); return 1; }
+  if (epi == EPI_DLRELU && !aux) { mlvae_set_error("mlvae_gemm_bf16: DLRELU needs aux"); return 1; }
+  if (epi == EPI_DROPOUT && !(drop_p >= 0.f && drop_p < 1.f)) {
+    mlvae_set_error("mlvae_gemm_bf16: dropout p=%f out of range", drop_p);
+    return 1;
+  }
+  if ((kshift != 0 || kshift_bstep != 0) && (trans_b || kshift_T <= 0)) {
+    mlvae_set_error("mlvae_gemm_bf16: kshift needs trans_b = 0, T > 0");
+    return 1;
+  }
+  // 16-byte chunks along the contiguous dimension: aligned bases, ld and extent multiples of 8
+  const bool akc = !trans_a, bkc = trans_b;
+  const int acont = akc ? K : M, bcont = bkc ? K : N;
+  if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || (lda % 8) || (ldb % 8) || (acont % 8) ||
+      (bcont % 8) || (a_bstride % 8) || (b_bstride % 8)) {
+    mlvae_set_error("mlvae_gemm_bf16: operands need 16-byte chunks (ld, contiguous extent %% 8)");
+    return 1;
+  }
+  // every in-range byte offset must stay below the descriptor's 2^31 range
+  const size_t a_rows = akc ? (size_t)M : (size_t)K, b_rows = bkc ? (size_t)N : (size_t)K;
+  if ((a_rows * lda + (size_t)(batch - 1) * a_bstride) * 2 >= OOB ||
+      (b_rows * ldb + (size_t)(batch - 1) * b_bstride) * 2 >= OOB) {
+    mlvae_set_error("mlvae_gemm_bf16: operand larger than 2 GB");
+    return 1;
+  }
+  GFArgs g;
+  g.M = M; g.N = N; g.K = K;
+  g.A = static_cast<const short*>(A); g.lda = lda; g.a_bs = a_bstride;
+  g.B = static_cast<const short*>(B); g.ldb = ldb; g.b_bs = b_bstride;
+  g.C = C; g.ldc = ldc; g.c_bs = c_bstride; g.beta = beta;
+  g.bias1 = bias1; g.bias2 = bias2; g.epi = epi; g.aux = aux; g.ldaux = ldaux;
+  g.kshiftT = kshift_T; g.kshift = kshift; g.kshift_bstep = kshift_bstep;
+  g.dseed = drop_seed; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
+  g.ws = ws;
+  int s, kc;
+  fast_plan(M, N, K, batch, &s, &kc);
+  if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
+    s = 1;
+    kc = ((K + TBK - 1) / TBK) * TBK;
+  }
+  if (K == 0) { s = 1; kc = TBK; }
+  g.splits = s; g.kchunk = kc;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), batch, s);
+  int rc;
+  if (akc && bkc) rc = launch_fast<true, true>(g, grid, st);
+  else if (akc) rc = launch_fast<true, false>(g, grid, st);
+  else if (bkc) rc = launch_fast<false, true>(g, grid, st);
+  else rc = launch_fast<false, false>(g, grid, st);
+  if (rc) return rc;
+  MLVAE_CHECK_LAUNCH();
+  if (s > 1) {
+    const size_t MN = (size_t)M * N;
+    int blocks = (int)((MN + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_fast<<<dim3(blocks, batch), 256, 0, st>>>(g);
+    MLVAE_CHECK_LAUNCH();
+  }
+  return 0;
+}

@@ -144,11 +144,18 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
   __shared__ int abort_flag;
 
   const int ngroups = 2 * a.NB;
-  const int gid = blockIdx.x % ngroups, js = blockIdx.x / ngroups;
+  int gid, js;
+  if (a.xcd_local) {
+    gid = blockIdx.x & 7; js = blockIdx.x >> 3;
+    if (gid >= ngroups) return;  // the whole workgroup leaves before any barrier
+  } else {
+    gid = blockIdx.x % ngroups; js = blockIdx.x / ngroups;
+  }
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int H = a.H, T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* W = dir ? a.W1 : a.W0;
+  __shared__ int placement;
 
   // wave w owns M-tile w: lane (bi, q) holds gates i,f,g,o of unit 4w+q, utterance bi.
   // Every wave computes partials of all MT tiles over its quarter of K.
@@ -179,6 +186,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
       }
     }
   }
+  const bool plain_st = a.xcd_local && group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement);
+  if (a.dbg && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
   if (tid == 0) abort_flag = 0;
   __syncthreads();
 
@@ -212,6 +221,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
         const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * a.Kp + kb + EPL * q;
         u32x4 hv[NL];
         unsigned spins = 0;
+        for (int d = (a.dbg_mode >> 5) & 63; d > 0; --d) __builtin_amdgcn_s_sleep(1);  // diag: delayed first sweep
         unsigned long long t_issue = 0;
         while (true) {
           if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
@@ -228,7 +238,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
             if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
             break;
           }
-          __builtin_amdgcn_s_sleep(4);
+          if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
         }
         STAMP(1);
         if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -296,7 +306,15 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
           const float h1 = __shfl(hv, lane + 16, 64);
           const float h2 = __shfl(hv, lane + 32, 64);
           const float h3 = __shfl(hv, lane + 48, 64);
-          if (q == 0) st_granule(xr, (unsigned)(row * sizeof(ET)), pack_bf16(hv, h1, h2, h3, tag));
+          if (q == 0) {
+            const unsigned long long gv = pack_bf16(hv, h1, h2, h3, tag);
+            if (plain_st) {  // same-XCD group: the line stays in the shared L2
+              u32x2 w2 = {(unsigned)gv, (unsigned)(gv >> 32)};
+              __builtin_amdgcn_raw_buffer_store_b64(w2, xr, (unsigned)(row * sizeof(ET)), 0, 0);
+            } else {
+              st_granule(xr, (unsigned)(row * sizeof(ET)), gv);
+            }
+          }
         }
       }
     }
@@ -428,7 +446,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
           if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
           break;
         }
-        __builtin_amdgcn_s_sleep(4);
+        if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
       }
       STAMP(1);
       if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -646,6 +664,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
                                         uc * 16 + half * 8);
       u32x4 pv[NPL];
       unsigned spins = 0;
+      for (int d = (a.dbg_mode >> 5) & 63; d > 0; --d) __builtin_amdgcn_s_sleep(1);  // diag: delayed first sweep
       unsigned long long t_issue = 0;
       while (true) {
         if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
@@ -660,7 +679,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
           if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
           break;
         }
-        __builtin_amdgcn_s_sleep(4);
+        if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
       }
       STAMP(1);
       WSTAMP(8);
@@ -771,6 +790,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
   }
 }
 
+unsigned long long* g_dbg = nullptr;
+int g_dbg_mode = 0;
+
 struct Plan {
   int NB, NJ, HJ, Kp, K4p;   // NJ/HJ of the launch being planned (fwd or bwd)
   bool rs;                   // backward in reduce-scatter form (lstm_bwd_rs_kernel)
@@ -805,10 +827,13 @@ Plan make_plan(int B, int H, int prec, bool fwd) {
   const int hjt = p.HJ > 16 ? p.HJ : 16;
   p.lds = fwd ? (size_t)(prec == PREC_F32 ? 1 : 2) * 4 * (p.HJ / 4) * 64 * 16
               : (size_t)2 * 4 * 16 * hjt * 4;
-  if (p.lds < MIN_LDS) p.lds = MIN_LDS;
-  p.xbytes_fwd = (size_t)2 * p.NB * NSLOT * BG * p.Kp * esz;
+  // > half of the CU's LDS keeps a second recurrence workgroup off the CU; bit 3 of the
+  // diagnostics mode reserves enough to keep a 74 KB GEMM workgroup off it too
+  const size_t min_lds = (g_dbg_mode & 8) ? (size_t)100 * 1024 : (size_t)MIN_LDS;
+  if (p.lds < min_lds) p.lds = min_lds;
+  p.xbytes_fwd = (size_t)2 * p.NB * NSLOT * BG * p.Kp * esz + (size_t)2 * p.NB * p.NJ * sizeof(unsigned);
   p.rs = !fwd && use_rs(H, prec);
-  p.xcd = p.rs && p.NJ <= 32 && 2 * p.NB <= 8;
+  p.xcd = (p.rs || (fwd && prec == PREC_BF16 && p.HJ == 16)) && p.NJ <= 32 && 2 * p.NB <= 8;
   p.xbytes_bwd = p.rs ? (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * 256 * sizeof(short) +
                             (size_t)2 * p.NB * p.NJ * sizeof(unsigned)
                       : (size_t)2 * p.NB * NSLOT * BG * p.K4p * esz;
@@ -833,7 +858,7 @@ int max_batch_per_launch(int H, bool fwd, int prec) {
 
 template <int PREC, int HJ, int NL>
 int launch_nl(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
-  dim3 grid(2 * a.NB * a.NJ);
+  dim3 grid(a.xcd_local ? 8 * a.NJ : 2 * a.NB * a.NJ);
   auto k = fwd ? lstm_fwd_kernel<PREC, HJ, NL> : lstm_bwd_kernel<PREC, HJ, NL>;
   const size_t lds = p.lds;
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -876,9 +901,6 @@ int launch_rs(const LstmArgs& a, const Plan& p, hipStream_t s) {
   return 0;
 }
 
-unsigned long long* g_dbg = nullptr;
-int g_dbg_mode = 0;
-
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
         float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
         unsigned short* yb = nullptr, unsigned short* dgb = nullptr) {
@@ -906,10 +928,13 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     a.xbuf = xbuf; a.err = err; a.dbg = g_dbg; a.dbg_mode = g_dbg_mode;
     a.Yb = yb ? yb + (size_t)b0 * T * 2 * H : nullptr;
     a.dGb = dgb ? dgb + (size_t)b0 * T * 8 * H : nullptr;
-    a.xcd_local = p.xcd && (g_dbg_mode & 2) && device_cus() == 256;
-    a.xtab = p.rs ? reinterpret_cast<unsigned*>(static_cast<char*>(xbuf) +
-                                                (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * 256 * sizeof(short))
-                  : nullptr;
+    // XCD-local groups: on by default for the forward (measured 2.67 vs 2.73 us/step at c2;
+    // bit 2 turns it off), opt-in for the backward (bit 1: no gain inside a training step,
+    // where the side-stream weight-gradient GEMMs want those XCDs)
+    a.xcd_local = p.xcd && device_cus() == 256 && (fwd ? !(g_dbg_mode & 4) : (g_dbg_mode & 2));
+    a.xtab = reinterpret_cast<unsigned*>(
+        static_cast<char*>(xbuf) + (p.rs ? (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * 256 * sizeof(short)
+                                         : (size_t)2 * p.NB * NSLOT * BG * p.Kp * (prec == PREC_F32 ? 4 : 2)));
     // re-initialise the exchange every call: zero fill = stale tag, zero padding
     if (hipMemsetAsync(xbuf, 0, fwd ? p.xbytes_fwd : p.xbytes_bwd, st) != hipSuccess) {
       mlvae_set_error("lstm: memset failed");
@@ -983,7 +1008,9 @@ extern "C" int mlvae_lstm_set_debug(void* buf) {
 // Diagnostics only (timing experiments): bit0 skips the forward's saved-activation stores,
 // bit1 enables XCD-local group placement of the reduce-scatter backward (measured at c2: poll
 // round trip 980 vs 1376 cycles, the same step time, and 3 % slower training steps -- the
-// groups take whole XCDs from the side-stream GEMMs).
+// groups take whole XCDs from the side-stream GEMMs), bit2 disables it for the forward,
+// bit3 reserves 100 KB LDS per recurrence workgroup, bit4 polls with s_sleep 1 instead of 4,
+// bits 5-10 delay the first poll sweep of every step by that many s_sleep 1.
 extern "C" int mlvae_lstm_set_debug_mode(int mode) {
   g_dbg_mode = mode;
   return 0;

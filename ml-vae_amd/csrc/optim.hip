@@ -6,8 +6,8 @@
 //     betas (0.9, 0.999), eps 1e-8, no weight decay, bias-corrected; step counter on device.
 //   bias gradients: deterministic column sums over the B*T rows.
 //   inter-layer LSTM dropout (p = 0.15 in train mode, ref:src/models/test_vanilla_vae/model.yaml:25):
-//     counter-based Philox-4x32-10 keyed by (seed, element index): the backward re-derives the
-//     forward mask instead of storing it.
+//     counter-based Philox-4x32-10 (common.h dropout_scale) keyed by (seed, element index): the
+//     backward re-derives the forward mask (dgrad GEMM epilogue) instead of storing it.
 #include "common.h"
 
 namespace {
@@ -202,39 +202,26 @@ static int colsum_chunks(int N, int C) {
 }
 
 // ---------------------------------------------------------------- dropout
-__device__ __forceinline__ void philox_round(unsigned& c0, unsigned& c1, unsigned& c2, unsigned& c3,
-                                             unsigned k0, unsigned k1) {
-  const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
-  const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
-  const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0;
-  const unsigned hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
-  const unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-  c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-}
-__device__ __forceinline__ unsigned philox_u32(unsigned long long seed, unsigned long long idx) {
-  unsigned c0 = (unsigned)idx, c1 = (unsigned)(idx >> 32), c2 = 0x5851F42Du, c3 = 0x14057B7Eu;
-  unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    philox_round(c0, c1, c2, c3, k0, k1);
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-  return c0;
-}
-
+// one thread per 4 consecutive elements: one Philox call gives all four mask words
 __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __restrict__ x,
                                                       float* __restrict__ y,
                                                       unsigned short* __restrict__ ybf,
                                                       const float* __restrict__ mask,
                                                       unsigned long long seed, float p) {
   const float keep = 1.f - p, scale = 1.f / keep;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    float m;
-    if (mask) m = mask[i];
-    else m = ((philox_u32(seed, i) >> 8) * (1.f / 16777216.f)) < keep ? scale : 0.f;
-    const float v = x[i] * m;
-    if (y) y[i] = v;
-    if (ybf) ybf[i] = (unsigned short)f2bf(v);
+  const size_t nq = (n + 3) / 4;
+  for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (size_t)gridDim.x * 256) {
+    unsigned r[4] = {0u, 0u, 0u, 0u};
+    if (!mask) philox4(seed, q, r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const size_t i = q * 4 + e;
+      if (i >= n) break;
+      const float m = mask ? mask[i] : dropout_word_scale(r[e], keep, scale);
+      const float v = x[i] * m;
+      if (y) y[i] = v;
+      if (ybf) ybf[i] = (unsigned short)f2bf(v);
+    }
   }
 }
 

@@ -18,6 +18,7 @@ Every tensor is row-major [B*T, C]; the flat parameter buffer keeps pairs that a
 launch reads as one matrix adjacent (mean/log_var heads, both LSTM directions).
 """
 import math
+import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
 
@@ -28,7 +29,7 @@ from ._lib import check, lib
 
 PREC = {"fp32": 0, "bf16": 1}
 LOSS = {"likelihood": 0, "mse": 1}
-EPI_NONE, EPI_LRELU, EPI_DLRELU = 0, 1, 2
+EPI_NONE, EPI_LRELU, EPI_DLRELU, EPI_DROPOUT = 0, 1, 2, 3
 
 
 @dataclass
@@ -251,6 +252,9 @@ class VAEEngine:
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
         self.global_offset = 0      # first global utterance index of this shard
+        mode = os.environ.get("MLVAE_LSTM_MODE")  # recurrence diagnostics / A-B switches
+        if mode:
+            lib().mlvae_lstm_set_debug_mode(int(mode))
         if params is not None:
             self.load_reference_params(params)
 
@@ -343,22 +347,32 @@ class VAEEngine:
                                _p(ws), w.gws_bytes, self._stream()), "mlvae_gemm")
 
     def _mm(self, w, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, A_bf=None, B_bf=None, bias1=None,
-            bias2=None, epi=0, aux=None, ldaux=0, kshift_T=0, kshift=0, beta=0.0):
+            bias2=None, epi=0, aux=None, ldaux=0, kshift_T=0, kshift=0, beta=0.0, drop_seed=None):
         """GEMM with each operand given as fp32 (A, B) and/or bf16 (A_bf, B_bf) pointer.
-        bf16 mode runs mlvae_gemm_ex (bf16 operands preferred); fp32 mode the exact kernel."""
+        bf16 mode runs mlvae_gemm_ex (bf16 operands preferred); fp32 mode the exact kernel.
+        drop_seed: fuse the inter-layer dropout backward into the epilogue (bf16 path only).
+        Returns True when that fusion happened."""
         if self.cfg.prec == "bf16":
             a, abf = (A_bf, 1) if A_bf is not None else (A, 0)
             b, bbf = (B_bf, 1) if B_bf is not None else (B, 0)
             if _aligned(a, lda, abf) and _aligned(b, ldb, bbf):
                 ws = w.gws_side if self._on_side else w.gws
+                if drop_seed is not None:
+                    check(lib().mlvae_gemm_ex_drop(ta, tb, M, N, K, 1.0, a, abf, lda, b, bbf, ldb, beta,
+                                                   C, ldc, bias1, bias2, EPI_DROPOUT, aux, ldaux,
+                                                   kshift_T, kshift, drop_seed, self.cfg.dropout,
+                                                   _p(ws), w.gws_bytes, self._stream()),
+                          "mlvae_gemm_ex_drop")
+                    return True
                 check(lib().mlvae_gemm_ex(ta, tb, M, N, K, 1.0, a, abf, lda, b, bbf, ldb, beta, C,
                                           ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift,
                                           _p(ws), w.gws_bytes, self._stream()), "mlvae_gemm_ex")
-                return
+                return False
         if A is None or B is None:
             raise RuntimeError("GEMM operand exists only as bf16 but is not 16-byte aligned")
         self._gemm(w, ta, tb, M, N, K, A, lda, B, ldb, C, ldc, bias1=bias1, bias2=bias2, epi=epi,
                    aux=aux, ldaux=ldaux, kshift_T=kshift_T, kshift=kshift, beta=beta)
+        return False
 
     def _colsum(self, w, N, Cn, src, ld, out, out2=None):
         ws = w.gws_side if self._on_side else w.gws
@@ -593,15 +607,24 @@ class VAEEngine:
                 else:
                     self._colsum(w, N, 8 * H, _p(dG), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
                                  gp(f"decoder.rnn.bias_hh_l{li}"))
-            self._side(wgl)
+            # The dgrad (+ dropout backward) is the critical path into the next BPTT; the
+            # weight gradients go to the side stream after it (so they overlap that BPTT, not
+            # this GEMM).  Below the bottom layer nothing waits on the dgrad: its weight
+            # gradients, the step's longest tail, go first.
+            if li == 0:
+                self._side(wgl)
             dx = w.dZs if li == 0 else w.dY[li - 1]
-            self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
-                     self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din, A_bf=pgb(dG_bf),
-                     B_bf=wb(f"decoder.rnn.weight_ih_l{li}"))
-            if li > 0 and xin is not w.Y[li - 1]:  # dropout between layers li-1 and li
-                seed, mask_ptr = w._drop_seed[li - 1]
+            drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
+            seed, mask_ptr = w._drop_seed[li - 1] if drop else (None, None)
+            fused = self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
+                             self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din,
+                             A_bf=pgb(dG_bf), B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
+                             drop_seed=seed if (drop and mask_ptr is None) else None)
+            if drop and not fused:
                 check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
                       "dropout_bwd")
+            if li > 0:
+                self._side(wgl)
         # ---- encoder
         w_kl, _ = self.loss_weights()
         check(l.mlvae_reparam_kl_bwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(w.lens), count,

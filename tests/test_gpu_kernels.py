@@ -228,3 +228,36 @@ def test_lstm_layer_fwd_bwd(prec, tol, B, T, H, D):
                                ws.numel() * 4, stream()))
         torch.cuda.synchronize()
         assert rel_err(out, ref) < tol * 5
+
+
+def test_dropout_mask_statistics_and_fused_backward():
+    """Inter-layer dropout (ref:src/modules/decoder.py:14, nn.LSTM dropout=0.15 in train mode):
+    the forward kernel keeps ~85 % of elements scaled by 1/0.85, and the dgrad GEMM epilogue
+    (mlvae_gemm_ex_drop, epilogue 3) applies bit-for-bit the same mask to its output."""
+    need_gpu()
+    l = lib()
+    torch.manual_seed(11)
+    p, seed = 0.15, 987654321
+    M, N, K = 300, 136, 256
+    x = torch.ones(M * N, device="cuda")
+    y = torch.empty_like(x)
+    check(l.mlvae_dropout_ex(x.numel(), P(x), P(y), None, None, seed, p, stream()))
+    torch.cuda.synchronize()
+    vals = sorted(set(torch.unique(y).tolist()))
+    assert len(vals) == 2 and vals[0] == 0.0 and abs(vals[1] - 1.0 / (1.0 - p)) < 1e-6, vals
+    keep = (y != 0).double().mean().item()
+    assert abs(keep - (1 - p)) < 0.01, keep
+    # fused epilogue == GEMM then dropout kernel (same seed, same flat index row*N + col)
+    A = torch.randn(M, K).to(torch.bfloat16).cuda()
+    B = torch.randn(K, N).to(torch.bfloat16).cuda()
+    ws = torch.empty(l.mlvae_gemm_ex_workspace_size(M, N, K) // 4 + 1, device="cuda")
+    C0 = torch.empty(M, N, device="cuda")
+    C1 = torch.empty(M, N, device="cuda")
+    check(l.mlvae_gemm_ex(0, 0, M, N, K, 1.0, A.data_ptr(), 1, K, B.data_ptr(), 1, N, 0.0, P(C0), N,
+                          None, None, 0, None, 0, 0, 0, P(ws), ws.numel() * 4, stream()))
+    check(l.mlvae_dropout(C0.numel(), P(C0), P(C0), None, seed, p, stream()))
+    check(l.mlvae_gemm_ex_drop(0, 0, M, N, K, 1.0, A.data_ptr(), 1, K, B.data_ptr(), 1, N, 0.0,
+                               P(C1), N, None, None, 3, None, 0, 0, 0, seed, p, P(ws),
+                               ws.numel() * 4, stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1)

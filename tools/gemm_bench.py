@@ -1,5 +1,5 @@
-"""Time the train step's big GEMM shapes (c2) through mlvae_gemm (fp32 operands) and
-mlvae_gemm_ex (bf16 operands).  usage: python tools/gemm_bench.py"""
+"""Time the train step's big GEMM shapes (c2, bf16 operands): mlvae_gemm_ex (128² register-staged)
+against mlvae_gemm_bf16 (256² LDS-DMA).  usage: python tools/gemm_bench.py"""
 import os
 import sys
 
@@ -10,33 +10,35 @@ from mlvae_hip._lib import check, lib  # noqa: E402
 
 N, H, D = 16000, 512, 1024
 SHAPES = [  # name, ta, tb, M, Ncols, K
-    ("fwd proj  Y=X W^T", 0, 1, N, 8 * H, D),
-    ("dgrad     dX=dG W", 0, 0, N, D, 8 * H),
-    ("wgrad ih  dG^T X ", 1, 0, 8 * H, D, N),
-    ("wgrad hh  dG^T h ", 1, 0, 4 * H, H, N),
+    ("fwd proj  Y=X W^T  ", 0, 1, N, 8 * H, D),
+    ("dgrad     dX=dG W  ", 0, 0, N, D, 8 * H),
+    ("dgrad     dX=dG W^T", 0, 1, N, D, 8 * H),
+    ("wgrad ih  dG^T X   ", 1, 0, 8 * H, D, N),
+    ("wgrad hh  dG^T h   ", 1, 0, 4 * H, H, N),
+    ("4096^3             ", 0, 1, 4096, 4096, 4096),
 ]
 
 
-def run(ta, tb, M, Nc, K, ex, abf, iters=10):
+def run(ta, tb, M, Nc, K, fast, iters=10):
     l = lib()
-    dt = torch.bfloat16 if abf else torch.float32
-    A = (torch.randn(K, M) if ta else torch.randn(M, K)).to(dt).cuda()
-    B = (torch.randn(Nc, K) if tb else torch.randn(K, Nc)).to(dt).cuda()
+    A = (torch.rand(K, M) if ta else torch.rand(M, K)).sub(0.5).to(torch.bfloat16).cuda()
+    B = (torch.rand(Nc, K) if tb else torch.rand(K, Nc)).sub(0.5).to(torch.bfloat16).cuda()
     C = torch.empty(M, Nc, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    wsz = (l.mlvae_gemm_ex_workspace_size if ex else l.mlvae_gemm_workspace_size)(M, Nc, K)
+    wsz = l.mlvae_gemm_bf16_workspace_size(M, Nc, K, 1) if fast else l.mlvae_gemm_ex_workspace_size(M, Nc, K)
     ws = torch.empty(wsz // 4 + 1, device="cuda")
 
     def call():
-        if ex:
-            check(l.mlvae_gemm_ex(ta, tb, M, Nc, K, 1.0, A.data_ptr(), abf, A.shape[1], B.data_ptr(),
-                                  abf, B.shape[1], 0.0, C.data_ptr(), Nc, None, None, 0, None, 0, 0, 0,
-                                  ws.data_ptr(), ws.numel() * 4, s))
+        if fast:
+            check(l.mlvae_gemm_bf16(ta, tb, M, Nc, K, 1, A.data_ptr(), A.shape[1], 0, B.data_ptr(),
+                                    B.shape[1], 0, C.data_ptr(), Nc, 0, 0.0, None, None, 0, None, 0,
+                                    0, 0, 0, 0, 0.0, ws.data_ptr(), ws.numel() * 4, s))
         else:
-            check(l.mlvae_gemm(1, ta, tb, M, Nc, K, 1.0, A.data_ptr(), A.shape[1], B.data_ptr(),
-                               B.shape[1], 0.0, C.data_ptr(), Nc, None, None, 0, None, 0, 0, 0,
-                               ws.data_ptr(), ws.numel() * 4, s))
-    call()
+            check(l.mlvae_gemm_ex(ta, tb, M, Nc, K, 1.0, A.data_ptr(), 1, A.shape[1], B.data_ptr(),
+                                  1, B.shape[1], 0.0, C.data_ptr(), Nc, None, None, 0, None, 0, 0, 0,
+                                  ws.data_ptr(), ws.numel() * 4, s))
+    for _ in range(3):
+        call()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -51,10 +53,10 @@ def run(ta, tb, M, Nc, K, ex, abf, iters=10):
 def main():
     for name, ta, tb, M, Nc, K in SHAPES:
         r = []
-        for ex, abf in ((0, 0), (1, 0), (1, 1)):
-            ms, tf = run(ta, tb, M, Nc, K, ex, abf)
+        for fast in (0, 1):
+            ms, tf = run(ta, tb, M, Nc, K, fast)
             r.append(f"{ms * 1e3:7.1f} us {tf:6.1f} TF")
-        print(f"{name}  M={M:5d} N={Nc:5d} K={K:5d} | old fp32-in: {r[0]} | ex fp32-in: {r[1]} | ex bf16-in: {r[2]}")
+        print(f"{name} M={M:5d} N={Nc:5d} K={K:5d} | gemm_ex: {r[0]} | gemm_bf16 256²: {r[1]}", flush=True)
 
 
 if __name__ == "__main__":
