@@ -74,6 +74,9 @@ int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch, co
                     float* ws, size_t ws_bytes, void* stream);
 /* y (bf16) = round-to-nearest-even(x), n elements. */
 int mlvae_cast_bf16(size_t n, const float* x, void* y, void* stream);
+/* y [cols, rows] (bf16) = transpose of x [rows, cols] (fp32, row-major): the k-contiguous copy of
+ * an LSTM input weight that the dgrad dX = dG W_ih reads (ref:src/modules/decoder.py:14-15). */
+int mlvae_cast_bf16_t(int rows, int cols, const float* x, void* y, void* stream);
 
 /* Bidirectional LSTM layer recurrence, both directions in one persistent launch.
  * gates [B*T, 8H]: in = x W_ih^T + b_ih + b_hh (cols [0,4H) forward, [4H,8H) reverse);

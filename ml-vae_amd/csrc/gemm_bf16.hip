@@ -466,3 +466,32 @@ extern "C" int mlvae_cast_bf16(size_t n, const float* x, void* y, void* stream) 
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
+
+// y[c][r] (bf16) = x[r][c] (fp32): transposed bf16 copy of a [rows, cols] weight (ld = cols),
+// so a dgrad dX = dG W reads W^T k-contiguous.  32 x 32 tiles through LDS.
+__global__ __launch_bounds__(256) void cast_bf16_t_kernel(int rows, int cols, const float* __restrict__ x,
+                                                          unsigned short* __restrict__ y) {
+  __shared__ float t[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r0 + ty + 8 * k, c = c0 + tx;
+    t[ty + 8 * k][tx] = (r < rows && c < cols) ? x[(size_t)r * cols + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + ty + 8 * k, r = r0 + tx;
+    if (c < cols && r < rows) y[(size_t)c * rows + r] = bf_bits(t[tx][ty + 8 * k]);
+  }
+}
+
+extern "C" int mlvae_cast_bf16_t(int rows, int cols, const float* x, void* y, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (!x || !y) { mlvae_set_error("mlvae_cast_bf16_t: null pointer"); return 1; }
+  dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+  cast_bf16_t_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(rows, cols, x, static_cast<unsigned short*>(y));
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}

@@ -161,42 +161,54 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wn * 64 + j * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) af[i] = frag<AKC>(As, wm * 128 + i * 16, kk, lane);
+      // operands swapped (D = B^T A^T): a lane's 4 results are 4 consecutive columns of one
+      // row, so the epilogue stores 16 B per lane
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile it+1 has landed (this wave's pieces)
     __syncthreads();                                 // ... everyone's; buffer cur is free
   }
 
-  // epilogue: lane holds C[m0 + wm*128 + i*16 + 4*(lane>>4) + r][n0 + wn*64 + j*16 + (lane&15)]
+  // epilogue: lane holds C[m0 + wm*128 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
   const bool split = g.splits > 1;
   float* Cb = g.C + bz * g.c_bs;
   float* wsz = split ? g.ws + ((size_t)bz * g.splits + blockIdx.z) * (size_t)g.M * g.N : nullptr;
+  const bool vec = (g.ldc % 4) == 0 && (((uintptr_t)Cb) % 16) == 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+    const int col = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
     if (col >= g.N) continue;
-    float b = 0.f;
+    f32x4 b = {0.f, 0.f, 0.f, 0.f};
     if (!split) {
-      if (g.bias1) b += g.bias1[col];
-      if (g.bias2) b += g.bias2[col];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 128 + i * 16 + 4 * (lane >> 4) + r;
-        if (row >= g.M) continue;
-        if (split) {
-          wsz[(size_t)row * g.N + col] = acc[i][j][r];
-        } else {
-          float* cp = Cb + (size_t)row * g.ldc + col;
-          *cp = epi_apply(g, acc[i][j][r] + b, row, col, cp);
+        if (col + r < g.N) {
+          if (g.bias1) b[r] += g.bias1[col + r];
+          if (g.bias2) b[r] += g.bias2[col + r];
         }
       }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = m0 + wm * 128 + i * 16 + (lane & 15);
+      if (row >= g.M) continue;
+      if (split) {  // N % 4 == 0 whenever split (checked on the host)
+        *reinterpret_cast<f32x4*>(wsz + (size_t)row * g.N + col) = acc[i][j];
+        continue;
+      }
+      float* cp = Cb + (size_t)row * g.ldc + col;
+      if (vec && col + 3 < g.N && g.beta == 0.f && g.epi == EPI_NONE) {
+        *reinterpret_cast<f32x4*>(cp) = acc[i][j] + b;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (col + r < g.N) cp[r] = epi_apply(g, acc[i][j][r] + b[r], row, col + r, cp + r);
+      }
+    }
   }
 }
 
@@ -307,7 +319,7 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   g.ws = ws;
   int s, kc;
   fast_plan(M, N, K, batch, &s, &kc);
-  if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
+  if (s > 1 && (N % 4 != 0 || !ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
     s = 1;
     kc = ((K + TBK - 1) / TBK) * TBK;
   }

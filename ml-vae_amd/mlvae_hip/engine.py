@@ -157,6 +157,7 @@ class _Work:
         self.Ydb = ([torch.empty(N, 2 * H, **b16) if cfg.dropout > 0 else None for _ in range(L - 1)]
                     if self.bf else None)
         self.dGb = [torch.empty(N, 8 * H, **b16) for _ in range(L)] if self.bf else None
+        self.Zb = torch.empty(N, Z, **b16) if self.bf else None  # first layer's GEMM operand
         if self.bf:
             self.Yd = [None] * (L - 1)  # the dropout output exists as bf16 only
         self.P1 = torch.empty(N, 2 * C, **f)
@@ -189,8 +190,10 @@ class _Work:
         for li in range(L):
             din = Z if li == 0 else 2 * H
             shapes += [(N, 8 * H, din), (8 * H, din, N)]
-        ws = max(max(l.mlvae_gemm_workspace_size(m, n, k), l.mlvae_gemm_ex_workspace_size(m, n, k))
+        ws = max(max(l.mlvae_gemm_workspace_size(m, n, k), l.mlvae_gemm_ex_workspace_size(m, n, k),
+                     l.mlvae_gemm_bf16_workspace_size(m, n, k, 1))
                  for m, n, k in shapes)
+        ws = max(ws, l.mlvae_gemm_bf16_workspace_size(4 * H, H, N, 2))  # both directions' dW_hh
         cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
         self.gws = torch.empty(max(ws, cs, 16) // 4 + 1, **f)
         self.gws_side = torch.empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
@@ -236,6 +239,11 @@ class VAEEngine:
         self.hyp = torch.zeros(4, **f)
         # bf16 mode: bf16 copy of the weights, refreshed at the start of every forward
         self.flat_bf = torch.empty(n, device=self.device, dtype=torch.bfloat16) if cfg.prec == "bf16" else None
+        # bf16 mode: k-contiguous W_ih^T [din, 8H] of the layers whose dgrad runs on the 256² GEMM
+        self.wih_t = {}
+        if cfg.prec == "bf16":
+            for li in range(1, cfg.L):
+                self.wih_t[li] = torch.empty(2 * cfg.H * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
         self.nparts = lib().mlvae_sumsq_partials_count(n)
         self.sq_parts = torch.zeros(self.nparts, device=self.device, dtype=torch.float64)
         self.seed = seed
@@ -374,6 +382,16 @@ class VAEEngine:
                    aux=aux, ldaux=ldaux, kshift_T=kshift_T, kshift=kshift, beta=beta)
         return False
 
+    def _fast(self, w, ta, tb, M, N, K, A_bf, lda, B_bf, ldb, C, ldc, batch=1, a_bs=0, b_bs=0,
+              c_bs=0, bias1=None, bias2=None, kshift_T=0, kshift=0, kstep=0, drop_seed=None):
+        """bf16 256² LDS-DMA GEMM (mlvae_gemm_bf16) over bf16 operands: the step's big products."""
+        ws = w.gws_side if self._on_side else w.gws
+        epi, p = (EPI_DROPOUT, self.cfg.dropout) if drop_seed is not None else (EPI_NONE, 0.0)
+        check(lib().mlvae_gemm_bf16(ta, tb, M, N, K, batch, A_bf, lda, a_bs, B_bf, ldb, b_bs, C, ldc,
+                                    c_bs, 0.0, bias1, bias2, epi, None, 0, kshift_T, kshift, kstep,
+                                    drop_seed or 0, p, _p(ws), w.gws_bytes, self._stream()),
+              "mlvae_gemm_bf16")
+
     def _colsum(self, w, N, Cn, src, ld, out, out2=None):
         ws = w.gws_side if self._on_side else w.gws
         check(lib().mlvae_colsum(N, Cn, src, ld, out, out2, 0.0, _p(ws), w.gws_bytes,
@@ -433,6 +451,10 @@ class VAEEngine:
         X = _p(x)
         if self.flat_bf is not None:  # this step's weights as bf16 GEMM operands
             check(l.mlvae_cast_bf16(self.layout.total, _p(self.flat), _pb(self.flat_bf), s), "cast_bf16")
+            if train:
+                for li, dst in self.wih_t.items():
+                    check(l.mlvae_cast_bf16_t(8 * cfg.H, 2 * cfg.H, self._ptr(f"decoder.rnn.weight_ih_l{li}"),
+                                              _pb(dst), s), "cast_bf16_t")
         wb = self._wb
         count = None
         if self.world > 1:
@@ -459,15 +481,23 @@ class VAEEngine:
         # ---- decoder BiLSTM (ref:src/modules/decoder.py:22)
         # layer input as (fp32 tensor or None, bf16 tensor or None, width)
         xin, xin_bf, din = w.Zs, None, Z
+        if w.bf:
+            check(l.mlvae_cast_bf16(N * Z, _p(w.Zs), _pb(w.Zb), s), "cast_bf16")
+            xin_bf = w.Zb
         w.layer_in = []
         for li in range(cfg.L):
             w.layer_in.append((xin, xin_bf, din))
-            self._mm(w, 0, 1, N, 8 * H, din, _p(xin) if xin is not None else None, din,
-                     self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
-                     A_bf=_pb(xin_bf) if xin_bf is not None else None,
-                     B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
-                     bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
-                     bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+            if w.bf and din % 8 == 0:  # input projection on the 256² GEMM
+                self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), din, wb(f"decoder.rnn.weight_ih_l{li}"),
+                           din, _p(w.G[li]), 8 * H, bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                           bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+            else:
+                self._mm(w, 0, 1, N, 8 * H, din, _p(xin) if xin is not None else None, din,
+                         self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
+                         A_bf=_pb(xin_bf) if xin_bf is not None else None,
+                         B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
+                         bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                         bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
             with self._timed("lstm_fwd"):
                 check(l.mlvae_lstm_fwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
@@ -591,14 +621,23 @@ class VAEEngine:
             Ybl = w.Yb[li] if w.bf else None
 
             def wgl(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, Ybl=Ybl):
-                self._mm(w, 1, 0, 8 * H, din, N, pg(dG), 8 * H, pg(xin), din,
-                         gp(f"decoder.rnn.weight_ih_l{li}"), din, A_bf=pgb(dG_bf), B_bf=pgb(xin_bf))
-                self._mm(w, 1, 0, 4 * H, H, N, pg(dG), 8 * H, _p(w.Y[li]), 2 * H,
-                         gp(f"decoder.rnn.weight_hh_l{li}"), H, A_bf=pgb(dG_bf), B_bf=pgb(Ybl),
-                         kshift_T=T, kshift=-1)
-                self._mm(w, 1, 0, 4 * H, H, N, pg(dG, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
-                         gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, A_bf=pgb(dG_bf, 4 * H),
-                         B_bf=pgb(Ybl, H), kshift_T=T, kshift=1)
+                if dG_bf is not None and xin_bf is not None and din % 8 == 0 and H % 8 == 0:
+                    # 256² GEMMs: dW_ih = dG^T X, and both directions' dW_hh = sum_t dG_t^T h_{t-/+1}
+                    # in one batched launch (the two weights are adjacent in the flat gradient)
+                    self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), din,
+                               gp(f"decoder.rnn.weight_ih_l{li}"), din)
+                    self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
+                               gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
+                               c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                else:
+                    self._mm(w, 1, 0, 8 * H, din, N, pg(dG), 8 * H, pg(xin), din,
+                             gp(f"decoder.rnn.weight_ih_l{li}"), din, A_bf=pgb(dG_bf), B_bf=pgb(xin_bf))
+                    self._mm(w, 1, 0, 4 * H, H, N, pg(dG), 8 * H, _p(w.Y[li]), 2 * H,
+                             gp(f"decoder.rnn.weight_hh_l{li}"), H, A_bf=pgb(dG_bf), B_bf=pgb(Ybl),
+                             kshift_T=T, kshift=-1)
+                    self._mm(w, 1, 0, 4 * H, H, N, pg(dG, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
+                             gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, A_bf=pgb(dG_bf, 4 * H),
+                             B_bf=pgb(Ybl, H), kshift_T=T, kshift=1)
                 if dG_bf is not None:
                     ws = w.gws_side if self._on_side else w.gws
                     check(lib().mlvae_colsum_ex(N, 8 * H, _pb(dG_bf), 1, 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
@@ -616,10 +655,16 @@ class VAEEngine:
             dx = w.dZs if li == 0 else w.dY[li - 1]
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
             seed, mask_ptr = w._drop_seed[li - 1] if drop else (None, None)
-            fused = self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
-                             self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din,
-                             A_bf=pgb(dG_bf), B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
-                             drop_seed=seed if (drop and mask_ptr is None) else None)
+            if dG_bf is not None and li in self.wih_t and din >= 256:
+                # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy
+                self._fast(w, 0, 1, N, din, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[li]), 8 * H,
+                           _p(dx), din, drop_seed=seed if (drop and mask_ptr is None) else None)
+                fused = drop and mask_ptr is None
+            else:
+                fused = self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
+                                 self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din,
+                                 A_bf=pgb(dG_bf), B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
+                                 drop_seed=seed if (drop and mask_ptr is None) else None)
             if drop and not fused:
                 check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
                       "dropout_bwd")

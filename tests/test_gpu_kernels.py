@@ -146,6 +146,17 @@ def test_cast_bf16():
     assert torch.equal(y.cpu(), x.to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("rows,cols", [(4096, 1024), (4096, 32), (37, 70)])
+def test_cast_bf16_transposed(rows, cols):
+    need_gpu()
+    x = torch.randn(rows, cols)
+    y = torch.empty(cols, rows, dtype=torch.bfloat16, device="cuda")
+    xd = x.cuda()
+    check(lib().mlvae_cast_bf16_t(rows, cols, P(xd), P(y), stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), x.t().contiguous().to(torch.bfloat16))
+
+
 def _lstm_ref(x, p, H):
     """One bidirectional layer from the oracle's explicit loop; returns y and autograd fn."""
     outs = []
