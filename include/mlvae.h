@@ -121,6 +121,25 @@ int mlvae_recon(int B, int T, int F, int loss_type, const float* mux, int ldmu, 
                 int ldlv, const float* x, int ldx, const float* lens, const int* count,
                 float* rec_out, float* partials, const float* drec, float rec_scale, float* dmux,
                 float* dlvx, void* stream);
+/* Fused decoder heads (bf16 mode): both FCBlock([2H, C, C, F]) heads forward, the recon loss
+ * (masked partial sums into partials[mlvae_heads_partials_count(B, T)], read by
+ * mlvae_elbo_finalize) and, when train, its gradient (scale rec_scale / (count * F)), both heads
+ * backward and dy = d loss / d rnn_out [B*T, 2H], in one launch.  y_bf16 [B*T, 2H] bf16 rnn output;
+ * w1_bf16 [2C, 2H] the two heads' stacked first-layer weights (bf16), w1t_bf16 its transpose
+ * [2H, 2C] (train); b1 [2C]; w2*/w3* fp32 [C, C] / [F, C].  Outputs fp32: p1 [B*T, 2C], p2m/p2v
+ * [B*T, C], mux/lvx [B*T, F]; train: dmux/dlvx (dlvx NULL for mse), dp2m/dp2v, dp1, dy.
+ * mlvae_heads_supported(C, F, 2H): C == 64, F in {64, 80}, 2H % 128 == 0.  Replaces
+ * ref:src/modules/decoder.py:24-25,37-53 + ref:src/modules/fc_block.py:9-16 and their autograd. */
+int mlvae_heads_partials_count(int B, int T);
+int mlvae_heads_supported(int C, int F, int H2);
+int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int train,
+                      const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
+                      const float* w2m, const float* b2m, const float* w3m, const float* b3m,
+                      const float* w2v, const float* b2v, const float* w3v, const float* b3v,
+                      const float* x, const float* lens, const int* count, float rec_scale,
+                      float* p1, float* p2m, float* p2v, float* mux, float* lvx, float* dmux,
+                      float* dlvx, float* dp2m, float* dp2v, float* dp1, float* dy,
+                      float* partials, void* stream);
 /* out[3] = {kld_loss, recon_loss, w_kl*kld + w_rec*recon}
  * (ref:src/utils/data_utils.py:67-104, ref:src/models/md_model.py:189-213). */
 int mlvae_elbo_finalize(const float* kl_partials, int nk, const float* rec_partials, int nr,

@@ -1,0 +1,398 @@
+// Fused decoder heads of the VAE train step (bf16 mode): both FCBlock heads forward, the
+// reconstruction loss with its masked partial sums and gradient, both heads backward and the
+// gradient wrt the BiLSTM output, in ONE launch over 64-frame row tiles.
+//
+//   mean_fc / log_var_fc = FCBlock([2H, C, C, F])    ref:src/modules/decoder.py:16-17,24-25
+//     P1 = lrelu(Y W1^T + b1)      (the two heads' first layers stacked: W1 [2C, 2H])
+//     P2 = lrelu(P1_h W2_h^T + b2_h)                 ref:src/modules/fc_block.py:9-16
+//     OUT_h = P2_h W3_h^T + b3_h   (mean, log_var)
+//   compute_recon_loss                               ref:src/modules/decoder.py:37-53
+//     likelihood: 0.5 (log 2pi + lv + (x - mu)^2 / (e^lv + 1e-5));  mse: (x - mu)^2
+//   apply_lens_to_loss mask / count (gradient scale w_rec / (count * F))
+//                                                    ref:src/utils/data_utils.py:67-104
+//   backward: dOUT -> dP2 = (dOUT W3) * lrelu'(P2) -> dP1 = (dP2 W2) * lrelu'(P1) -> dY = dP1 W1
+//
+// It replaces 12-14 dependent launches (GEMMs of 13-40 us each at M = B*T, N <= 128, plus the
+// recon kernel) on the step's critical path between the last forward recurrence and the first
+// BPTT.  Every product is v_mfma_f32_16x16x32_bf16 with fp32 accumulation; operands swapped
+// (D^T = B^T A^T) so a lane's four results are four consecutive columns of one row (16-byte
+// stores, 8-byte LDS writes).
+//
+// Workgroup = 64 rows, 4 waves; wave w owns rows 16w .. 16w+15 through every stage, so the
+// per-row LDS images are private to a wave and only the shared weight images and the staged
+// W1 / W1^T chunks need workgroup barriers.  Weight images are built per workgroup from the
+// fp32 parameters (two row-major, two transposed; bf16, padded rows: conflict-free 16-lane
+// ds_read_b128).  Saved tensors for the weight-gradient GEMMs (side stream) are written fp32.
+#include "common.h"
+
+namespace {
+
+constexpr float LOG_2PI_H = 1.8378770351409912f;  // fp32(log(2 pi)), ref:src/modules/decoder.py:42
+constexpr int RT = 64;                             // rows per workgroup
+
+struct HeadArgs {
+  int B, T, N, H2, loss_type, train;
+  const unsigned short* Y;    // [N, H2] bf16
+  const unsigned short* W1;   // [2C, H2] bf16
+  const unsigned short* W1t;  // [H2, 2C] bf16 (train)
+  const float* b1;            // [2C]
+  const float* W2[2]; const float* b2[2]; const float* W3[2]; const float* b3[2];
+  const float* x; const float* lens; const int* count; float rec_scale;
+  float* P1; float* P2[2]; float* OUT[2]; float* dOUT[2]; float* dP2[2]; float* dP1; float* dY;
+  float* partials;
+};
+
+__device__ __forceinline__ bf16x8 lds8(const short* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void st4bf(short* p, f32x4 v) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+}
+__device__ __forceinline__ bf16x8 gld8(const unsigned short* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int C, int F>
+__global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
+  constexpr int C2 = 2 * C, FK = (F + 31) / 32 * 32;
+  constexpr int LC = C + 8, LF = FK + 8, L2C = C2 + 8, LS1 = 64 + 8;
+  constexpr int NC = C / 16, NF = F / 16, NC2 = C2 / 16;
+  // LDS image offsets (shorts)
+  constexpr int O_W2I = 0, O_W2T = O_W2I + 2 * C * LC, O_W3I = O_W2T + 2 * C * LC;
+  constexpr int O_W3T = O_W3I + 2 * F * LC, O_P1 = O_W3T + 2 * C * LF;
+  constexpr int O_P2 = O_P1 + RT * L2C, O_DO = O_P2 + 2 * RT * LC, O_END = O_DO + 2 * RT * LF;
+  constexpr int O_S1 = O_P2;   // stage-1 W1 chunks (2 x [2C][72]) alias P2 + dOUT images
+  constexpr int O_S7 = O_W3I;  // stage-7 W1^T chunk ([128][L2C]) aliases the W3 images
+  static_assert(O_S1 + 2 * C2 * LS1 <= O_END, "stage-1 staging overlaps");
+  static_assert(O_S7 + 128 * L2C <= O_P1, "stage-7 staging overlaps");
+  static_assert(O_END * 2 <= 160 * 1024, "LDS budget");
+  extern __shared__ __attribute__((aligned(16))) short sm[];
+  __shared__ float red[4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int r0 = blockIdx.x * RT;
+  const int lrow = 16 * wave + l15;          // this lane's row within the tile (operand / result)
+  const int grow = r0 + lrow;                // global frame row
+  const bool rv = grow < a.N;
+  const int H2 = a.H2;
+
+  // ---- stage 0: weight images (bf16) from the fp32 parameters
+  for (int idx = tid; idx < 2 * C * (C / 4); idx += 256) {
+    const int h = idx / (C * C / 4), rem = idx % (C * C / 4), n = rem / (C / 4), k = (rem % (C / 4)) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(a.W2[h] + n * C + k);
+    st4bf(sm + O_W2I + h * C * LC + n * LC + k, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm[O_W2T + h * C * LC + (k + i) * LC + n] = f2bf(v[i]);
+  }
+  for (int idx = tid; idx < 2 * F * (C / 4); idx += 256) {
+    const int h = idx / (F * C / 4), rem = idx % (F * C / 4), f = rem / (C / 4), k = (rem % (C / 4)) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(a.W3[h] + f * C + k);
+    st4bf(sm + O_W3I + h * F * LC + f * LC + k, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm[O_W3T + h * C * LF + (k + i) * LF + f] = f2bf(v[i]);
+  }
+  if constexpr (FK > F) {  // zero K padding of W3^T
+    for (int idx = tid; idx < 2 * C * (FK - F); idx += 256) {
+      const int h = idx / (C * (FK - F)), rem = idx % (C * (FK - F));
+      sm[O_W3T + h * C * LF + (rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
+    }
+  }
+
+  // ---- stage 1: P1 = lrelu(Y W1^T + b1) over K = 2H in 64-wide chunks
+  f32x4 acc1[NC2];
+#pragma unroll
+  for (int j = 0; j < NC2; ++j) acc1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    constexpr int WPT = C2 * 8 / 256;  // 16-byte pieces of a W1 chunk per thread
+    u32x4 wr[WPT];
+    auto wload = [&](int k0) {
+#pragma unroll
+      for (int i = 0; i < WPT; ++i) {
+        const int idx = tid + 256 * i, row = idx >> 3, c8 = idx & 7;
+        wr[i] = *reinterpret_cast<const u32x4*>(a.W1 + (size_t)row * H2 + k0 + 8 * c8);
+      }
+    };
+    auto wstore = [&](int buf) {
+#pragma unroll
+      for (int i = 0; i < WPT; ++i) {
+        const int idx = tid + 256 * i, row = idx >> 3, c8 = idx & 7;
+        *reinterpret_cast<u32x4*>(sm + O_S1 + buf * C2 * LS1 + row * LS1 + 8 * c8) = wr[i];
+      }
+    };
+    const unsigned short* yrow = a.Y + (size_t)(rv ? grow : 0) * H2;
+    bf16x8 ac[2], an[2];
+    const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto aload = [&](int k0, bf16x8* d) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) d[s] = rv ? gld8(yrow + k0 + 32 * s + 8 * q) : z8;
+    };
+    const int nk = H2 / 64;
+    wload(0);
+    aload(0, ac);
+    wstore(0);
+    __syncthreads();
+    for (int kc = 0; kc < nk; ++kc) {
+      if (kc + 1 < nk) { wload((kc + 1) * 64); aload((kc + 1) * 64, an); }
+      const short* Wb = sm + O_S1 + (kc & 1) * C2 * LS1;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < NC2; ++j)
+          acc1[j] = mfma(lds8(Wb + (16 * j + l15) * LS1 + 32 * s + 8 * q), ac[s], acc1[j]);
+      if (kc + 1 < nk) wstore((kc + 1) & 1);
+      __syncthreads();
+      ac[0] = an[0]; ac[1] = an[1];
+    }
+  }
+  // lane: P1[lrow][16j + 4q + r]
+#pragma unroll
+  for (int j = 0; j < NC2; ++j) {
+    const int col = 16 * j + 4 * q;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc1[j][r] = lrelu(acc1[j][r] + a.b1[col + r]);
+    st4bf(sm + O_P1 + lrow * L2C + col, acc1[j]);
+    if (rv && a.train) *reinterpret_cast<f32x4*>(a.P1 + (size_t)grow * C2 + col) = acc1[j];
+  }
+
+  // ---- stages 2-3 per head: P2 = lrelu(P1_h W2^T + b2), OUT = P2 W3^T + b3
+  f32x4 acc2[2][NC], acc3[2][NF];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc2[h][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < C; kk += 32) {
+      const bf16x8 av = lds8(sm + O_P1 + lrow * L2C + h * C + kk + 8 * q);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        acc2[h][j] = mfma(lds8(sm + O_W2I + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc2[h][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int col = 16 * j + 4 * q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc2[h][j][r] = lrelu(acc2[h][j][r] + a.b2[h][col + r]);
+      st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc2[h][j]);
+      if (rv && a.train) *reinterpret_cast<f32x4*>(a.P2[h] + (size_t)grow * C + col) = acc2[h][j];
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc3[h][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < C; kk += 32) {
+      const bf16x8 av = lds8(sm + O_P2 + h * RT * LC + lrow * LC + kk + 8 * q);
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        acc3[h][j] = mfma(lds8(sm + O_W3I + h * F * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc3[h][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int col = 16 * j + 4 * q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc3[h][j][r] += a.b3[h][col + r];
+      if (rv) *reinterpret_cast<f32x4*>(a.OUT[h] + (size_t)grow * F + col) = acc3[h][j];
+    }
+  }
+
+  // ---- stage 4: reconstruction loss, masked partial sum, gradient wrt (mu, log_var)
+  __shared__ float inv_cnt;
+  if (tid == 0) {
+    int c = 0;
+    if (a.count) c = *a.count;
+    else for (int b = 0; b < a.B; ++b) c += valid_frames(a.lens[b], a.T);
+    inv_cnt = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
+  }
+  __syncthreads();  // also: all waves are past stage 1 (the staging aliases P2 / dOUT images)
+  const bool lik = a.loss_type == 0;
+  bool m = false;
+  if (rv) {
+    const int b = grow / a.T, t = grow % a.T;
+    m = t < valid_frames(a.lens[b], a.T);
+  }
+  const float s = m ? a.rec_scale * inv_cnt : 0.f;
+  float lsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int col = 16 * j + 4 * q;
+    f32x4 xv = {0.f, 0.f, 0.f, 0.f};
+    if (rv) xv = *reinterpret_cast<const f32x4*>(a.x + (size_t)grow * F + col);
+    f32x4 gm, gv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float mu = acc3[0][j][r], d = xv[r] - mu;
+      float rr, gmu, glv = 0.f;
+      if (lik) {
+        const float lv = acc3[1][j][r];
+        const float elv = expf(lv), ev = elv + 1e-5f;
+        rr = 0.5f * (LOG_2PI_H + lv + d * d / ev);
+        gmu = -d / ev;
+        glv = 0.5f * (1.f - d * d * elv / (ev * ev));
+      } else {
+        rr = d * d;
+        gmu = -2.f * d;
+      }
+      if (m) lsum += rr;
+      gm[r] = s * gmu;
+      gv[r] = s * glv;
+    }
+    if (a.train) {
+      st4bf(sm + O_DO + lrow * LF + col, gm);
+      st4bf(sm + O_DO + RT * LF + lrow * LF + col, gv);
+      if (rv) {
+        *reinterpret_cast<f32x4*>(a.dOUT[0] + (size_t)grow * F + col) = gm;
+        if (lik) *reinterpret_cast<f32x4*>(a.dOUT[1] + (size_t)grow * F + col) = gv;
+      }
+    }
+  }
+  lsum = wave_sum(lsum);
+  if (lane == 0) red[wave] = lsum;
+  if constexpr (FK > F) {
+    if (a.train) {  // zero the K padding of this wave's dOUT rows
+      for (int idx = lane; idx < 2 * 16 * (FK - F); idx += 64) {
+        const int h = idx / (16 * (FK - F)), rem = idx % (16 * (FK - F));
+        sm[O_DO + h * RT * LF + (16 * wave + rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) a.partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (!a.train) return;
+
+  // ---- stages 5-6 per head: dP2 = (dOUT W3) * lrelu'(P2), dP1_h = (dP2 W2) * lrelu'(P1_h)
+  const int nh = lik ? 2 : 1;  // mse: log_var gets no gradient (torch leaves its grads None)
+  for (int h = 0; h < 2; ++h) {
+    f32x4 acc5[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc5[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (h < nh) {
+#pragma unroll
+      for (int kk = 0; kk < FK; kk += 32) {
+        const bf16x8 av = lds8(sm + O_DO + h * RT * LF + lrow * LF + kk + 8 * q);
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+          acc5[j] = mfma(lds8(sm + O_W3T + h * C * LF + (16 * j + l15) * LF + kk + 8 * q), av, acc5[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int col = 16 * j + 4 * q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc5[j][r] *= lrelu_d(acc2[h][j][r]);
+      // dP2 image reuses this head's P2 image (P2 itself is dead after stage 3)
+      st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc5[j]);
+      if (rv && h < nh) *reinterpret_cast<f32x4*>(a.dP2[h] + (size_t)grow * C + col) = acc5[j];
+    }
+    f32x4 acc6[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc6[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (h < nh) {
+#pragma unroll
+      for (int kk = 0; kk < C; kk += 32) {
+        const bf16x8 av = lds8(sm + O_P2 + h * RT * LC + lrow * LC + kk + 8 * q);
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+          acc6[j] = mfma(lds8(sm + O_W2T + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc6[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int col = h * C + 16 * j + 4 * q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc6[j][r] *= lrelu_d(acc1[h * NC + j][r]);
+      st4bf(sm + O_P1 + lrow * L2C + col, acc6[j]);  // dP1 image reuses the P1 image
+      if (rv) *reinterpret_cast<f32x4*>(a.dP1 + (size_t)grow * C2 + col) = acc6[j];
+    }
+  }
+
+  // ---- stage 7: dY = dP1 W1 (K = 2C), 128 output columns per staged W1^T chunk
+  bf16x8 af[C2 / 32];
+#pragma unroll
+  for (int s7 = 0; s7 < C2 / 32; ++s7) af[s7] = lds8(sm + O_P1 + lrow * L2C + 32 * s7 + 8 * q);
+  float* dyrow = a.dY + (size_t)grow * H2;
+  for (int n0 = 0; n0 < H2; n0 += 128) {
+    __syncthreads();  // previous chunk consumed (first pass: every wave is past stage 5)
+    constexpr int PPT = 128 * C2 / 8 / 256;  // 16-byte pieces per thread
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int idx = tid + 256 * i, row = idx / (C2 / 8), c8 = idx % (C2 / 8);
+      *reinterpret_cast<u32x4*>(sm + O_S7 + row * L2C + 8 * c8) =
+          *reinterpret_cast<const u32x4*>(a.W1t + (size_t)(n0 + row) * C2 + 8 * c8);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s7 = 0; s7 < C2 / 32; ++s7)
+        acc = mfma(lds8(sm + O_S7 + (16 * j + l15) * L2C + 32 * s7 + 8 * q), af[s7], acc);
+      if (rv) *reinterpret_cast<f32x4*>(dyrow + n0 + 16 * j + 4 * q) = acc;
+    }
+  }
+}
+
+template <int C, int F>
+int launch_heads(const HeadArgs& a, hipStream_t st) {
+  constexpr int FK = (F + 31) / 32 * 32, LC = C + 8, LF = FK + 8, L2C = 2 * C + 8;
+  constexpr size_t lds = (size_t)(2 * C * LC * 2 + 2 * F * LC + 2 * C * LF + RT * L2C + 2 * RT * LC +
+                                  2 * RT * LF) * sizeof(short);
+  auto k = heads_kernel<C, F>;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess) {
+      mlvae_set_error("heads: cannot reserve %zu B LDS", lds);
+      return 2;
+    }
+    attr = true;
+  }
+  k<<<(a.N + RT - 1) / RT, 256, lds, st>>>(a);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int mlvae_heads_partials_count(int B, int T) { return (B * T + RT - 1) / RT; }
+
+extern "C" int mlvae_heads_supported(int C, int F, int H2) {
+  return C == 64 && (F == 64 || F == 80) && H2 > 0 && H2 % 128 == 0;
+}
+
+extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int train,
+                                 const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
+                                 const float* b1, const float* w2m, const float* b2m,
+                                 const float* w3m, const float* b3m, const float* w2v,
+                                 const float* b2v, const float* w3v, const float* b3v,
+                                 const float* x, const float* lens, const int* count,
+                                 float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
+                                 float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
+                                 float* dp1, float* dy, float* partials, void* stream) {
+  if (B <= 0 || T <= 0) return 0;
+  if (!mlvae_heads_supported(C, F, H2)) {
+    mlvae_set_error("heads: unsupported shape C=%d F=%d 2H=%d (C 64, F 64|80, 2H %% 128)", C, F, H2);
+    return 1;
+  }
+  if (loss_type != 0 && loss_type != 1) { mlvae_set_error("Invalid loss type: %d", loss_type); return 1; }
+  if (!y_bf16 || !w1_bf16 || !b1 || !w2m || !w3m || !w2v || !w3v || !b2m || !b3m || !b2v || !b3v ||
+      !x || !lens || !mux || !lvx || !partials ||
+      (train && (!w1t_bf16 || !p1 || !p2m || !p2v || !dmux || (loss_type == 0 && !dlvx) || !dp2m ||
+                 !dp2v || !dp1 || !dy))) {
+    mlvae_set_error("heads: null pointer");
+    return 1;
+  }
+  HeadArgs a;
+  a.B = B; a.T = T; a.N = B * T; a.H2 = H2; a.loss_type = loss_type; a.train = train;
+  a.Y = static_cast<const unsigned short*>(y_bf16);
+  a.W1 = static_cast<const unsigned short*>(w1_bf16);
+  a.W1t = static_cast<const unsigned short*>(w1t_bf16);
+  a.b1 = b1;
+  a.W2[0] = w2m; a.b2[0] = b2m; a.W3[0] = w3m; a.b3[0] = b3m;
+  a.W2[1] = w2v; a.b2[1] = b2v; a.W3[1] = w3v; a.b3[1] = b3v;
+  a.x = x; a.lens = lens; a.count = count; a.rec_scale = rec_scale;
+  a.P1 = p1; a.P2[0] = p2m; a.P2[1] = p2v; a.OUT[0] = mux; a.OUT[1] = lvx;
+  a.dOUT[0] = dmux; a.dOUT[1] = dlvx; a.dP2[0] = dp2m; a.dP2[1] = dp2v; a.dP1 = dp1; a.dY = dy;
+  a.partials = partials;
+  hipStream_t st = (hipStream_t)stream;
+  return F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
+}

@@ -38,6 +38,10 @@ _SIGS = {
     "mlvae_lstm_fwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_elbo_partials_count": [I, I, I],
+    "mlvae_heads_partials_count": [I, I],
+    "mlvae_heads_supported": [I, I, I],
+    "mlvae_heads_fused": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
+                          P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mlvae_reparam_kl_fwd": [I, I, I, P, I, P, P, P, P, P, P],
     "mlvae_reparam_kl_bwd": [I, I, I, P, I, P, P, P, P, P, F, P, I, P],
     "mlvae_recon": [I, I, I, I, P, I, P, I, P, I, P, P, P, P, P, F, P, P, P],

@@ -181,6 +181,8 @@ class _Work:
         self.nr = l.mlvae_elbo_partials_count(B, T, F)
         self.pk = torch.empty(self.nk, **f)
         self.pr = torch.empty(self.nr, **f)
+        self.nh = l.mlvae_heads_partials_count(B, T)
+        self.ph = torch.empty(self.nh, **f)   # fused heads' recon partials
         self.loss = torch.zeros(3, **f)   # [kld_loss, recon_loss, total]
         self.count = torch.zeros(1, device=device, dtype=torch.int32)
         # GEMM split-K workspace: the largest any call of the step asks for
@@ -241,6 +243,10 @@ class VAEEngine:
         self.flat_bf = torch.empty(n, device=self.device, dtype=torch.bfloat16) if cfg.prec == "bf16" else None
         # bf16 mode: k-contiguous W_ih^T [din, 8H] of the layers whose dgrad runs on the 256² GEMM
         self.wih_t = {}
+        # bf16 mode: the heads run as one fused kernel (heads.hip) when the shape is supported
+        self.fused_heads = (cfg.prec == "bf16" and bool(lib().mlvae_heads_supported(cfg.C, cfg.F, 2 * cfg.H)))
+        self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
+                     if self.fused_heads else None)
         if cfg.prec == "bf16":
             for li in range(1, cfg.L):
                 self.wih_t[li] = torch.empty(2 * cfg.H * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
@@ -451,6 +457,9 @@ class VAEEngine:
         X = _p(x)
         if self.flat_bf is not None:  # this step's weights as bf16 GEMM operands
             check(l.mlvae_cast_bf16(self.layout.total, _p(self.flat), _pb(self.flat_bf), s), "cast_bf16")
+            if train and self.w1_t is not None:
+                check(l.mlvae_cast_bf16_t(2 * cfg.C, 2 * cfg.H, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                                          _pb(self.w1_t), s), "cast_bf16_t")
             if train:
                 for li, dst in self.wih_t.items():
                     check(l.mlvae_cast_bf16_t(8 * cfg.H, 2 * cfg.H, self._ptr(f"decoder.rnn.weight_ih_l{li}"),
@@ -510,6 +519,28 @@ class VAEEngine:
         w.rnn_out = w.Y[cfg.L - 1]
         w.rnn_out_bf = w.Yb[cfg.L - 1] if w.bf else None
         # ---- heads (ref:src/modules/decoder.py:24-25, FCBlock ref:src/modules/fc_block.py:9-16)
+        lt = LOSS[cfg.loss_type]
+        w_kl, w_rec = self.loss_weights()
+        w.heads_fused = self.fused_heads and w.bf
+        if w.heads_fused:
+            # both heads forward + recon loss (+ gradient) + heads backward + dY in one launch
+            hp = lambda name: self._ptr(f"decoder.{name}")
+            tr = 1 if train else 0
+            check(l.mlvae_heads_fused(
+                B, T, Fd, C, 2 * H, lt, tr, _pb(w.rnn_out_bf), wb("decoder.mean_fc.blocks.0.weight"),
+                _pb(self.w1_t) if train else None, hp("mean_fc.blocks.0.bias"),
+                hp("mean_fc.blocks.2.weight"), hp("mean_fc.blocks.2.bias"),
+                hp("mean_fc.blocks.4.weight"), hp("mean_fc.blocks.4.bias"),
+                hp("log_var_fc.blocks.2.weight"), hp("log_var_fc.blocks.2.bias"),
+                hp("log_var_fc.blocks.4.weight"), hp("log_var_fc.blocks.4.bias"),
+                X, _p(lens), count, w_rec, _p(w.P1), _p(w.P2m), _p(w.P2v), _p(w.MUX), _p(w.LVX),
+                _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
+                _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
+                _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
+                _p(w.ph), s), "heads_fused")
+            check(l.mlvae_elbo_finalize(_p(w.pk), w.nk, _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
+                                        w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
+            return w
         R = _p(w.rnn_out)
         self._mm(w, 0, 1, N, 2 * C, 2 * H, R, 2 * H, self._ptr("decoder.mean_fc.blocks.0.weight"),
                  2 * H, _p(w.P1), 2 * C, A_bf=_pb(w.rnn_out_bf) if w.bf else None,
@@ -525,8 +556,6 @@ class VAEEngine:
                      _p(out), Fd, B_bf=wb(f"decoder.{hd}.blocks.4.weight"),
                      bias1=self._ptr(f"decoder.{hd}.blocks.4.bias"))
         # ---- ELBO part 2 (+ its gradient when training)
-        lt = LOSS[cfg.loss_type]
-        w_kl, w_rec = self.loss_weights()
         dmux = _p(w.dMUX) if train else None
         dlvx = _p(w.dLVX) if (train and lt == 0) else None
         check(l.mlvae_recon(B, T, Fd, lt, _p(w.MUX), Fd, _p(w.LVX), Fd, X, Fd, _p(lens), count,
@@ -570,7 +599,9 @@ class VAEEngine:
         gp = lambda name: self._ptr(name, g)
         mse = cfg.loss_type == "mse"
         count = _p(w.count) if self.world > 1 else None
-        # ---- heads tail: dgrad chain on the main stream, wgrads on the side stream
+        # ---- heads tail: dgrad chain on the main stream (already done inside the fused heads
+        # kernel when it ran), wgrads on the side stream
+        fused = getattr(w, "heads_fused", False)
         heads = [("mean_fc", w.P2m, w.dMUX, w.dP2m, 0)]
         if not mse:
             heads.append(("log_var_fc", w.P2v, w.dLVX, w.dP2v, C))
@@ -582,17 +613,19 @@ class VAEEngine:
                 self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
                 self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
             self._side(wg3)
-            self._mm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C,
-                     B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
+            if not fused:
+                self._mm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C,
+                         B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
 
             def wg2(hd=hd, dP2=dP2, off=off):
                 self._mm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
                          gp(f"decoder.{hd}.blocks.2.weight"), C)
                 self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
             self._side(wg2)
-            self._mm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C,
-                     B_bf=wb(f"decoder.{hd}.blocks.2.weight"), epi=EPI_DLRELU,
-                     aux=_p(w.P1, off), ldaux=2 * C)
+            if not fused:
+                self._mm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C,
+                         B_bf=wb(f"decoder.{hd}.blocks.2.weight"), epi=EPI_DLRELU,
+                         aux=_p(w.P1, off), ldaux=2 * C)
         K1 = C if mse else 2 * C  # mse: the log_var head gets no gradient (torch: grad None)
         R = _p(w.rnn_out)
         R_bf = _pb(w.rnn_out_bf) if w.bf else None
@@ -602,8 +635,9 @@ class VAEEngine:
                      gp("decoder.mean_fc.blocks.0.weight"), 2 * H, B_bf=R_bf)
             self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
         self._side(wg1)
-        self._mm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
-                 2 * H, _p(w.dY[cfg.L - 1]), 2 * H, B_bf=wb("decoder.mean_fc.blocks.0.weight"))
+        if not fused:
+            self._mm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                     2 * H, _p(w.dY[cfg.L - 1]), 2 * H, B_bf=wb("decoder.mean_fc.blocks.0.weight"))
         # ---- BiLSTM layers, top to bottom
         for li in range(cfg.L - 1, -1, -1):
             xin, xin_bf, din = w.layer_in[li]

@@ -1,0 +1,94 @@
+"""Fused decoder heads (heads.hip) against an fp64 autograd restatement of
+ref:src/modules/decoder.py:24-25,37-53 + ref:src/modules/fc_block.py on the same bf16 operands.
+Tolerances: the kernel feeds bf16 MFMAs (activations rounded to bf16 between layers)."""
+import math
+
+import pytest
+import torch
+
+from gpu_utils import P, need_gpu, norm_rel, rel_err, stream
+from mlvae_hip._lib import check, lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _valid(lens, T):
+    """SpeechBrain length_to_mask in fp32 (ref:src/utils/data_utils.py:86-87)."""
+    lim = (lens.float() * T)
+    return (torch.arange(T).float()[None, :] < lim[:, None])
+
+
+@pytest.mark.parametrize("loss_type", [0, 1])
+@pytest.mark.parametrize("B,T,F,H2,train", [(3, 50, 80, 256, 1), (2, 64, 64, 384, 1), (3, 50, 80, 256, 0)])
+def test_heads_fused(loss_type, B, T, F, H2, train):
+    need_gpu()
+    torch.manual_seed(B * 1000 + T + F + H2 + loss_type)
+    C, N = 64, B * T
+    rec_scale = 0.7
+    Y = torch.randn(N, H2).to(torch.bfloat16)
+    W1 = (torch.randn(2 * C, H2) / math.sqrt(H2)).to(torch.bfloat16)
+    b1 = torch.randn(2 * C) * 0.1
+    W2 = [torch.randn(C, C) / 8 for _ in range(2)]
+    b2 = [torch.randn(C) * 0.1 for _ in range(2)]
+    W3 = [torch.randn(F, C) / 8 for _ in range(2)]
+    b3 = [torch.randn(F) * 0.1 for _ in range(2)]
+    x = torch.randn(N, F)
+    lens = torch.tensor([1.0, 0.7, 0.31][:B])
+    mask = _valid(lens, T).reshape(N, 1).double()
+    count = int(mask.sum().item())
+
+    # fp64 reference
+    Yd = Y.double().requires_grad_(True)
+    lrelu = lambda v: torch.nn.functional.leaky_relu(v, 0.01)
+    P1 = lrelu(Yd @ W1.double().t() + b1.double())
+    outs, p2s = [], []
+    for h in range(2):
+        p2 = lrelu(P1[:, h * C:(h + 1) * C] @ W2[h].double().t() + b2[h].double())
+        p2s.append(p2)
+        outs.append(p2 @ W3[h].double().t() + b3[h].double())
+    for o in outs:
+        o.retain_grad()
+    mu, lv = outs
+    d = x.double() - mu
+    if loss_type == 0:
+        r = 0.5 * (math.log(2 * math.pi) + lv + d * d / (torch.exp(lv) + 1e-5))
+    else:
+        r = d * d
+    lsum = (r * mask).sum()
+    (rec_scale * lsum / (count * F)).backward()
+
+    l = lib()
+    dev = lambda t: t.contiguous().cuda()
+    dY, dW1 = dev(Y), dev(W1)
+    dW1t = dev(W1.t())
+    db1 = dev(b1)
+    dW2, db2, dW3, db3 = [dev(t) for t in W2], [dev(t) for t in b2], [dev(t) for t in W3], [dev(t) for t in b3]
+    dx, dlens = dev(x), dev(lens)
+    f = dict(device="cuda", dtype=torch.float32)
+    o = {k: torch.zeros(N, n, **f) for k, n in (("p1", 2 * C), ("p2m", C), ("p2v", C), ("mux", F),
+                                                  ("lvx", F), ("dmux", F), ("dlvx", F), ("dp2m", C),
+                                                  ("dp2v", C), ("dp1", 2 * C), ("dy", H2))}
+    parts = torch.zeros(l.mlvae_heads_partials_count(B, T), **f)
+    assert l.mlvae_heads_supported(C, F, H2)
+    tr = lambda k: P(o[k]) if train else None
+    check(l.mlvae_heads_fused(B, T, F, C, H2, loss_type, train, dY.data_ptr(), dW1.data_ptr(),
+                              dW1t.data_ptr() if train else None, P(db1), P(dW2[0]), P(db2[0]),
+                              P(dW3[0]), P(db3[0]), P(dW2[1]), P(db2[1]), P(dW3[1]), P(db3[1]),
+                              P(dx), P(dlens), None, rec_scale, tr("p1"), tr("p2m"), tr("p2v"),
+                              P(o["mux"]), P(o["lvx"]), tr("dmux"),
+                              P(o["dlvx"]) if (train and loss_type == 0) else None, tr("dp2m"),
+                              tr("dp2v"), tr("dp1"), tr("dy"), P(parts), stream()))
+    torch.cuda.synchronize()
+    assert rel_err(o["mux"], mu) < 2e-2
+    assert rel_err(o["lvx"], lv) < 2e-2
+    assert abs(parts.sum().item() - lsum.item()) / abs(lsum.item()) < 1e-2
+    if not train:
+        return
+    assert rel_err(o["p1"], P1) < 1e-2
+    assert rel_err(o["p2m"], p2s[0]) < 2e-2
+    assert norm_rel(o["dmux"], mu.grad) < 2e-2
+    if loss_type == 0:
+        assert norm_rel(o["dlvx"], lv.grad) < 2e-2
+    assert norm_rel(o["dy"], Yd.grad) < 3e-2
+    if loss_type == 1:  # mse: the log_var head gets no gradient
+        assert o["dp1"][:, C:].abs().max().item() == 0.0
