@@ -140,6 +140,42 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
                       float* p1, float* p2m, float* p2v, float* mux, float* lvx, float* dmux,
                       float* dlvx, float* dp2m, float* dp2v, float* dp1, float* dy,
                       float* partials, void* stream);
+/* Skinny products of the bottom LSTM layer (bf16; one side is the latent width):
+ * mlvae_skinny_nt: C [M, N] (fp32, ldc) = A [M, K] . Bt [N, K]^T, bf16 k-contiguous operands,
+ *   N in {16, 32, 48, 64}, K % 32 == 0: dZ = dG W_ih over the k-contiguous W_ih^T copy.
+ * mlvae_skinny_tn: W [M, nw] (fp32 row-major) = A^T B over K frames, A stored [K, M] (lda), B
+ *   stored [K, NB] (ldb), NB in {16..64} % 16, M % 64 == 0; bias1/bias2 [M] (either may be NULL)
+ *   = column nw of the product (B's column nw all ones: the bias gradient as MFMA work).  Frame
+ *   splits go to fp32 slabs (workspace: mlvae_skinny_tn_workspace_size) summed in a fixed order.
+ * Replace the autograd of layer 0's input projection (ref:src/modules/decoder.py:14-15,22). */
+int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                    float* C, int ldc, void* stream);
+size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K);
+int mlvae_skinny_tn(int M, int NB, int K, const void* A, int lda, const void* B, int ldb, int nw,
+                    float* W, float* bias1, float* bias2, float* ws, size_t ws_bytes, void* stream);
+/* Fused VanillaVAE encoder (bf16; mlvae_encoder_supported: E == 64, Z == 32, F in {64, 80}).
+ * Forward: FC(F->E) LReLU FC(E->E) LReLU -> [mu | log_var] -> z = eps exp(lv/2) + mu, with the
+ * masked KL sums in kl_partials[mlvae_encoder_partials_count] (read by mlvae_elbo_finalize).
+ * eps_in NULL: eps = Philox(seed, offset + n*Z + k) (the mlvae_randn stream) -> eps_out.
+ * z_bf16 [B*T, z_ld]: z_ld = Z, or >= Z + 16 with columns Z..Z+15 = [1, 0, ...] (the ones column
+ * of mlvae_skinny_tn's bias gradient).  e1/e2 bf16 [B*T, E] are kept for the backward.
+ * Backward: from dz (the gradient reaching z) the reparam/KL gradient, both LReLU dgrads and the
+ * six encoder weight/bias gradients (overwritten; fixed-order reduce over the workspace
+ * mlvae_encoder_workspace_size).  Replaces ref:src/modules/vanilla_vae.py:13-45 and its autograd. */
+int mlvae_encoder_supported(int F, int E, int Z);
+int mlvae_encoder_partials_count(int B, int T);
+size_t mlvae_encoder_workspace_size(int B, int T, int F, int E, int Z);
+int mlvae_encoder_fwd(int B, int T, int F, int E, int Z, const float* x, const float* w0,
+                      const float* b0, const float* w1, const float* b1, const float* wml,
+                      const float* bml, const float* eps_in, unsigned long long seed,
+                      unsigned long long offset, const float* lens, void* e1_bf16, void* e2_bf16,
+                      float* ml, float* z, void* z_bf16, int z_ld, float* eps_out,
+                      float* kl_partials, void* stream);
+int mlvae_encoder_bwd(int B, int T, int F, int E, int Z, const float* dz, const float* ml,
+                      const float* eps, const void* e1_bf16, const void* e2_bf16, const float* x,
+                      const float* wml, const float* w1, const float* lens, const int* count,
+                      float kl_scale, float* dwml, float* dbml, float* dw1, float* db1, float* dw0,
+                      float* db0, float* ws, size_t ws_bytes, void* stream);
 /* out[3] = {kld_loss, recon_loss, w_kl*kld + w_rec*recon}
  * (ref:src/utils/data_utils.py:67-104, ref:src/models/md_model.py:189-213). */
 int mlvae_elbo_finalize(const float* kl_partials, int nk, const float* rec_partials, int nr,

@@ -1,0 +1,226 @@
+// Skinny products of the bottom LSTM layer (bf16 mode), where one GEMM side is the latent
+// width Z (16-64): on a 256-wide GEMM tile 7/8 of every MFMA and B load is padding.
+//
+//   dZ = dG W_ih           [B*T, Z]  = [B*T, 8H] . [8H, Z]        (dgrad into the encoder)
+//   dW_ih | db = dG^T [Z | 1]   [8H, Z+1] = [8H, B*T] . [B*T, Z+1] (weight + bias gradients:
+//                                 the ones column turns the bias column sum into MFMA work)
+// ref:src/modules/decoder.py:14-15,22 (nn.LSTM input projection of layer 0, its autograd).
+//
+// skinny_nt: C[M, NB] = A[M, K] . Bt[NB, K]^T, A and Bt k-contiguous bf16.  A wave owns 16 rows
+//   and all NB columns; fragments are loaded straight from global (16 B per lane, four K-steps
+//   in flight); operands swapped so a lane stores 4 consecutive columns.
+// skinny_tn: P_s[M, NB] = A[Ks, M]^T . B[Ks, NB] over one frame range Ks per split s; A and B
+//   m/n-contiguous bf16, staged through LDS (64 frames per chunk) and read with
+//   ds_read_b64_tr_b16; fp32 partial slabs per split, reduced in a fixed order by
+//   skinny_reduce into the weight columns and (optionally) two bias vectors.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) bf16x4* lds_b4_p;
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int NT>  // NB = 16 * NT
+__global__ __launch_bounds__(256) void skinny_nt_kernel(int M, int K, const unsigned short* __restrict__ A,
+                                                        int lda, const unsigned short* __restrict__ Bt,
+                                                        int ldb, float* __restrict__ C, int ldc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int row = (blockIdx.x * 4 + wave) * 16 + l15;
+  const bool rv = row < M;
+  const unsigned short* ap = A + (size_t)(rv ? row : 0) * lda + 8 * q;
+  const unsigned short* bp = Bt + (size_t)l15 * ldb + 8 * q;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;  // K-steps of 32 in flight
+  int k = 0;
+  for (; k + 32 * U <= K; k += 32 * U) {
+    bf16x8 af[U], bf[U][NT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      af[u] = rv ? *reinterpret_cast<const bf16x8*>(ap + k + 32 * u) : z8;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bf[u][j] = *reinterpret_cast<const bf16x8*>(bp + (size_t)16 * j * ldb + k + 32 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = mfma16(bf[u][j], af[u], acc[j]);
+  }
+  for (; k < K; k += 32) {  // K % 32 == 0 (checked on the host)
+    const bf16x8 a1 = rv ? *reinterpret_cast<const bf16x8*>(ap + k) : z8;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      acc[j] = mfma16(*reinterpret_cast<const bf16x8*>(bp + (size_t)16 * j * ldb + k), a1, acc[j]);
+  }
+  if (!rv) return;
+  // swapped operands: lane holds C[row][16j + 4q + r]
+#pragma unroll
+  for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + 16 * j + 4 * q) = acc[j];
+}
+
+// LDS images: A [64 frames][64 m + 8], B [64 frames][NB + 8] (bf16); transposed fragment reads.
+template <int NT>
+__global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk,
+                                                        const unsigned short* __restrict__ A, int lda,
+                                                        const unsigned short* __restrict__ B, int ldb,
+                                                        float* __restrict__ ws) {
+  constexpr int NB = 16 * NT, LA = 64 + 8, LB = NB + 8;
+  __shared__ __attribute__((aligned(16))) short sa[64 * LA];
+  __shared__ __attribute__((aligned(16))) short sb[64 * LB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * 64, s = blockIdx.y;
+  const int kbeg = s * kchunk, kend = min(K, kbeg + kchunk);
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staging roles: A chunk = 64 frames x 8 pieces of 16 B; B chunk = 64 frames x NB/8 pieces
+  constexpr int PB = 64 * NB / 8;
+  for (int k0 = kbeg; k0 < kend; k0 += 64) {
+    u32x4 va[2], vb[(PB + 255) / 256];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i, fr = idx >> 3, c8 = idx & 7;
+      const int f = k0 + fr;
+      va[i] = f < kend ? *reinterpret_cast<const u32x4*>(A + (size_t)f * lda + m0 + 8 * c8) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < (PB + 255) / 256; ++i) {
+      const int idx = tid + 256 * i, fr = idx / (NB / 8), c8 = idx % (NB / 8);
+      const int f = k0 + fr;
+      vb[i] = (idx < PB && f < kend) ? *reinterpret_cast<const u32x4*>(B + (size_t)f * ldb + 8 * c8)
+                                     : u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();  // previous chunk's fragments are consumed
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i, fr = idx >> 3, c8 = idx & 7;
+      *reinterpret_cast<u32x4*>(sa + fr * LA + 8 * c8) = va[i];
+    }
+#pragma unroll
+    for (int i = 0; i < (PB + 255) / 256; ++i) {
+      const int idx = tid + 256 * i, fr = idx / (NB / 8), c8 = idx % (NB / 8);
+      if (idx < PB) *reinterpret_cast<u32x4*>(sb + fr * LB + 8 * c8) = vb[i];
+    }
+    __syncthreads();
+    // wave w: m rows 16w .. 16w+15 (A^T fragment by transposed reads), all NB columns
+    const int g = lane >> 4, i4 = lane & 15, qq = i4 >> 2, pp = i4 & 3;
+#pragma unroll
+    for (int kk = 0; kk < 64; kk += 32) {
+      const int r1 = kk + 8 * g + qq, r2 = r1 + 4;
+      const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r1 * LA + 16 * wave + 4 * pp));
+      const bf16x4 a2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r2 * LA + 16 * wave + 4 * pp));
+      const bf16x8 af = {a1[0], a1[1], a1[2], a1[3], a2[0], a2[1], a2[2], a2[3]};
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sb + r1 * LB + 16 * j + 4 * pp));
+        const bf16x4 b2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sb + r2 * LB + 16 * j + 4 * pp));
+        const bf16x8 bfr = {b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+        acc[j] = mfma16(bfr, af, acc[j]);  // swapped: lane holds P[m][16j + 4q + r]
+      }
+    }
+  }
+  const int m = m0 + 16 * wave + (lane & 15), q = lane >> 4;
+  if (m >= M) return;
+  float* out = ws + ((size_t)s * M + m) * NB;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(out + 16 * j + 4 * q) = acc[j];
+}
+
+// W[m][n] = sum_s P_s[m][n] for n < nw; bias1[m] = bias2[m] = sum_s P_s[m][nw] (if given)
+__global__ __launch_bounds__(256) void skinny_reduce(int M, int NB, int S, int nw, const float* __restrict__ ws,
+                                                     float* __restrict__ W, float* __restrict__ b1,
+                                                     float* __restrict__ b2) {
+  const int ncol = nw + ((b1 || b2) ? 1 : 0);
+  const size_t total = (size_t)M * ncol;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int m = (int)(i / ncol), n = (int)(i % ncol);
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += ws[((size_t)s * M + m) * NB + n];
+    if (n < nw) W[(size_t)m * nw + n] = v;
+    else {
+      if (b1) b1[m] = v;
+      if (b2) b2[m] = v;
+    }
+  }
+}
+
+int tn_splits(int M, int K) {
+  const int mb = (M + 63) / 64;
+  int s = (512 + mb - 1) / mb;
+  const int maxs = (K + 255) / 256;  // >= 4 chunks of 64 frames per split
+  if (s > maxs) s = maxs;
+  return s < 1 ? 1 : s;
+}
+
+}  // namespace
+
+extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                               float* C, int ldc, void* stream) {
+  if (M <= 0) return 0;
+  if (!A || !Bt || !C || N % 16 || N < 16 || N > 64 || K % 32 || lda % 8 || ldb % 8 || ldc % 4 ||
+      ((uintptr_t)A % 16) || ((uintptr_t)Bt % 16) || ((uintptr_t)C % 16)) {
+    mlvae_set_error("mlvae_skinny_nt: N in {16..64} %% 16, K %% 32, aligned 16-byte rows");
+    return 1;
+  }
+  const unsigned short* a = static_cast<const unsigned short*>(A);
+  const unsigned short* b = static_cast<const unsigned short*>(Bt);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((M + 63) / 64);
+  switch (N / 16) {
+    case 1: skinny_nt_kernel<1><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+    case 2: skinny_nt_kernel<2><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+    case 3: skinny_nt_kernel<3><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+    default: skinny_nt_kernel<4><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+  }
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K) {
+  return (size_t)tn_splits(M, K) * M * NB * sizeof(float);
+}
+
+// W [M, nw] (+ bias1/bias2 [M] = column nw) = A^T B over K frames; B carries NB >= nw + 1
+// columns when biases are wanted (column nw all ones), else NB >= nw.
+extern "C" int mlvae_skinny_tn(int M, int NB, int K, const void* A, int lda, const void* B, int ldb,
+                               int nw, float* W, float* bias1, float* bias2, float* ws,
+                               size_t ws_bytes, void* stream) {
+  if (M <= 0) return 0;
+  if (!A || !B || !W || M % 64 || NB % 16 || NB < 16 || NB > 64 || nw < 1 ||
+      nw + ((bias1 || bias2) ? 1 : 0) > NB || lda % 8 || ldb % 8 || ((uintptr_t)A % 16) ||
+      ((uintptr_t)B % 16)) {
+    mlvae_set_error("mlvae_skinny_tn: M %% 64, NB in {16..64} %% 16, nw (+1) <= NB, aligned rows");
+    return 1;
+  }
+  const int S = tn_splits(M, K);
+  if (!ws || ws_bytes < (size_t)S * M * NB * sizeof(float)) {
+    mlvae_set_error("mlvae_skinny_tn: workspace too small");
+    return 1;
+  }
+  int kc = (K + S - 1) / S;
+  kc = (kc + 63) / 64 * 64;
+  const unsigned short* a = static_cast<const unsigned short*>(A);
+  const unsigned short* b = static_cast<const unsigned short*>(B);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(M / 64, S);
+  switch (NB / 16) {
+    case 1: skinny_tn_kernel<1><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
+    case 2: skinny_tn_kernel<2><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
+    case 3: skinny_tn_kernel<3><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
+    default: skinny_tn_kernel<4><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
+  }
+  MLVAE_CHECK_LAUNCH();
+  const size_t total = (size_t)M * (nw + 1);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  skinny_reduce<<<blocks, 256, 0, st>>>(M, NB, S, nw, ws, W, bias1, bias2);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}

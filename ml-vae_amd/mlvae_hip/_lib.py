@@ -42,6 +42,14 @@ _SIGS = {
     "mlvae_heads_supported": [I, I, I],
     "mlvae_heads_fused": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
                           P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],
+    "mlvae_skinny_tn_workspace_size": [I, I, I],
+    "mlvae_skinny_tn": [I, I, I, P, I, P, I, I, P, P, P, P, SZ, P],
+    "mlvae_encoder_supported": [I, I, I],
+    "mlvae_encoder_partials_count": [I, I],
+    "mlvae_encoder_workspace_size": [I, I, I, I, I],
+    "mlvae_encoder_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, U64, U64, P, P, P, P, P, P, I, P, P, P],
+    "mlvae_encoder_bwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, F, P, P, P, P, P, P, P, SZ, P],
     "mlvae_reparam_kl_fwd": [I, I, I, P, I, P, P, P, P, P, P],
     "mlvae_reparam_kl_bwd": [I, I, I, P, I, P, P, P, P, P, F, P, I, P],
     "mlvae_recon": [I, I, I, I, P, I, P, I, P, I, P, P, P, P, P, F, P, P, P],
@@ -68,6 +76,9 @@ _RESTYPE = {
     "mlvae_gemm_workspace_size": SZ,
     "mlvae_gemm_ex_workspace_size": SZ,
     "mlvae_colsum_workspace_size": SZ,
+    "mlvae_gemm_bf16_workspace_size": SZ,
+    "mlvae_skinny_tn_workspace_size": SZ,
+    "mlvae_encoder_workspace_size": SZ,
 }
 
 _lib = None

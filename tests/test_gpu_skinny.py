@@ -1,0 +1,59 @@
+"""Skinny products of the bottom LSTM layer (skinny.hip): dZ = dG W_ih (NT) and
+dW_ih | bias = dG^T [z | 1] (TN, fixed-order frame-split reduce), against fp64 products of the
+same bf16 operands (ref:src/modules/decoder.py:14-15,22, the layer-0 input projection's autograd)."""
+import pytest
+import torch
+
+from gpu_utils import P, need_gpu, rel_err, stream
+from mlvae_hip._lib import check, lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K", [(16000, 32, 4096), (1000, 16, 64), (77, 48, 256), (300, 64, 96)])
+def test_skinny_nt(M, N, K):
+    need_gpu()
+    torch.manual_seed(M + N + K)
+    A = torch.randn(M, K).to(torch.bfloat16)
+    Bt = torch.randn(N, K).to(torch.bfloat16)
+    ref = A.double() @ Bt.double().t()
+    dA, dB = A.cuda(), Bt.cuda()
+    C = torch.full((M, N), float("nan"), device="cuda")
+    check(lib().mlvae_skinny_nt(M, N, K, dA.data_ptr(), K, dB.data_ptr(), K, P(C), N, stream()))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,K,nw,NB,bias", [(4096, 16000, 32, 48, True), (2048, 1000, 32, 48, True),
+                                            (512, 130, 16, 16, False), (256, 64, 40, 64, True)])
+def test_skinny_tn(M, K, nw, NB, bias):
+    need_gpu()
+    torch.manual_seed(M + K + nw)
+    A = torch.randn(K, M).to(torch.bfloat16)          # dG [frames, gate rows]
+    Bm = torch.zeros(K, NB)
+    Bm[:, :nw] = torch.randn(K, nw)
+    if bias:
+        Bm[:, nw] = 1.0                                # the ones column of [z | 1 | 0 ...]
+    Bm = Bm.to(torch.bfloat16)
+    ref = A.double().t() @ Bm.double()                # [M, NB]
+    l = lib()
+    dA, dB = A.cuda(), Bm.cuda()
+    ws = torch.empty(l.mlvae_skinny_tn_workspace_size(M, NB, K) // 4 + 1, device="cuda")
+    outs = []
+    for _ in range(2):
+        W = torch.full((M, nw), float("nan"), device="cuda")
+        b1 = torch.full((M,), float("nan"), device="cuda")
+        b2 = torch.full((M,), float("nan"), device="cuda")
+        check(l.mlvae_skinny_tn(M, NB, K, dA.data_ptr(), M, dB.data_ptr(), NB, nw, P(W),
+                                P(b1) if bias else None, P(b2) if bias else None, P(ws),
+                                ws.numel() * 4, stream()))
+        torch.cuda.synchronize()
+        outs.append((W.cpu(), b1.cpu(), b2.cpu()))
+    W, b1, b2 = outs[0]
+    assert rel_err(W, ref[:, :nw]) < 1e-5
+    if bias:
+        assert rel_err(b1, ref[:, nw]) < 1e-5
+        assert torch.equal(b1, b2)
+    else:
+        assert torch.isnan(b1).all()                   # no bias output requested: untouched
+    assert torch.equal(outs[0][0], outs[1][0])         # fixed-order reduce: bit-identical reruns
