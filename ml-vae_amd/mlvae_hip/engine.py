@@ -136,7 +136,7 @@ class ParamLayout:
 class _Work:
     """Activation/gradient workspaces for one (B, T): allocated once, reused every step."""
 
-    def __init__(self, cfg, B, T, device):
+    def __init__(self, cfg, B, T, device, enc_fused=False):
         N = B * T
         F, E, Z, H, L, C = cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C
         f = dict(device=device, dtype=torch.float32)
@@ -157,7 +157,13 @@ class _Work:
         self.Ydb = ([torch.empty(N, 2 * H, **b16) if cfg.dropout > 0 else None for _ in range(L - 1)]
                     if self.bf else None)
         self.dGb = [torch.empty(N, 8 * H, **b16) for _ in range(L)] if self.bf else None
-        self.Zb = torch.empty(N, Z, **b16) if self.bf else None  # first layer's GEMM operand
+        # fused encoder (encoder.hip): z as bf16 [N, Z + 16] = [z | 1 | 0 ...], the ones column
+        # feeding the bottom layer's bias gradient (skinny.hip); bf16 hidden activations
+        self.enc_fused = self.bf and enc_fused
+        self.ZA = Z + 16 if self.enc_fused else Z
+        self.Zb = torch.empty(N, self.ZA, **b16) if self.bf else None  # first layer's GEMM operand
+        self.E1b = torch.empty(N, E, **b16) if self.enc_fused else None
+        self.E2b = torch.empty(N, E, **b16) if self.enc_fused else None
         if self.bf:
             self.Yd = [None] * (L - 1)  # the dropout output exists as bf16 only
         self.P1 = torch.empty(N, 2 * C, **f)
@@ -183,6 +189,10 @@ class _Work:
         self.pr = torch.empty(self.nr, **f)
         self.nh = l.mlvae_heads_partials_count(B, T)
         self.ph = torch.empty(self.nh, **f)   # fused heads' recon partials
+        self.nke = l.mlvae_encoder_partials_count(B, T) if self.enc_fused else 0
+        self.pke = torch.empty(max(self.nke, 1), **f)  # fused encoder's KL partials
+        ewb = l.mlvae_encoder_workspace_size(B, T, F, E, Z) if self.enc_fused else 0
+        self.enc_ws = torch.empty(ewb // 4 + 1, **f)
         self.loss = torch.zeros(3, **f)   # [kld_loss, recon_loss, total]
         self.count = torch.zeros(1, device=device, dtype=torch.int32)
         # GEMM split-K workspace: the largest any call of the step asks for
@@ -196,6 +206,8 @@ class _Work:
                      l.mlvae_gemm_bf16_workspace_size(m, n, k, 1))
                  for m, n, k in shapes)
         ws = max(ws, l.mlvae_gemm_bf16_workspace_size(4 * H, H, N, 2))  # both directions' dW_hh
+        if self.enc_fused:
+            ws = max(ws, l.mlvae_skinny_tn_workspace_size(8 * H, self.ZA, N))
         cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
         self.gws = torch.empty(max(ws, cs, 16) // 4 + 1, **f)
         self.gws_side = torch.empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
@@ -247,9 +259,15 @@ class VAEEngine:
         self.fused_heads = (cfg.prec == "bf16" and bool(lib().mlvae_heads_supported(cfg.C, cfg.F, 2 * cfg.H)))
         self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
                      if self.fused_heads else None)
+        # bf16 mode: the encoder (+ reparameterisation + KL) runs as two fused kernels
+        # (encoder.hip) and the bottom layer's products on skinny kernels (skinny.hip)
+        self.fused_encoder = (cfg.prec == "bf16" and
+                              bool(lib().mlvae_encoder_supported(cfg.F, cfg.E, cfg.Z)))
         if cfg.prec == "bf16":
             for li in range(1, cfg.L):
                 self.wih_t[li] = torch.empty(2 * cfg.H * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
+            if self.fused_encoder:  # dZ = dG W_ih_l0 over its k-contiguous transpose
+                self.wih_t[0] = torch.empty(cfg.Z * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
         self.nparts = lib().mlvae_sumsq_partials_count(n)
         self.sq_parts = torch.zeros(self.nparts, device=self.device, dtype=torch.float64)
         self.seed = seed
@@ -266,9 +284,6 @@ class VAEEngine:
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
         self.global_offset = 0      # first global utterance index of this shard
-        mode = os.environ.get("MLVAE_LSTM_MODE")  # recurrence diagnostics / A-B switches
-        if mode:
-            lib().mlvae_lstm_set_debug_mode(int(mode))
         if params is not None:
             self.load_reference_params(params)
 
@@ -344,7 +359,8 @@ class VAEEngine:
     def work(self, B, T):
         key = (B, T)
         if key not in self._work:
-            self._work = {key: _Work(self.cfg, B, T, self.device)}  # keep one shape resident
+            self._work = {key: _Work(self.cfg, B, T, self.device,  # keep one shape resident
+                                     enc_fused=self.fused_encoder)}
         return self._work[key]
 
     # ------------------------------------------------------------------ launch helpers
@@ -449,6 +465,8 @@ class VAEEngine:
         if Fdim != cfg.F:
             raise ValueError(f"feature dim {Fdim} != input_size {cfg.F}")
         x = x.contiguous()
+        if x.data_ptr() % 16:  # the fused kernels read 16-byte rows
+            x = x.clone()
         lens = lens.to(device=self.device, dtype=torch.float32).contiguous()
         w = self.work(B, T)
         w.x, w.lens = x, lens
@@ -462,42 +480,53 @@ class VAEEngine:
                                           _pb(self.w1_t), s), "cast_bf16_t")
             if train:
                 for li, dst in self.wih_t.items():
-                    check(l.mlvae_cast_bf16_t(8 * cfg.H, 2 * cfg.H, self._ptr(f"decoder.rnn.weight_ih_l{li}"),
-                                              _pb(dst), s), "cast_bf16_t")
+                    check(l.mlvae_cast_bf16_t(8 * cfg.H, cfg.Z if li == 0 else 2 * cfg.H,
+                                              self._ptr(f"decoder.rnn.weight_ih_l{li}"), _pb(dst), s),
+                          "cast_bf16_t")
         wb = self._wb
         count = None
         if self.world > 1:
             count = self._global_count(w)
-        # ---- reparameterisation noise
-        if eps is None:
-            check(l.mlvae_randn(N * Z, self.seed, self._eps_offset(T) + self.rng_step * (1 << 40),
-                                _p(w.eps), s), "mlvae_randn")
-            eps_t = w.eps
+        eps_off = self._eps_offset(T) + self.rng_step * (1 << 40)
+        eps_t = None if eps is None else eps.to(self.device, torch.float32).contiguous().view(N, Z)
+        w.eps_used = w.eps if eps_t is None else eps_t
+        if w.enc_fused:
+            # ---- encoder + reparameterisation noise + z + KL partial sums, one launch
+            # (encoder.hip; ref:src/modules/vanilla_vae.py:21-45)
+            ep = lambda n: self._ptr(f"encoder.{n}")
+            check(l.mlvae_encoder_fwd(B, T, Fd, E, Z, X, ep("fc.0.blocks.0.weight"), ep("fc.0.blocks.0.bias"),
+                                      ep("fc.0.blocks.2.weight"), ep("fc.0.blocks.2.bias"),
+                                      ep("mean_fc.weight"), ep("mean_fc.bias"),
+                                      None if eps_t is None else _p(eps_t), self.seed, eps_off, _p(lens),
+                                      _pb(w.E1b), _pb(w.E2b), _p(w.ML), _p(w.Zs), _pb(w.Zb), w.ZA,
+                                      _p(w.eps) if eps_t is None else None, _p(w.pke), s), "encoder_fwd")
+            w.kl_parts = (w.pke, w.nke)
         else:
-            eps_t = eps.to(self.device, torch.float32).contiguous().view(N, Z)
-        w.eps_used = eps_t
-        # ---- encoder (ref:src/modules/vanilla_vae.py:21-28)
-        self._mm(w, 0, 1, N, E, Fd, X, Fd, self._ptr("encoder.fc.0.blocks.0.weight"), Fd,
-                 _p(w.E1), E, B_bf=wb("encoder.fc.0.blocks.0.weight"),
-                 bias1=self._ptr("encoder.fc.0.blocks.0.bias"), epi=EPI_LRELU)
-        self._mm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
-                 _p(w.E2), E, B_bf=wb("encoder.fc.0.blocks.2.weight"),
-                 bias1=self._ptr("encoder.fc.0.blocks.2.bias"), epi=EPI_LRELU)
-        self._mm(w, 0, 1, N, 2 * Z, E, _p(w.E2), E, self._ptr("encoder.mean_fc.weight"), E,
-                 _p(w.ML), 2 * Z, B_bf=wb("encoder.mean_fc.weight"), bias1=self._ptr("encoder.mean_fc.bias"))
-        check(l.mlvae_reparam_kl_fwd(B, T, Z, _p(w.ML), 2 * Z, _p(eps_t), _p(lens), _p(w.Zs),
-                                     None, _p(w.pk), s), "reparam_kl_fwd")
+            # ---- reparameterisation noise
+            if eps_t is None:
+                check(l.mlvae_randn(N * Z, self.seed, eps_off, _p(w.eps), s), "mlvae_randn")
+            # ---- encoder (ref:src/modules/vanilla_vae.py:21-28)
+            self._mm(w, 0, 1, N, E, Fd, X, Fd, self._ptr("encoder.fc.0.blocks.0.weight"), Fd,
+                     _p(w.E1), E, B_bf=wb("encoder.fc.0.blocks.0.weight"),
+                     bias1=self._ptr("encoder.fc.0.blocks.0.bias"), epi=EPI_LRELU)
+            self._mm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
+                     _p(w.E2), E, B_bf=wb("encoder.fc.0.blocks.2.weight"),
+                     bias1=self._ptr("encoder.fc.0.blocks.2.bias"), epi=EPI_LRELU)
+            self._mm(w, 0, 1, N, 2 * Z, E, _p(w.E2), E, self._ptr("encoder.mean_fc.weight"), E,
+                     _p(w.ML), 2 * Z, B_bf=wb("encoder.mean_fc.weight"), bias1=self._ptr("encoder.mean_fc.bias"))
+            check(l.mlvae_reparam_kl_fwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(lens), _p(w.Zs),
+                                         None, _p(w.pk), s), "reparam_kl_fwd")
+            if w.bf:
+                check(l.mlvae_cast_bf16(N * Z, _p(w.Zs), _pb(w.Zb), s), "cast_bf16")
+            w.kl_parts = (w.pk, w.nk)
         # ---- decoder BiLSTM (ref:src/modules/decoder.py:22)
-        # layer input as (fp32 tensor or None, bf16 tensor or None, width)
-        xin, xin_bf, din = w.Zs, None, Z
-        if w.bf:
-            check(l.mlvae_cast_bf16(N * Z, _p(w.Zs), _pb(w.Zb), s), "cast_bf16")
-            xin_bf = w.Zb
+        # layer input as (fp32 tensor or None, bf16 tensor or None, width, bf16 row stride)
+        xin, xin_bf, din, ldx = w.Zs, (w.Zb if w.bf else None), Z, w.ZA
         w.layer_in = []
         for li in range(cfg.L):
-            w.layer_in.append((xin, xin_bf, din))
+            w.layer_in.append((xin, xin_bf, din, ldx))
             if w.bf and din % 8 == 0:  # input projection on the 256² GEMM
-                self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), din, wb(f"decoder.rnn.weight_ih_l{li}"),
+                self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), ldx, wb(f"decoder.rnn.weight_ih_l{li}"),
                            din, _p(w.G[li]), 8 * H, bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
                            bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
             else:
@@ -512,7 +541,7 @@ class VAEEngine:
                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
                                           _p(w.Cs[li]), _p(w.Y[li]), _pb(w.Yb[li]) if w.bf else None,
                                           _p(w.xbuf), w.xbuf.numel(), _p(w.err), s), "lstm_fwd")
-            xin, xin_bf, din = w.Y[li], (w.Yb[li] if w.bf else None), 2 * H
+            xin, xin_bf, din, ldx = w.Y[li], (w.Yb[li] if w.bf else None), 2 * H, 2 * H
             if li < cfg.L - 1 and train and cfg.dropout > 0:
                 xin, xin_bf = w.Yd[li], (w.Ydb[li] if w.bf else None)
                 self._dropout(w, li, w.Y[li], xin, dropout_masks)
@@ -538,7 +567,7 @@ class VAEEngine:
                 _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
                 _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
                 _p(w.ph), s), "heads_fused")
-            check(l.mlvae_elbo_finalize(_p(w.pk), w.nk, _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
+            check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w
         R = _p(w.rnn_out)
@@ -560,7 +589,7 @@ class VAEEngine:
         dlvx = _p(w.dLVX) if (train and lt == 0) else None
         check(l.mlvae_recon(B, T, Fd, lt, _p(w.MUX), Fd, _p(w.LVX), Fd, X, Fd, _p(lens), count,
                             None, _p(w.pr), None, w_rec, dmux, dlvx, s), "recon")
-        check(l.mlvae_elbo_finalize(_p(w.pk), w.nk, _p(w.pr), w.nr, _p(lens), count, B, T, Z, Fd,
+        check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.pr), w.nr, _p(lens), count, B, T, Z, Fd,
                                     w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
         return w
 
@@ -640,7 +669,7 @@ class VAEEngine:
                      2 * H, _p(w.dY[cfg.L - 1]), 2 * H, B_bf=wb("decoder.mean_fc.blocks.0.weight"))
         # ---- BiLSTM layers, top to bottom
         for li in range(cfg.L - 1, -1, -1):
-            xin, xin_bf, din = w.layer_in[li]
+            xin, xin_bf, din, ldx = w.layer_in[li]
             Gl = w.G[li]
             dGb = w.dGb[li] if w.bf else None
             with self._timed("lstm_bwd"):
@@ -654,11 +683,23 @@ class VAEEngine:
             pgb = lambda t, off=0: None if t is None else _pb(t, off)
             Ybl = w.Yb[li] if w.bf else None
 
-            def wgl(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, Ybl=Ybl):
+            def wgl(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx, Ybl=Ybl):
+                if li == 0 and w.enc_fused:
+                    # dW_ih_l0 | db_ih_l0 = db_hh_l0 = dG^T [z | 1] (skinny.hip), then both
+                    # directions' dW_hh_l0 in one batched 256² launch
+                    ws = w.gws_side if self._on_side else w.gws
+                    check(lib().mlvae_skinny_tn(8 * H, w.ZA, N, _pb(dG_bf), 8 * H, _pb(w.Zb), w.ZA, Z,
+                                                gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
+                                                gp("decoder.rnn.bias_hh_l0"), _p(ws), w.gws_bytes,
+                                                self._stream()), "skinny_tn")
+                    self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
+                               gp("decoder.rnn.weight_hh_l0"), H, batch=2, a_bs=4 * H, b_bs=H,
+                               c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                    return
                 if dG_bf is not None and xin_bf is not None and din % 8 == 0 and H % 8 == 0:
                     # 256² GEMMs: dW_ih = dG^T X, and both directions' dW_hh = sum_t dG_t^T h_{t-/+1}
                     # in one batched launch (the two weights are adjacent in the flat gradient)
-                    self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), din,
+                    self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
                                gp(f"decoder.rnn.weight_ih_l{li}"), din)
                     self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
                                gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
@@ -689,7 +730,12 @@ class VAEEngine:
             dx = w.dZs if li == 0 else w.dY[li - 1]
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
             seed, mask_ptr = w._drop_seed[li - 1] if drop else (None, None)
-            if dG_bf is not None and li in self.wih_t and din >= 256:
+            if li == 0 and w.enc_fused:
+                # dZ = dG W_ih_l0: [N, 8H] x [8H, Z] on the skinny NT kernel
+                check(l.mlvae_skinny_nt(N, Z, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[0]), 8 * H,
+                                        _p(w.dZs), Z, s), "skinny_nt")
+                fused = False
+            elif dG_bf is not None and li in self.wih_t and din >= 256:
                 # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy
                 self._fast(w, 0, 1, N, din, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[li]), 8 * H,
                            _p(dx), din, drop_seed=seed if (drop and mask_ptr is None) else None)
@@ -706,6 +752,18 @@ class VAEEngine:
                 self._side(wgl)
         # ---- encoder
         w_kl, _ = self.loss_weights()
+        if w.enc_fused:
+            # reparam/KL gradient, both LReLU dgrads and the six encoder gradients (encoder.hip)
+            ep = lambda n: self._ptr(f"encoder.{n}")
+            ge = lambda n: gp(f"encoder.{n}")
+            check(l.mlvae_encoder_bwd(B, T, Fd, E, Z, _p(w.dZs), _p(w.ML), _p(w.eps_used), _pb(w.E1b),
+                                      _pb(w.E2b), _p(w.x), ep("mean_fc.weight"), ep("fc.0.blocks.2.weight"),
+                                      _p(w.lens), count, w_kl, ge("mean_fc.weight"), ge("mean_fc.bias"),
+                                      ge("fc.0.blocks.2.weight"), ge("fc.0.blocks.2.bias"),
+                                      ge("fc.0.blocks.0.weight"), ge("fc.0.blocks.0.bias"), _p(w.enc_ws),
+                                      w.enc_ws.numel() * 4, s), "encoder_bwd")
+            self._join_side()
+            return
         check(l.mlvae_reparam_kl_bwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(w.lens), count,
                                      _p(w.dZs), None, w_kl, _p(w.dML), 2 * Z, s), "reparam_kl_bwd")
 
