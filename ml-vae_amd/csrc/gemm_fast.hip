@@ -24,6 +24,7 @@
 //   * XCD-aware bijective tile order; optional batch (gridDim.y) and split-K (gridDim.z, fp32
 //     partial slabs + a fixed-order reduce: deterministic).
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -44,6 +45,7 @@ struct GFArgs {
   int kshiftT, kshift, kshift_bstep;
   unsigned long long dseed; float dkeep, dscale;
   int splits, kchunk;
+  int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
   float* ws;
 };
 
@@ -123,7 +125,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     const int b = blockIdx.x, xcd = b % 8, local = b / 8, q = ntiles / 8, r = ntiles % 8;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
   }
-  const int m0 = (tile / TN) * TBM, n0 = (tile % TN) * TBN;
+  int mt = tile / TN, nt = tile % TN;
+  if (g.group_m > 1) {  // grouped order: concurrent tiles share group_m A panels and fewer B panels
+    const int grp = tile / (g.group_m * TN), mfirst = grp * g.group_m;
+    const int gsz = min(TM - mfirst, g.group_m), in = tile - grp * g.group_m * TN;
+    mt = mfirst + in % gsz;
+    nt = in / gsz;
+  }
+  const int m0 = mt * TBM, n0 = nt * TBN;
   const int bz = blockIdx.y;
   const short* Ap = g.A + bz * g.a_bs;
   const short* Bp = g.B + bz * g.b_bs;
@@ -326,6 +335,13 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   }
   if (K == 0) { s = 1; kc = TBK; }
   g.splits = s; g.kchunk = kc;
+  // tile order: groups of 4 M-panels walked column-major (projection at c2: 189 -> 173 us);
+  // MLVAE_GEMM_GROUP_M overrides (0/1 = plain row-major runs)
+  static const int group_m = [] {
+    const char* e = getenv("MLVAE_GEMM_GROUP_M");
+    return e ? atoi(e) : 4;
+  }();
+  g.group_m = group_m;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), batch, s);
   int rc;

@@ -2,7 +2,10 @@
 ROCm, gloo for CPU tests).  SURVEY.md 8(e):
 
 * every rank trains its own shard of the global batch with replicated weights;
-* the flat gradient buffer (8.70 M fp32 = 34.8 MB at c2) is summed with ONE all-reduce;
+* the flat gradient buffer (8.70 M fp32 = 34.8 MB at c2) is summed in two buckets: the top
+  LSTM layer + decoder heads (74 % of it at c2, final once the top layer's weight gradients
+  are done) on a communication stream while the lower layers' BPTT runs, the rest (bottom
+  layer + encoder) in optimizer_step;
 * the masked-mean denominators use the all-reduced valid-frame count, so each rank's
   gradient is its exact share of the global masked mean and the SUM over ranks equals the
   single-GPU gradient of the global batch (no 1/world rescale, exact for unequal lengths);
@@ -31,6 +34,16 @@ def broadcast_params(flat, group=None):
 def allreduce_step(grad_flat, loss3, group=None):
     """Sum the flat gradient buffer and the [kld, recon, total] loss shares over ranks."""
     dist.all_reduce(grad_flat, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(loss3, op=dist.ReduceOp.SUM, group=group)
+
+
+def allreduce_grad_bucket(buf, group=None):
+    """Sum one contiguous bucket of the flat gradient over ranks, in place, on the caller's
+    current stream."""
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+
+
+def allreduce_loss(loss3, group=None):
     dist.all_reduce(loss3, op=dist.ReduceOp.SUM, group=group)
 
 

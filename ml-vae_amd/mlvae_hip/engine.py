@@ -284,6 +284,12 @@ class VAEEngine:
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
         self.global_offset = 0      # first global utterance index of this shard
+        # data parallel: the gradient suffix from the top LSTM layer on (top layer + heads) is
+        # all-reduced on comm_stream during the lower layers' BPTT, the prefix in optimizer_step
+        self.bucket_allreduce = True
+        self.comm_stream = None
+        self._ar_pending = False
+        self.ar_split = self.layout.offsets[f"decoder.rnn.weight_ih_l{cfg.L - 1}"]
         if params is not None:
             self.load_reference_params(params)
 
@@ -750,6 +756,8 @@ class VAEEngine:
                       "dropout_bwd")
             if li > 0:
                 self._side(wgl)
+            if li == cfg.L - 1 and self.world > 1 and self.bucket_allreduce:
+                self._start_suffix_allreduce()
         # ---- encoder
         w_kl, _ = self.loss_weights()
         if w.enc_fused:
@@ -799,9 +807,29 @@ class VAEEngine:
                                 cfg.lr, b1, b2, cfg.adam_eps, cfg.max_grad_norm,
                                 _p(self.grad_norm), _p(self.hyp), 1, s), "adam")
 
+    def _start_suffix_allreduce(self):
+        """Everything the top LSTM layer's and the heads' gradients depend on is queued (the
+        side stream holds their weight-gradient GEMMs): sum that contiguous suffix of the flat
+        gradient over ranks on a communication stream, overlapping the lower layers' BPTT."""
+        from . import dist as mdist
+        if self.comm_stream is None:
+            self.comm_stream = torch.cuda.Stream(self.device)
+        self.comm_stream.wait_stream(torch.cuda.current_stream(self.device))
+        if self.overlap:
+            self.comm_stream.wait_stream(self.side_stream)
+        with torch.cuda.stream(self.comm_stream):
+            mdist.allreduce_grad_bucket(self.grad[self.ar_split:], self.process_group)
+        self._ar_pending = True
+
     def _allreduce_grads(self, w):
         from . import dist as mdist
-        mdist.allreduce_step(self.grad, w.loss, self.process_group)
+        if self._ar_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+            mdist.allreduce_grad_bucket(self.grad[:self.ar_split], self.process_group)
+            self._ar_pending = False
+        else:
+            mdist.allreduce_grad_bucket(self.grad, self.process_group)
+        mdist.allreduce_loss(w.loss, self.process_group)
 
     def _main(self):
         """Context: run on the high-priority main stream, ordered after (and before) the

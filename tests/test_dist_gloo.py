@@ -28,7 +28,13 @@ def _worker(rank, world, port, q):
     grad[shard] = mask.unsqueeze(-1).expand(-1, -1, C) / (count.item() * C)
     loss3 = torch.tensor([0.0, share.item(), share.item()])
     flat = grad.reshape(-1).clone()
+    buckets = grad.reshape(-1).clone()
     mdist.allreduce_step(flat, loss3)
+    # the engine's two buckets (suffix during the BPTT, prefix in optimizer_step) sum the same
+    split = 37
+    mdist.allreduce_grad_bucket(buckets[split:])
+    mdist.allreduce_grad_bucket(buckets[:split])
+    assert torch.equal(buckets, flat)
     params = torch.full((5,), float(rank))
     mdist.broadcast_params(params)
     q.put((rank, loss3[2].item(), flat.reshape(B, T, C), params))

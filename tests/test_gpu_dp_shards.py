@@ -34,6 +34,7 @@ def test_two_shards_sum_to_full_batch(monkeypatch):
     for r, sl in enumerate((slice(0, 2), slice(2, B))):
         eng = VAEEngine(cfg, params=params)
         eng.world, eng.global_offset = 2, sl.start
+        eng.bucket_allreduce = False  # no collective here: the shards are summed by hand
         w = eng.forward(x[sl].contiguous(), lens[sl].contiguous(), train=True)
         eng.backward(w)
         torch.cuda.synchronize()
@@ -45,3 +46,35 @@ def test_two_shards_sum_to_full_batch(monkeypatch):
     assert torch.allclose(lsum, wf.loss, rtol=1e-5, atol=1e-7), (lsum, wf.loss)
     scale = full.grad.abs().max().item()
     assert (gsum - full.grad).abs().max().item() <= 1e-5 * scale
+
+
+def test_bucketed_allreduce_sees_final_gradients(monkeypatch):
+    """world = 2 on one GPU with a stand-in collective that doubles its bucket on the stream it
+    is issued on: the suffix bucket (top LSTM layer + heads) goes out on the communication
+    stream during the bottom layer's BPTT, the prefix in optimizer_step.  Both must see the
+    final gradients: the result is exactly 2x a single engine's (bf16 path, side streams on)."""
+    need_gpu()
+    F, E, Z, H, L, C, B, T = 80, 64, 32, 128, 2, 64, 4, 60
+    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.0, prec="bf16")
+    params = O.init_params(F, E, Z, H, L, C, seed=3)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(B, T, F, generator=g).cuda()
+    eps = torch.randn(B, T, Z, generator=g).cuda()
+    lens = torch.tensor([1.0, 0.8, 0.55, 0.9]).cuda()
+    ref = VAEEngine(cfg, params=params)
+    wr = ref.forward(x, lens, eps=eps, train=True)
+    ref.backward(wr)
+    torch.cuda.synchronize()
+    monkeypatch.setattr(mdist, "allreduce_count", lambda c, group=None: c)
+    monkeypatch.setattr(mdist, "allreduce_grad_bucket", lambda b, group=None: b.mul_(2.0))
+    monkeypatch.setattr(mdist, "allreduce_loss", lambda l, group=None: l.mul_(2.0))
+    eng = VAEEngine(cfg, params=params)
+    eng.world = 2
+    w = eng.forward(x, lens, eps=eps, train=True)
+    eng.backward(w)
+    assert eng._ar_pending
+    eng._allreduce_grads(w)
+    torch.cuda.synchronize()
+    eng.check_errors()
+    assert torch.equal(eng.grad, 2.0 * ref.grad)
+    assert torch.equal(w.loss, 2.0 * wr.loss)
