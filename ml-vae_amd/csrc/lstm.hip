@@ -131,7 +131,7 @@ __device__ __forceinline__ bool tags_ok(u32x4 v, unsigned tag, bool g0, bool g1)
 // double-buffered for bf16 (one barrier per step); single-buffered for fp32, whose
 // resident weights leave no room for a second buffer (two barriers).
 template <int PREC, int HJ, int NL>
-__global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
+__global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   typedef typename Elt<PREC>::T ET;
   constexpr int ROWS = 4 * HJ, MT = ROWS / 16;       // gate rows, 16-row MFMA tiles
   constexpr int KS = 4;
@@ -139,8 +139,16 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
   constexpr int KSTEP = PREC == PREC_F32 ? 16 : 32;  // k consumed per 16-byte operand load
   constexpr int EPL = PREC == PREC_F32 ? 4 : 8;      // elements per 16-byte load
   constexpr int GE = Elt<PREC>::GE;
+  // bf16, 16 units per workgroup: a fifth "io" wave moves the step's HBM traffic through two
+  // LDS rings -- the input projection two steps ahead, the saved activations two steps behind
+  // -- so the four polling waves' memory queues hold nothing but the hand-off (an HBM load
+  // queued ahead of a poll delays it: 2.74 -> 2.14 us/step with the loads taken out)
+  constexpr bool IOW = PREC == PREC_BF16 && HJ == 16;
+  constexpr int GXS = 16 * 4 + 4, OUS = 16 * 8 + 4;  // padded per-utterance strides (floats)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f32x4* red0 = reinterpret_cast<f32x4*>(smem);  // [NRED][4][MT][64] partials
+  float* gxr = reinterpret_cast<float*>(smem + NRED * 4 * MT * 64 * 16);  // [2][16 utt][16 unit][4 gate]
+  float* outr = gxr + 2 * 16 * GXS;                                        // [2][16 utt][16 unit][8]
   __shared__ int abort_flag;
 
   const int ngroups = 2 * a.NB;
@@ -189,6 +197,66 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
   const bool plain_st = a.xcd_local && group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement);
   if (a.dbg && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
   if (tid == 0) abort_flag = 0;
+
+  // ---- io wave (IOW): lane (b = lane >> 2, g = lane & 3) moves the 64-byte row segment of
+  // utterance b, gate g, 16 units; lanes (b, kind) of the c / h / h-bf16 rows likewise
+  const int iob = lane >> 2, iog = lane & 3, iobg = grp * BG + iob;
+  const bool iobv = iobg < a.B;
+  f32x4 ld0[4], ld1[4];  // input-projection segments in flight (even / odd steps)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ld0[i] = ld1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto io_gload = [&](int s_, f32x4 (&v)[4]) {
+    if (iobv && s_ < T) {
+      const int t_ = dir ? T - 1 - s_ : s_;
+      const float* p = a.G + ((size_t)iobg * T + t_) * 8 * H + dir * 4 * H + iog * H + j0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const f32x4*>(p + 4 * i);
+    }
+  };
+  auto io_gwrite = [&](int s_, const f32x4 (&v)[4]) {
+    float* d = gxr + ((s_ & 1) * 16 + iob) * GXS + iog;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) d[u * 4] = v[u >> 2][u & 3];
+  };
+  auto io_store = [&](int s_) {
+    if (s_ < 0 || s_ >= T || (a.dbg_mode & 1)) return;
+    const int t_ = dir ? T - 1 - s_ : s_;
+    const float* src = outr + (s_ & 1) * 16 * OUS;
+    if (iobv) {  // activated gates of (b, g)
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = src[iob * OUS + u * 8 + iog];
+      float* gp = a.G + ((size_t)iobg * T + t_) * 8 * H + dir * 4 * H + iog * H + j0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<f32x4*>(gp + 4 * i) = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+    }
+    const int b2 = lane & 15, kind = lane >> 4, bg2 = grp * BG + b2;
+    if (kind < 3 && bg2 < a.B) {  // kind 0: c, 1: h, 2: h as bf16
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = src[b2 * OUS + u * 8 + (kind == 0 ? 4 : 5)];
+      const size_t o = ((size_t)bg2 * T + t_) * 2 * H + dir * H + j0;
+      if (kind < 2) {
+        float* dp = (kind == 0 ? a.Cs : a.Y) + o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<f32x4*>(dp + 4 * i) = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+      } else if (a.Yb) {
+        bf16x8 h0, h1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { h0[u] = f2bf(v[u]); h1[u] = f2bf(v[8 + u]); }
+        *reinterpret_cast<bf16x8*>(a.Yb + o) = h0;
+        *reinterpret_cast<bf16x8*>(a.Yb + o + 8) = h1;
+      }
+    }
+  };
+  if (IOW && wave == 4) {
+    io_gload(0, ld0);
+    io_gload(1, ld1);
+    io_gwrite(0, ld0);
+    io_gload(2, ld0);
+  }
   __syncthreads();
 
   const size_t xslot = (size_t)BG * a.Kp;  // elements per slot
@@ -199,15 +267,16 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
   // plain stores, so the compiler never has to drain those stores to order an aliasing load)
   float gx[4] = {0.f, 0.f, 0.f, 0.f};
   auto load_gx = [&](int s_) {
-    if (valid && s_ < T) {
+    if (valid && s_ < T && !(s_ > 0 && (a.dbg_mode & 2048))) {  // bit 11: timing without prefetch
       const int t_ = dir ? T - 1 - s_ : s_;
       const float* gp = a.G + ((size_t)bglob * T + t_) * 8 * H + dir * 4 * H + j0 + jj;
 #pragma unroll
       for (int g = 0; g < 4; ++g) gx[g] = gp[g * H];
     }
   };
-  load_gx(0);
+  if constexpr (!IOW) load_gx(0);
   float c = 0.f;
+  if (!IOW || wave < 4) {
   for (int s = 0; s < T; ++s) {
     STAMP(0);
     const int t = dir ? T - 1 - s : s;
@@ -283,6 +352,12 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
       if (KS > 1 && abort_flag) break;
       STAMP(3);
     }
+    if constexpr (IOW) {  // this step's input projection, staged by the io wave
+      if (owner) {
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(gxr + ((s & 1) * 16 + bi) * GXS + jj * 4);
+        gx[0] = g4[0]; gx[1] = g4[1]; gx[2] = g4[2]; gx[3] = g4[3];
+      }
+    }
     float ig = 0.f, fg = 0.f, gg = 0.f, og = 0.f, hv = 0.f;
     if (owner) {
       if (valid) {
@@ -319,13 +394,45 @@ __global__ __launch_bounds__(256) void lstm_fwd_kernel(LstmArgs a) {
       }
     }
     STAMP(4);
-    load_gx(s + 1);
-    if (valid && !(a.dbg_mode & 1)) {  // saved activations: plain stores, off the critical path
-      float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + jj;
-      gp[0] = ig; gp[H] = fg; gp[2 * H] = gg; gp[3 * H] = og;
-      a.Cs[n * 2 * H + dir * H + j0 + jj] = c;
-      a.Y[n * 2 * H + dir * H + j0 + jj] = hv;
-      if (a.Yb) a.Yb[n * 2 * H + dir * H + j0 + jj] = (unsigned short)f2bf(hv);
+    if constexpr (IOW) {  // saved activations into the out ring; the io wave stores them
+      if (owner) {
+        float* o = outr + ((s & 1) * 16 + bi) * OUS + jj * 8;
+        *reinterpret_cast<f32x4*>(o) = f32x4{ig, fg, gg, og};
+        o[4] = c;
+        o[5] = hv;
+      }
+    } else {
+      load_gx(s + 1);
+      if (valid && !(a.dbg_mode & 1)) {  // saved activations: plain stores, off the critical path
+        float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + jj;
+        gp[0] = ig; gp[H] = fg; gp[2 * H] = gg; gp[3 * H] = og;
+        a.Cs[n * 2 * H + dir * H + j0 + jj] = c;
+        a.Y[n * 2 * H + dir * H + j0 + jj] = hv;
+        if (a.Yb) a.Yb[n * 2 * H + dir * H + j0 + jj] = (unsigned short)f2bf(hv);
+      }
+    }
+  }
+  } else if constexpr (IOW) {
+    // io wave: one barrier per step s >= 1 like the polling waves.  Before barrier s: the
+    // input projection of step s into ring slot s & 1 (loaded two steps ago), the load of
+    // step s + 2, and the stores of step s - 2's activations (written before barrier s - 1)
+    auto io_step = [&](int s_, f32x4 (&v)[4]) -> bool {
+      io_gwrite(s_, v);
+      io_gload(s_ + 2, v);
+      io_store(s_ - 2);
+      __syncthreads();
+      return !abort_flag;
+    };
+    for (int s = 1; s < T; s += 2) {
+      if (!io_step(s, ld1)) break;
+      if (s + 1 < T && !io_step(s + 1, ld0)) break;
+    }
+  }
+  if constexpr (IOW) {
+    __syncthreads();  // the last step's activations are in the ring
+    if (wave == 4) {
+      io_store(T - 2);
+      io_store(T - 1);
     }
   }
 }
@@ -639,7 +746,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
   struct CellIn { float gi, gf, gg, go, cc, cp, dy; };
   const int j = j0 + uc;
   auto load_cell = [&](int s_, CellIn& c) {
-    if (bvalid && s_ < T) {
+    if (bvalid && s_ < T && !(s_ > 0 && (a.dbg_mode & 2048))) {  // bit 11: timing without prefetch
       const int t_ = dir ? s_ : T - 1 - s_;
       const int tp_ = dir ? t_ + 1 : t_ - 1;
       const size_t n_ = (size_t)bglob * T + t_;
@@ -827,6 +934,7 @@ Plan make_plan(int B, int H, int prec, bool fwd) {
   const int hjt = p.HJ > 16 ? p.HJ : 16;
   p.lds = fwd ? (size_t)(prec == PREC_F32 ? 1 : 2) * 4 * (p.HJ / 4) * 64 * 16
               : (size_t)2 * 4 * 16 * hjt * 4;
+  if (fwd && prec == PREC_BF16 && p.HJ == 16) p.lds += (size_t)2 * 16 * (68 + 132) * 4;  // io rings
   // > half of the CU's LDS keeps a second recurrence workgroup off the CU; bit 3 of the
   // diagnostics mode reserves enough to keep a 74 KB GEMM workgroup off it too
   const size_t min_lds = (g_dbg_mode & 8) ? (size_t)100 * 1024 : (size_t)MIN_LDS;
@@ -865,7 +973,8 @@ int launch_nl(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
     mlvae_set_error("lstm: cannot reserve %zu B LDS", lds);
     return 2;
   }
-  k<<<grid, 256, lds, s>>>(a);
+  const int nthr = (fwd && PREC == PREC_BF16 && HJ == 16) ? 320 : 256;  // + the io wave
+  k<<<grid, nthr, lds, s>>>(a);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
