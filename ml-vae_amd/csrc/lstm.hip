@@ -150,6 +150,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   float* gxr = reinterpret_cast<float*>(smem + NRED * 4 * MT * 64 * 16);  // [2][16 utt][16 unit][4 gate]
   float* outr = gxr + 2 * 16 * GXS;                                        // [2][16 utt][16 unit][8]
   __shared__ int abort_flag;
+  __shared__ volatile int poll_seq;  // last step whose hand-off wave 0 has received
 
   const int ngroups = 2 * a.NB;
   int gid, js;
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   }
   const bool plain_st = a.xcd_local && group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement);
   if (a.dbg && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
-  if (tid == 0) abort_flag = 0;
+  if (tid == 0) { abort_flag = 0; poll_seq = 0; }
 
   // ---- io wave (IOW): lane (b = lane >> 2, g = lane & 3) moves the 64-byte row segment of
   // utterance b, gate g, 16 units; lanes (b, kind) of the c / h / h-bf16 rows likewise
@@ -310,6 +311,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
           if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
         }
         STAMP(1);
+        if (tid == 0) poll_seq = s;  // the io wave issues its HBM traffic behind this poll
         if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
           a.dbg[(size_t)s * 16 + 5] = t_issue;
           a.dbg[(size_t)s * 16 + 6] = spins;
@@ -418,6 +420,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
     // step s + 2, and the stores of step s - 2's activations (written before barrier s - 1)
     auto io_step = [&](int s_, f32x4 (&v)[4]) -> bool {
       io_gwrite(s_, v);
+      // issue the HBM traffic only once step s_'s hand-off has arrived, so that it has drained
+      // before the next poll is issued (measured 2.34 -> 2.18 us/step)
+      for (unsigned sp = 0; poll_seq < s_ && sp < SPIN_LIMIT; ++sp) __builtin_amdgcn_s_sleep(1);
       io_gload(s_ + 2, v);
       io_store(s_ - 2);
       __syncthreads();

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmlvae.so")
+LIB_PATH = os.environ.get("MLVAE_LIB_PATH") or os.path.join(_HERE, "libmlvae.so")  # override: A/B timing
 
 P = C.c_void_p
 I = C.c_int
