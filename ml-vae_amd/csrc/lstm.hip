@@ -764,12 +764,15 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
     }
   };
   float dc = 0.f;
-  // one BPTT step; false = abort (spin limit)
-  auto step = [&](int s, const CellIn& cur, CellIn& nxt) -> bool {
+  // one BPTT step; false = abort (spin limit).  The cell inputs of step s + 2 are loaded right
+  // behind step s's hand-off (three rotating buffers): a full step before the next poll is
+  // issued, so that poll does not queue behind HBM loads in this wave's memory queue
+  auto step = [&](int s, const CellIn& cur, CellIn& fill) -> bool {
     STAMP(0);
     const int t = dir ? s : T - 1 - s;
     const size_t n = (size_t)bglob * T + t;
     float dhrec = 0.f;
+    if (s == 0) load_cell(2, fill);
     if (s > 0) {
       const unsigned tag = step_tag(s - 1);
       const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot + (size_t)js * NJ * 256 +
@@ -795,6 +798,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
       }
       STAMP(1);
       WSTAMP(8);
+      load_cell(s + 2, fill);
       if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
         a.dbg[(size_t)s * 16 + 5] = t_issue;
         a.dbg[(size_t)s * 16 + 6] = spins;
@@ -844,8 +848,6 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
       dG2 = dcs * cur.gi * (1.f - cur.gg * cur.gg);
       dG3 = d_o * cur.go * (1.f - cur.go);
     }
-    // prefetch after the cell math: its operand waits then cover only loads already landed
-    load_cell(s + 1, nxt);
     if (s + 1 < T) {
       short* A = abuf + (s & 1) * 16 * AST;
       bf16x4 pk = {f2bf(dG0), f2bf(dG1), f2bf(dG2), f2bf(dG3)};
@@ -894,11 +896,13 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
     }
     return true;
   };
-  CellIn c0 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  CellIn c0 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0;
   load_cell(0, c0);
-  for (int s = 0; s < T; s += 2) {
-    if (!step(s, c0, c1)) break;
+  load_cell(1, c1);
+  for (int s = 0; s < T; s += 3) {
+    if (!step(s, c0, c2)) break;
     if (s + 1 < T && !step(s + 1, c1, c0)) break;
+    if (s + 2 < T && !step(s + 2, c2, c1)) break;
   }
 }
 
