@@ -427,33 +427,33 @@ __global__ __launch_bounds__(256) void encoder_bwd_kernel(EncBwdArgs a) {
     slab[2 * EW * EW + EW * F + tid] = (sb[0][tid] + sb[1][tid]) + (sb[2][tid] + sb[3][tid]);
 }
 
-// sum the per-workgroup slabs in a fixed order (4 interleaved chains) into the gradients
+// sum the per-workgroup slabs into the gradients: a block covers 64 slab elements with four
+// threads each (slab quarters, summed in order), combined in a fixed order through LDS
 template <int F>
 __global__ __launch_bounds__(256) void encoder_reduce(int G, const float* __restrict__ ws,
                                                       float* __restrict__ dwml, float* __restrict__ dbml,
                                                       float* __restrict__ dw1, float* __restrict__ db1,
                                                       float* __restrict__ dw0, float* __restrict__ db0) {
   constexpr int SLAB = slab_floats<F>();
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < SLAB; i += gridDim.x * 256) {
-    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-    int g = 0;
-    for (; g + 4 <= G; g += 4) {
-      v0 += ws[(size_t)g * SLAB + i];
-      v1 += ws[(size_t)(g + 1) * SLAB + i];
-      v2 += ws[(size_t)(g + 2) * SLAB + i];
-      v3 += ws[(size_t)(g + 3) * SLAB + i];
-    }
-    for (; g < G; ++g) v0 += ws[(size_t)g * SLAB + i];
-    const float v = (v0 + v1) + (v2 + v3);
-    if (i < EW * EW) dwml[i] = v;
-    else if (i < 2 * EW * EW) dw1[i - EW * EW] = v;
-    else if (i < 2 * EW * EW + EW * F) dw0[i - 2 * EW * EW] = v;
-    else {
-      const int c = i - (2 * EW * EW + EW * F);
-      if (c < EW) dbml[c] = v;
-      else if (c < 2 * EW) db1[c - EW] = v;
-      else db0[c - 2 * EW] = v;
-    }
+  __shared__ float part[4][64];
+  const int e = threadIdx.x & 63, qtr = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + e;
+  const int g0 = qtr * G / 4, g1 = (qtr + 1) * G / 4;
+  float v = 0.f;
+  if (i < SLAB)
+    for (int g = g0; g < g1; ++g) v += ws[(size_t)g * SLAB + i];
+  part[qtr][e] = v;
+  __syncthreads();
+  if (qtr != 0 || i >= SLAB) return;
+  v = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
+  if (i < EW * EW) dwml[i] = v;
+  else if (i < 2 * EW * EW) dw1[i - EW * EW] = v;
+  else if (i < 2 * EW * EW + EW * F) dw0[i - 2 * EW * EW] = v;
+  else {
+    const int c = i - (2 * EW * EW + EW * F);
+    if (c < EW) dbml[c] = v;
+    else if (c < 2 * EW) db1[c - EW] = v;
+    else db0[c - 2 * EW] = v;
   }
 }
 
@@ -546,7 +546,7 @@ extern "C" int mlvae_encoder_bwd(int B, int T, int F, int E, int Z, const float*
   a.ws = ws;
   hipStream_t st = (hipStream_t)stream;
   const int slab = 2 * EW * EW + EW * F + 3 * EW;
-  const int rblocks = (slab + 255) / 256;
+  const int rblocks = (slab + 63) / 64;
   if (F == 80) {
     encoder_bwd_kernel<80><<<G, 256, 0, st>>>(a);
     MLVAE_CHECK_LAUNCH();

@@ -65,6 +65,59 @@ __global__ __launch_bounds__(256) void skinny_nt_kernel(int M, int K, const unsi
   for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + 16 * j + 4 * q) = acc[j];
 }
 
+// K split over the four waves of a 16-row workgroup (4x the loads in flight per row tile;
+// the NT loop above is latency-bound at B*T = 16,000 rows: 67 us), partials summed in LDS in
+// a fixed order.  K % 128 == 0.
+template <int NT>
+__global__ __launch_bounds__(256) void skinny_nt_ks_kernel(int M, int K, const unsigned short* __restrict__ A,
+                                                           int lda, const unsigned short* __restrict__ Bt,
+                                                           int ldb, float* __restrict__ C, int ldc) {
+  __shared__ f32x4 red[3][NT][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int row = blockIdx.x * 16 + l15;
+  const bool rv = row < M;
+  const int kq = K / 4, kb = wave * kq;
+  const unsigned short* ap = A + (size_t)(rv ? row : 0) * lda + kb + 8 * q;
+  const unsigned short* bp = Bt + (size_t)l15 * ldb + kb + 8 * q;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;
+  int k = 0;
+  for (; k + 32 * U <= kq; k += 32 * U) {
+    bf16x8 af[U], bf[U][NT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      af[u] = rv ? *reinterpret_cast<const bf16x8*>(ap + k + 32 * u) : z8;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        bf[u][j] = *reinterpret_cast<const bf16x8*>(bp + (size_t)16 * j * ldb + k + 32 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = mfma16(bf[u][j], af[u], acc[j]);
+  }
+  for (; k < kq; k += 32) {
+    const bf16x8 a1 = rv ? *reinterpret_cast<const bf16x8*>(ap + k) : z8;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      acc[j] = mfma16(*reinterpret_cast<const bf16x8*>(bp + (size_t)16 * j * ldb + k), a1, acc[j]);
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) red[wave - 1][j][lane] = acc[j];
+  }
+  __syncthreads();
+  if (wave != 0 || !rv) return;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + 16 * j + 4 * q) =
+        ((acc[j] + red[0][j][lane]) + red[1][j][lane]) + red[2][j][lane];
+}
+
 // LDS images: A [64 frames][64 m + 8], B [64 frames][NB + 8] (bf16); transposed fragment reads.
 template <int NT>
 __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk,
@@ -172,6 +225,17 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
   const unsigned short* a = static_cast<const unsigned short*>(A);
   const unsigned short* b = static_cast<const unsigned short*>(Bt);
   hipStream_t st = (hipStream_t)stream;
+  if (K % 128 == 0) {
+    dim3 g16((M + 15) / 16);
+    switch (N / 16) {
+      case 1: skinny_nt_ks_kernel<1><<<g16, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      case 2: skinny_nt_ks_kernel<2><<<g16, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      case 3: skinny_nt_ks_kernel<3><<<g16, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      default: skinny_nt_ks_kernel<4><<<g16, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+    }
+    MLVAE_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid((M + 63) / 64);
   switch (N / 16) {
     case 1: skinny_nt_kernel<1><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;

@@ -691,13 +691,8 @@ class VAEEngine:
 
             def wgl(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx, Ybl=Ybl):
                 if li == 0 and w.enc_fused:
-                    # dW_ih_l0 | db_ih_l0 = db_hh_l0 = dG^T [z | 1] (skinny.hip), then both
-                    # directions' dW_hh_l0 in one batched 256² launch
-                    ws = w.gws_side if self._on_side else w.gws
-                    check(lib().mlvae_skinny_tn(8 * H, w.ZA, N, _pb(dG_bf), 8 * H, _pb(w.Zb), w.ZA, Z,
-                                                gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
-                                                gp("decoder.rnn.bias_hh_l0"), _p(ws), w.gws_bytes,
-                                                self._stream()), "skinny_tn")
+                    # both directions' dW_hh_l0 in one batched 256² launch; dW_ih_l0 and the
+                    # biases follow the encoder backward on the main stream (skinny_tn below)
                     self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
                                gp("decoder.rnn.weight_hh_l0"), H, batch=2, a_bs=4 * H, b_bs=H,
                                c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
@@ -770,6 +765,11 @@ class VAEEngine:
                                       ge("fc.0.blocks.2.weight"), ge("fc.0.blocks.2.bias"),
                                       ge("fc.0.blocks.0.weight"), ge("fc.0.blocks.0.bias"), _p(w.enc_ws),
                                       w.enc_ws.numel() * 4, s), "encoder_bwd")
+            # dW_ih_l0 | db_ih_l0 = db_hh_l0 = dG^T [z | 1] (skinny.hip), on the main stream
+            # while the side stream finishes dW_hh_l0 (the step's two tails run side by side)
+            check(l.mlvae_skinny_tn(8 * H, w.ZA, N, _pb(w.dGb[0]), 8 * H, _pb(w.Zb), w.ZA, Z,
+                                    gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
+                                    gp("decoder.rnn.bias_hh_l0"), _p(w.gws), w.gws_bytes, s), "skinny_tn")
             self._join_side()
             return
         check(l.mlvae_reparam_kl_bwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(w.lens), count,
