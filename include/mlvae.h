@@ -232,6 +232,28 @@ int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
 int mlvae_dropout_ex(size_t n, const float* x, float* y, void* y_bf16, const float* mask,
                      unsigned long long seed, float p, void* stream);
 
+/* GMM-VAE latent block (SURVEY 8(f) rank 1; replaces ref:src/modules/gmm_vae.py:24-67).
+ * P = the five heads as one stacked GEMM output, rows of width >= 4*N*Z + N:
+ * [prior_mean | prior_log_var | mean | log_var] (N*Z each), then the N gmm logits.
+ * Forward: z = eps*exp(lv/2) + mean; kl = -0.5(1 + lv - plv - (e^lv + (m-pm)^2)/(e^plv + 1e-5));
+ * w = hard Gumbel-softmax(logits, tau) (straight-through value), ysoft = its soft sample.
+ * expo = the Exp(1) draws [rows, N] or NULL: Philox(seed, offset + r*N + n) (ref :31).
+ * Backward: dP from dz, dkl, dw (each NULL = 0); logits get the straight-through gradient. */
+int mlvae_gmm_latent_fwd(int rows, int N, int Z, const float* P, int ldp, const float* eps,
+                         const float* expo, unsigned long long seed, unsigned long long offset,
+                         float tau, float* z, float* kl, float* w, float* ysoft, void* stream);
+int mlvae_gmm_latent_bwd(int rows, int N, int Z, const float* P, int ldp, const float* eps,
+                         const float* ysoft, float tau, const float* dz, const float* dkl,
+                         const float* dw, float* dP, int lddp, void* stream);
+/* apply_weight (ref:src/utils/data_utils.py:32-64): y[r,c] = sum_n w[r,n] x[r, n*C + c];
+ * backward dx[r, n*C + c] = w[r,n] dy[r,c] and dw[r,n] = sum_c dy[r,c] x[r, n*C + c]
+ * (dx or dw may be NULL). */
+int mlvae_apply_weight_fwd(int rows, int N, int C, const float* x, int ldx, const float* w,
+                           float* y, int ldy, void* stream);
+int mlvae_apply_weight_bwd(int rows, int N, int C, const float* x, int ldx, const float* w,
+                           const float* dy, int lddy, float* dx, int lddx, float* dw,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

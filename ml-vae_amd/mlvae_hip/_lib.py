@@ -68,6 +68,10 @@ _SIGS = {
     "mlvae_lrelu_bwd": [SZ, P, P, P, P],
     "mlvae_clip_scale": [P, SZ, P, I, F, P, P],
     "mlvae_masked_mean_bwd": [I, I, I, P, I, P, P, P],
+    "mlvae_gmm_latent_fwd": [I, I, I, P, I, P, P, U64, U64, F, P, P, P, P, P],
+    "mlvae_gmm_latent_bwd": [I, I, I, P, I, P, P, F, P, P, P, P, I, P],
+    "mlvae_apply_weight_fwd": [I, I, I, P, I, P, P, I, P],
+    "mlvae_apply_weight_bwd": [I, I, I, P, I, P, P, I, P, I, P, P],
     "mlvae_lstm_set_debug": [P],
     "mlvae_lstm_set_debug_mode": [I],
 }

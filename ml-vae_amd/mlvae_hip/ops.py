@@ -362,3 +362,78 @@ def bilstm(x, lstm_module, train):
     p = float(lstm_module.dropout) if train else 0.0
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
     return BiLSTMFn.apply(x, H, L, p, seed, *weights)
+
+
+# --------------------------------------------------------------------------- GMM-VAE / H-VAE
+class GmmLatentFn(torch.autograd.Function):
+    """GMM-VAE latent block on the stacked head output P = [pm | plv | m | lv | logits]
+    (ref:src/modules/gmm_vae.py:24-67): returns z, per-element KL and the straight-through
+    hard Gumbel-softmax weights.  expo = the Exp(1) draws [.., N] (None: library Philox)."""
+
+    @staticmethod
+    def forward(ctx, P, eps, expo, N, Z, tau, seed):
+        P, eps = _need(P, "gmm heads"), _need(eps, "eps")
+        expo = _need(expo, "expo") if expo is not None else None
+        rows = _rows(P)
+        z = torch.empty(*P.shape[:-1], N * Z, device=P.device, dtype=torch.float32)
+        kl = torch.empty_like(z)
+        w = torch.empty(*P.shape[:-1], N, device=P.device, dtype=torch.float32)
+        ysoft = torch.empty_like(w)
+        check(lib().mlvae_gmm_latent_fwd(rows, N, Z, _p(P), P.shape[-1], _p(eps),
+                                         _p(expo) if expo is not None else None, seed, 0, tau,
+                                         _p(z), _p(kl), _p(w), _p(ysoft), _stream()),
+              "gmm_latent_fwd")
+        ctx.save_for_backward(P, eps, ysoft)
+        ctx.shape = (N, Z, tau)
+        return z, kl, w
+
+    @staticmethod
+    def backward(ctx, dz, dkl, dw):
+        P, eps, ysoft = ctx.saved_tensors
+        N, Z, tau = ctx.shape
+        opt = lambda t, n: _need(t, n) if t is not None else None
+        dz, dkl, dw = opt(dz, "dz"), opt(dkl, "dkl"), opt(dw, "dw")
+        dP = torch.empty_like(P)
+        nz = lambda t: _p(t) if t is not None else None
+        check(lib().mlvae_gmm_latent_bwd(_rows(P), N, Z, _p(P), P.shape[-1], _p(eps), _p(ysoft),
+                                         tau, nz(dz), nz(dkl), nz(dw), _p(dP), P.shape[-1],
+                                         _stream()), "gmm_latent_bwd")
+        return dP, None, None, None, None, None, None
+
+
+class ApplyWeightFn(torch.autograd.Function):
+    """y[.., c] = sum_n w[.., n] x[.., n*C + c] (ref:src/utils/data_utils.py:32-64)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x, w = _need(x, "apply_weight x"), _need(w, "apply_weight weight")
+        N = w.shape[-1]
+        C = x.shape[-1] // N
+        rows = _rows(w)
+        if x.numel() != rows * N * C:
+            raise ValueError(f"apply_weight: x {tuple(x.shape)} does not match weight {tuple(w.shape)}")
+        y = torch.empty(*w.shape[:-1], C, device=x.device, dtype=torch.float32)
+        check(lib().mlvae_apply_weight_fwd(rows, N, C, _p(x), N * C, _p(w), _p(y), C, _stream()),
+              "apply_weight_fwd")
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = _need(dy, "apply_weight grad")
+        N = w.shape[-1]
+        C = x.shape[-1] // N
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        check(lib().mlvae_apply_weight_bwd(_rows(w), N, C, _p(x), N * C, _p(w), _p(dy), C,
+                                           _p(dx) if dx is not None else None, N * C,
+                                           _p(dw) if dw is not None else None, _stream()),
+              "apply_weight_bwd")
+        return dx, dw
+
+
+def apply_weight(x, weight):
+    """(B,T,N*C) or (B,T,N,C) weighted by (B,T,N) -> (B,T,C)."""
+    B, T, N = weight.shape
+    return ApplyWeightFn.apply(x.reshape(B, T, -1), weight)

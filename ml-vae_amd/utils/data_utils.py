@@ -18,3 +18,10 @@ def apply_lens_to_loss(loss, lens, reduction='mean'):
     """sum(loss * mask) / sum(mask) ('mean'), / B ('batchmean') or per utterance ('batch'),
     mask = frames t < lens*T (relative lengths, fp32 compare as SpeechBrain's length_to_mask)."""
     return ops.masked_mean(loss, lens, reduction)
+
+
+def apply_weight(x, weight):
+    """Mixture weighting as one HIP launch (ref:src/utils/data_utils.py:32-64).
+
+    x: (B, T, N, C) or (B, T, N * C); weight: (B, T, N) -> (B, T, C)."""
+    return ops.apply_weight(x, weight)

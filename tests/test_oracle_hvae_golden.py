@@ -71,3 +71,17 @@ def test_apply_weight_matches_reference():
     for tag in ("flat", "split"):
         x, w, y = (torch.from_numpy(d[f"{tag}/{k}"]) for k in "xwy")
         assert rel(O.apply_weight(x, w), y) < 1e-6
+
+
+@pytest.mark.parametrize("case", ["gmm_tiny", "hvae_tiny"])
+def test_module_state_dict_matches_reference(case):
+    """The HIP-backed modules keep the reference's parameter names and shapes (checkpoints load)."""
+    from modules.gmm_vae import GMMVAE
+    from modules.h_vae import HierarchicalVAE
+    meta, params, *_ = load(case)
+    cls = GMMVAE if meta["kind"] == "gmm" else HierarchicalVAE
+    m = cls([meta["F"], meta["E"], meta["E"]], meta["Z"], meta["N"])
+    sd = m.state_dict()
+    assert list(sd) == meta["param_names"]
+    assert all(sd[k].shape == params[k].shape for k in sd)
+    m.load_state_dict(dict(params))
