@@ -66,6 +66,11 @@ int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K, float alph
  * order.  Replaces the LSTM input projection, its dgrad and the weight gradients
  * (ref:src/modules/decoder.py:14-15,22). */
 size_t mlvae_gemm_bf16_workspace_size(int M, int N, int K, int batch);
+/* split-K planning target of mlvae_gemm_bf16 in workgroups (default 256, one per CU); returns
+ * the previous value (values < 1 only query).  Host-side launch planning state: set it on the
+ * launching thread right before the launches it should shape (the engine lowers it for weight
+ * gradients that overlap a recurrence).  Workspace sizes assume the default or lower. */
+int mlvae_gemm_bf16_set_split_target(int workgroups);
 int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch, const void* A,
                     int lda, long long a_bstride, const void* B, int ldb, long long b_bstride,
                     float* C, int ldc, long long c_bstride, float beta, const float* bias1,

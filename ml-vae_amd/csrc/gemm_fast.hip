@@ -256,11 +256,17 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s) {
 // split-K: long-K products (weight gradients over B*T frames) with fewer tiles than half the
 // CUs, until ~1 workgroup per CU, keeping >= 8 K-steps per split (at >= 128 tiles the extra
 // partial-slab round trip costs more than the idle CUs: dgrad 252 tiles, 224 vs 196 us)
+// split-K workgroup target (~256 = one per CU).  mlvae_gemm_bf16_set_split_target() lowers it
+// for weight gradients that overlap a recurrence: fewer workgroups leave CUs and memory
+// bandwidth to the latency-bound hand-off chain (c2: 256 -> 128 takes 0.15 ms off the step).
+int g_split_target = 256;
+int split_target() { return g_split_target; }
+
 void fast_plan(int M, int N, int K, int batch, int* splits, int* kchunk) {
   const long tiles = (long)((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN) * batch;
   int s = 1;
   if (tiles < 128 && K >= TBK * 16) {
-    s = (int)((256 + tiles - 1) / tiles);
+    s = (int)((split_target() + tiles - 1) / tiles);
     const int maxs = K / (TBK * 8);
     if (s > maxs) s = maxs;
     if (s > 32) s = 32;
@@ -274,6 +280,12 @@ void fast_plan(int M, int N, int K, int batch, int* splits, int* kchunk) {
 }
 
 }  // namespace
+
+extern "C" int mlvae_gemm_bf16_set_split_target(int workgroups) {
+  const int prev = g_split_target;
+  if (workgroups >= 1) g_split_target = workgroups;
+  return prev;
+}
 
 extern "C" size_t mlvae_gemm_bf16_workspace_size(int M, int N, int K, int batch) {
   int s, kc;

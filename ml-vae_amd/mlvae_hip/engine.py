@@ -274,6 +274,10 @@ class VAEEngine:
         self.rng_step = 0
         self._work = {}
         self.overlap = True         # weight-gradient GEMMs on a side stream
+        # split-K workgroup targets of the weight-gradient GEMMs (mlvae_gemm_bf16): those that
+        # overlap a recurrence / those in the step's tail (env overrides for A/B sweeps)
+        self.split_overlap = int(os.environ.get("MLVAE_SPLIT_OVERLAP", "128"))
+        self.split_tail = int(os.environ.get("MLVAE_SPLIT_TAIL", "256"))
         self.side_stream = torch.cuda.Stream(self.device)
         # the step's critical path (recurrences, dgrads) runs on a high-priority stream so the
         # dispatcher prefers its workgroups over the side stream's weight-gradient GEMMs
@@ -689,7 +693,18 @@ class VAEEngine:
             pgb = lambda t, off=0: None if t is None else _pb(t, off)
             Ybl = w.Yb[li] if w.bf else None
 
-            def wgl(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx, Ybl=Ybl):
+            def wgl(li=li, **kw):
+                # split-K target: the upper layers' weight gradients overlap the next BPTT, so
+                # they take half the CUs; the bottom layer's run in the step's tail
+                prev = l.mlvae_gemm_bf16_set_split_target(self.split_tail if li == 0 else
+                                                          self.split_overlap)
+                try:
+                    wgl_body(li=li, **kw)
+                finally:
+                    l.mlvae_gemm_bf16_set_split_target(prev)
+
+            def wgl_body(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx,
+                         Ybl=Ybl):
                 if li == 0 and w.enc_fused:
                     # both directions' dW_hh_l0 in one batched 256² launch; dW_ih_l0 and the
                     # biases follow the encoder backward on the main stream (skinny_tn below)
