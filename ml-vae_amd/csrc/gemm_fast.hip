@@ -212,6 +212,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       float* cp = Cb + (size_t)row * g.ldc + col;
       if (vec && col + 3 < g.N && g.beta == 0.f && g.epi == EPI_NONE) {
         *reinterpret_cast<f32x4*>(cp) = acc[i][j] + b;
+      } else if (vec && col + 3 < g.N && g.beta == 0.f && g.epi == EPI_DROPOUT) {
+        // the 4 columns are one aligned Philox counter (row*ldc + col is a multiple of 4):
+        // one call gives all four mask words, as dropout_scale() does element by element
+        unsigned w4[4];
+        philox4(g.dseed, ((size_t)row * g.ldc + col) >> 2, w4);
+        f32x4 v = acc[i][j] + b;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
+        *reinterpret_cast<f32x4*>(cp) = v;
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)

@@ -1,5 +1,6 @@
 """Time the train step's big GEMM shapes (c2, bf16 operands): mlvae_gemm_ex (128² register-staged)
-against mlvae_gemm_bf16 (256² LDS-DMA).  usage: python tools/gemm_bench.py"""
+against mlvae_gemm_bf16 (256² LDS-DMA), with torch.matmul (hipBLASLt, bf16 out) as the
+library reference point.  usage: python tools/gemm_bench.py"""
 import os
 import sys
 
@@ -25,6 +26,9 @@ def run(ta, tb, M, Nc, K, fast, iters=10):
     B = (torch.rand(Nc, K) if tb else torch.rand(K, Nc)).sub(0.5).to(torch.bfloat16).cuda()
     C = torch.empty(M, Nc, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
+    if fast == 2:  # hipBLASLt through torch
+        At, Bt = (A.t() if ta else A), (B.t() if tb else B)
+        return _time(lambda: torch.matmul(At, Bt), iters, M, Nc, K)
     wsz = l.mlvae_gemm_bf16_workspace_size(M, Nc, K, 1) if fast else l.mlvae_gemm_ex_workspace_size(M, Nc, K)
     ws = torch.empty(wsz // 4 + 1, device="cuda")
 
@@ -37,6 +41,10 @@ def run(ta, tb, M, Nc, K, fast, iters=10):
             check(l.mlvae_gemm_ex(ta, tb, M, Nc, K, 1.0, A.data_ptr(), 1, A.shape[1], B.data_ptr(),
                                   1, B.shape[1], 0.0, C.data_ptr(), Nc, None, None, 0, None, 0, 0, 0,
                                   ws.data_ptr(), ws.numel() * 4, s))
+    return _time(call, iters, M, Nc, K)
+
+
+def _time(call, iters, M, Nc, K):
     for _ in range(3):
         call()
     torch.cuda.synchronize()
@@ -53,10 +61,10 @@ def run(ta, tb, M, Nc, K, fast, iters=10):
 def main():
     for name, ta, tb, M, Nc, K in SHAPES:
         r = []
-        for fast in (0, 1):
+        for fast in (0, 1, 2):
             ms, tf = run(ta, tb, M, Nc, K, fast)
             r.append(f"{ms * 1e3:7.1f} us {tf:6.1f} TF")
-        print(f"{name} M={M:5d} N={Nc:5d} K={K:5d} | gemm_ex: {r[0]} | gemm_bf16 256²: {r[1]}", flush=True)
+        print(f"{name} M={M:5d} N={Nc:5d} K={K:5d} | gemm_ex: {r[0]} | gemm_bf16 256²: {r[1]} | hipBLASLt: {r[2]}", flush=True)
 
 
 if __name__ == "__main__":
