@@ -22,6 +22,7 @@
 // The backward's weight gradients (sums over frames) read the 64-frame tile's activations and
 // gradients back through LDS with transposing reads (ds_read_b64_tr_b16).
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -247,8 +248,15 @@ template <int F>
 constexpr int slab_floats() { return 2 * EW * EW + EW * F + 3 * EW; }
 
 int bwd_grid(int N) {
+  // cap on workgroups (each folds its tiles into one weight-gradient slab); MLVAE_ENC_BWD_GRID
+  // overrides it for A/B timing
+  static const int cap = [] {
+    const char* e = getenv("MLVAE_ENC_BWD_GRID");
+    const int v = e ? atoi(e) : 128;
+    return v < 1 ? 128 : v;
+  }();
   const int tiles = (N + 63) / 64;
-  return tiles > 128 ? 128 : (tiles < 1 ? 1 : tiles);
+  return tiles > cap ? cap : (tiles < 1 ? 1 : tiles);
 }
 
 template <int F>
