@@ -153,6 +153,11 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
  *   = column nw of the product (B's column nw all ones: the bias gradient as MFMA work).  Frame
  *   splits go to fp32 slabs (workspace: mlvae_skinny_tn_workspace_size) summed in a fixed order.
  * Replace the autograd of layer 0's input projection (ref:src/modules/decoder.py:14-15,22). */
+/* C[M, N] = A[M, K] B[N, K]^T + bias1 + bias2 (bf16 operands, k-contiguous, fp32 C), K in
+ * {8, 16, 24, 32}, N % 16 == 0, 16-byte aligned rows; biases may be NULL.  The layer-0 LSTM
+ * input projection z W_ih^T + b_ih + b_hh (ref:src/modules/decoder.py:14-15,22), K = latent. */
+int mlvae_skinny_proj(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                      const float* bias1, const float* bias2, float* C, int ldc, void* stream);
 int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                     float* C, int ldc, void* stream);
 size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K);

@@ -9,6 +9,11 @@
 // skinny_nt: C[M, NB] = A[M, K] . Bt[NB, K]^T, A and Bt k-contiguous bf16.  A wave owns 16 rows
 //   and all NB columns; fragments are loaded straight from global (16 B per lane, four K-steps
 //   in flight); operands swapped so a lane stores 4 consecutive columns.
+// skinny_proj: C[M, N] = A[M, K] . B[N, K]^T + bias1 + bias2 with K <= 32 (fp32 C): the layer-0
+//   input projection G = z W_ih^T + b_ih + b_hh, whose K is the latent width.  One MFMA per
+//   16 x 16 output block, fragments straight from global (W_ih is L2-resident), no LDS, small
+//   register footprint: many waves per CU keep the 16-byte stores of the write-bound output
+//   in flight (the 256-wide LDS tile ran one workgroup per CU and serialised its epilogue).
 // skinny_tn: P_s[M, NB] = A[Ks, M]^T . B[Ks, NB] over one frame range Ks per split s; A and B
 //   m/n-contiguous bf16, staged through LDS (64 frames per chunk) and read with
 //   ds_read_b64_tr_b16; fp32 partial slabs per split, reduced in a fixed order by
@@ -204,6 +209,37 @@ __global__ __launch_bounds__(256) void skinny_reduce(int M, int NB, int S, int n
   }
 }
 
+constexpr int PROJ_CN = 512;  // output columns per workgroup (64 rows x 512 cols)
+
+__global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
+                                                          const unsigned short* __restrict__ A, int lda,
+                                                          const unsigned short* __restrict__ B, int ldb,
+                                                          const float* __restrict__ b1,
+                                                          const float* __restrict__ b2,
+                                                          float* __restrict__ C, int ldc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rr = lane & 15, kq = lane >> 4;
+  const int row = blockIdx.x * 64 + wave * 16 + rr;
+  const int n0 = blockIdx.y * PROJ_CN;
+  const bool kin = 8 * kq < K;  // K % 8 == 0 (checked on the host)
+  bf16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (kin && row < M) a = *reinterpret_cast<const bf16x8*>(A + (size_t)row * lda + 8 * kq);
+#pragma unroll 8
+  for (int j = 0; j < PROJ_CN / 16; ++j) {
+    const int cb = n0 + 16 * j;
+    if (cb >= N) break;  // N % 16 == 0: whole blocks only
+    bf16x8 b = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (kin) b = *reinterpret_cast<const bf16x8*>(B + (size_t)(cb + rr) * ldb + 8 * kq);
+    // operands swapped: lane holds C[row][cb + 4 kq + r], r = 0..3
+    const f32x4 acc = mfma16(b, a, f32x4{0.f, 0.f, 0.f, 0.f});
+    const int col = cb + 4 * kq;
+    f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+    if (b1) bias += *reinterpret_cast<const f32x4*>(b1 + col);
+    if (b2) bias += *reinterpret_cast<const f32x4*>(b2 + col);
+    if (row < M) *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + col) = acc + bias;
+  }
+}
+
 int tn_splits(int M, int K) {
   const int mb = (M + 63) / 64;
   int s = (512 + mb - 1) / mb;
@@ -243,6 +279,24 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
     case 3: skinny_nt_kernel<3><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
     default: skinny_nt_kernel<4><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
   }
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_skinny_proj(int M, int N, int K, const void* A, int lda, const void* B,
+                                 int ldb, const float* bias1, const float* bias2, float* C, int ldc,
+                                 void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (!A || !B || !C || K < 8 || K > 32 || K % 8 || N % 16 || lda % 8 || ldb % 8 || ldc % 4 ||
+      ((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16) ||
+      ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16)) {
+    mlvae_set_error("mlvae_skinny_proj: K in {8,16,24,32}, N %% 16, aligned 16-byte rows");
+    return 1;
+  }
+  dim3 grid((M + 63) / 64, (N + PROJ_CN - 1) / PROJ_CN);
+  skinny_proj_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(
+      M, N, K, static_cast<const unsigned short*>(A), lda, static_cast<const unsigned short*>(B),
+      ldb, bias1, bias2, C, ldc);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

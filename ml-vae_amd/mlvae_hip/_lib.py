@@ -43,6 +43,7 @@ _SIGS = {
     "mlvae_heads_supported": [I, I, I],
     "mlvae_heads_fused": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
                           P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "mlvae_skinny_proj": [I, I, I, P, I, P, I, P, P, P, I, P],
     "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],
     "mlvae_skinny_tn_workspace_size": [I, I, I],
     "mlvae_skinny_tn": [I, I, I, P, I, P, I, I, P, P, P, P, SZ, P],

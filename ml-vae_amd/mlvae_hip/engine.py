@@ -278,6 +278,8 @@ class VAEEngine:
         # overlap a recurrence / those in the step's tail (env overrides for A/B sweeps)
         self.split_overlap = int(os.environ.get("MLVAE_SPLIT_OVERLAP", "128"))
         self.split_tail = int(os.environ.get("MLVAE_SPLIT_TAIL", "256"))
+        # layer-0 input projection (K = latent width) on skinny_proj instead of the 256² GEMM
+        self.skinny_proj = os.environ.get("MLVAE_PROJ0", "skinny") == "skinny"
         self.side_stream = torch.cuda.Stream(self.device)
         # the step's critical path (recurrences, dgrads) runs on a high-priority stream so the
         # dispatcher prefers its workgroups over the side stream's weight-gradient GEMMs
@@ -535,7 +537,14 @@ class VAEEngine:
         w.layer_in = []
         for li in range(cfg.L):
             w.layer_in.append((xin, xin_bf, din, ldx))
-            if w.bf and din % 8 == 0:  # input projection on the 256² GEMM
+            if w.bf and din <= 32 and din % 8 == 0 and self.skinny_proj:
+                # K = latent width: the write-bound skinny projection kernel (skinny.hip)
+                check(l.mlvae_skinny_proj(N, 8 * H, din, _pb(xin_bf), ldx,
+                                          wb(f"decoder.rnn.weight_ih_l{li}"), din,
+                                          self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                                          self._ptr(f"decoder.rnn.bias_hh_l{li}"), _p(w.G[li]), 8 * H,
+                                          s), "skinny_proj")
+            elif w.bf and din % 8 == 0:  # input projection on the 256² GEMM
                 self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), ldx, wb(f"decoder.rnn.weight_ih_l{li}"),
                            din, _p(w.G[li]), 8 * H, bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
                            bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))

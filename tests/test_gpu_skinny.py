@@ -57,3 +57,25 @@ def test_skinny_tn(M, K, nw, NB, bias):
     else:
         assert torch.isnan(b1).all()                   # no bias output requested: untouched
     assert torch.equal(outs[0][0], outs[1][0])         # fixed-order reduce: bit-identical reruns
+
+
+@pytest.mark.parametrize("M,N,K,lda", [(16000, 4096, 32, 48), (1000, 4096, 16, 32), (77, 48, 24, 24)])
+def test_skinny_proj_matches_fp32_reference(M, N, K, lda):
+    """Layer-0 input projection z W_ih^T + b_ih + b_hh (K = latent width, A rows strided like
+    the engine's [z | 1 | 0..] operand) against a torch fp32 product of the same bf16 values."""
+    need_gpu()
+    l = lib()
+    g = torch.Generator().manual_seed(21)
+    A = torch.randn(M, lda, generator=g).to(torch.bfloat16)
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16)
+    b1, b2 = torch.randn(N, generator=g), torch.randn(N, generator=g)
+    ref = A[:, :K].float() @ B.float().t() + b1 + b2
+    Ad, Bd, C = A.cuda(), B.cuda(), torch.empty(M, N, device="cuda")
+    b1d, b2d = b1.cuda(), b2.cuda()  # held: a freed temporary's block would be reused
+    check(l.mlvae_skinny_proj(M, N, K, Ad.data_ptr(), lda, Bd.data_ptr(), K, P(b1d), P(b2d), P(C),
+                              N, stream()))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 1e-5
+    # bad shapes are refused, not launched
+    assert l.mlvae_skinny_proj(M, N, 40, Ad.data_ptr(), lda, Bd.data_ptr(), 40, None, None, P(C),
+                               N, stream()) != 0
