@@ -217,26 +217,43 @@ __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
                                                           const float* __restrict__ b1,
                                                           const float* __restrict__ b2,
                                                           float* __restrict__ C, int ldc) {
+  constexpr int LS = 64 + 4;  // staging row stride (floats)
+  __shared__ __attribute__((aligned(16))) float stg[4][16 * LS];  // per wave: 16 rows x 64 cols
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rr = lane & 15, kq = lane >> 4;
-  const int row = blockIdx.x * 64 + wave * 16 + rr;
+  const int r0 = blockIdx.x * 64 + wave * 16;
   const int n0 = blockIdx.y * PROJ_CN;
   const bool kin = 8 * kq < K;  // K % 8 == 0 (checked on the host)
   bf16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (kin && row < M) a = *reinterpret_cast<const bf16x8*>(A + (size_t)row * lda + 8 * kq);
-#pragma unroll 8
-  for (int j = 0; j < PROJ_CN / 16; ++j) {
-    const int cb = n0 + 16 * j;
-    if (cb >= N) break;  // N % 16 == 0: whole blocks only
-    bf16x8 b = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (kin) b = *reinterpret_cast<const bf16x8*>(B + (size_t)(cb + rr) * ldb + 8 * kq);
-    // operands swapped: lane holds C[row][cb + 4 kq + r], r = 0..3
-    const f32x4 acc = mfma16(b, a, f32x4{0.f, 0.f, 0.f, 0.f});
-    const int col = cb + 4 * kq;
-    f32x4 bias = {0.f, 0.f, 0.f, 0.f};
-    if (b1) bias += *reinterpret_cast<const f32x4*>(b1 + col);
-    if (b2) bias += *reinterpret_cast<const f32x4*>(b2 + col);
-    if (row < M) *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + col) = acc + bias;
+  if (kin && r0 + rr < M) a = *reinterpret_cast<const bf16x8*>(A + (size_t)(r0 + rr) * lda + 8 * kq);
+  float* sw = stg[wave];
+  for (int c0 = n0; c0 < n0 + PROJ_CN && c0 < N; c0 += 64) {  // N % 16 == 0; 64-column chunks
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+      const int cb = c0 + 16 * jb;
+      if (cb < N) {
+        bf16x8 b = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (kin) b = *reinterpret_cast<const bf16x8*>(B + (size_t)(cb + rr) * ldb + 8 * kq);
+        // operands swapped: lane holds C[r0 + rr][cb + 4 kq + r], r = 0..3
+        const f32x4 acc = mfma16(b, a, f32x4{0.f, 0.f, 0.f, 0.f});
+        *reinterpret_cast<f32x4*>(sw + rr * LS + 16 * jb + 4 * kq) = acc;
+      }
+    }
+    __syncthreads();
+    // read back row-contiguous: one store instruction = 4 rows x 256 contiguous bytes
+    const int col = c0 + 4 * (lane & 15);
+    if (col < N) {
+      f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+      if (b1) bias += *reinterpret_cast<const f32x4*>(b1 + col);
+      if (b2) bias += *reinterpret_cast<const f32x4*>(b2 + col);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 4 * q + (lane >> 4);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(sw + r * LS + 4 * (lane & 15));
+        if (r0 + r < M) *reinterpret_cast<f32x4*>(C + (size_t)(r0 + r) * ldc + col) = v + bias;
+      }
+    }
+    __syncthreads();  // the staging tile is rewritten by the next chunk
   }
 }
 

@@ -272,3 +272,26 @@ def test_dropout_mask_statistics_and_fused_backward():
                                ws.numel() * 4, stream()))
     torch.cuda.synchronize()
     assert torch.equal(C0, C1)
+
+
+def test_dropout_vector_and_scalar_paths_agree():
+    """mlvae_dropout_ex's 16-byte path (aligned) and its element path (unaligned views) give the
+    same masked values, fp32 and bf16, for a length that is not a multiple of 4."""
+    need_gpu()
+    l = lib()
+    n, seed, p = 100_003, 4242, 0.15
+    x = torch.randn(n + 1, device="cuda")
+    outs = []
+    for off in (0, 1):  # element offset 1 = 4-byte misaligned pointers: element path
+        y = torch.zeros(n + 1, device="cuda")
+        yb = torch.zeros(n + 1, device="cuda", dtype=torch.bfloat16)
+        xs = x.clone()
+        if off:
+            xs[1:] = x[:n]
+        check(l.mlvae_dropout_ex(n, P(xs, off), P(y, off), yb.data_ptr() + 2 * off, None, seed, p,
+                                 stream()))
+        torch.cuda.synchronize()
+        outs.append((y[off:off + n].cpu(), yb[off:off + n].view(torch.int16).cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    kept = (outs[0][0] != 0).float().mean().item()
+    assert abs(kept - (1 - p)) < 0.01
