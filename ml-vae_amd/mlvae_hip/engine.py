@@ -431,19 +431,39 @@ class VAEEngine:
         check(lib().mlvae_colsum(N, Cn, src, ld, out, out2, 0.0, _p(ws), w.gws_bytes,
                                  self._stream()), "mlvae_colsum")
 
-    def _side(self, fn):
-        """Run fn's launches on the side stream once everything queued so far on the main
-        stream is done (weight gradients overlap the next BPTT recurrence)."""
+    def _side(self, fn, ev=None):
+        """Run fn's launches on the side stream once everything queued on the main stream up
+        to event ev (default: now) is done (weight gradients overlap the next BPTT)."""
         if not self.overlap:
             return fn()
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+        if ev is None:
+            ev = self._mark()
         self.side_stream.wait_event(ev)
         self._on_side = True
         try:
             fn()
         finally:
             self._on_side = False
+
+    def _mark(self):
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def _defer_side(self, pending, fn):
+        """Queue fn for the side stream behind the main stream's current position, but issue
+        its launches only at the next _flush_side, so the critical-path launch is enqueued
+        first.  (Measured neutral at c2, where the host enqueues a whole step in 0.38 ms of
+        the GPU's 5.8 -- tools/host_rate.py -- and runs far ahead; it matters only when the
+        host falls behind.)"""
+        if not self.overlap:
+            return fn()
+        pending.append((fn, self._mark()))
+
+    def _flush_side(self, pending):
+        for fn, ev in pending:
+            self._side(fn, ev)
+        pending.clear()
 
     def _timed(self, name):
         """HIP events around one launch on the main stream (bench.py's roofline timing)."""
@@ -650,6 +670,8 @@ class VAEEngine:
         # ---- heads tail: dgrad chain on the main stream (already done inside the fused heads
         # kernel when it ran), wgrads on the side stream
         fused = getattr(w, "heads_fused", False)
+        pending = []  # side-stream work issued right after the next critical-path launch
+        side = (lambda fn: self._defer_side(pending, fn)) if fused else self._side
         heads = [("mean_fc", w.P2m, w.dMUX, w.dP2m, 0)]
         if not mse:
             heads.append(("log_var_fc", w.P2v, w.dLVX, w.dP2v, C))
@@ -660,7 +682,7 @@ class VAEEngine:
             def wg3(hd=hd, dOut=dOut, P2=P2):
                 self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
                 self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
-            self._side(wg3)
+            side(wg3)
             if not fused:
                 self._mm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C,
                          B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
@@ -669,7 +691,7 @@ class VAEEngine:
                 self._mm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
                          gp(f"decoder.{hd}.blocks.2.weight"), C)
                 self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
-            self._side(wg2)
+            side(wg2)
             if not fused:
                 self._mm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C,
                          B_bf=wb(f"decoder.{hd}.blocks.2.weight"), epi=EPI_DLRELU,
@@ -682,7 +704,7 @@ class VAEEngine:
             self._mm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
                      gp("decoder.mean_fc.blocks.0.weight"), 2 * H, B_bf=R_bf)
             self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
-        self._side(wg1)
+        side(wg1)
         if not fused:
             self._mm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
                      2 * H, _p(w.dY[cfg.L - 1]), 2 * H, B_bf=wb("decoder.mean_fc.blocks.0.weight"))
@@ -696,6 +718,7 @@ class VAEEngine:
                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
                                           _p(w.Cs[li]), _p(w.dY[li]), _pb(dGb) if dGb is not None else None,
                                           _p(w.xbuf), w.xbuf.numel(), _p(w.err), s), "lstm_bwd")
+            self._flush_side(pending)
             # dG: fp32 in G (fp32 mode) or bf16 in dGb (bf16 mode)
             dG, dG_bf = (None, dGb) if dGb is not None else (Gl, None)
             pg = lambda t, off=0: None if t is None else _p(t, off)
@@ -753,7 +776,7 @@ class VAEEngine:
             # this GEMM).  Below the bottom layer nothing waits on the dgrad: its weight
             # gradients, the step's longest tail, go first.
             if li == 0:
-                self._side(wgl)
+                self._defer_side(pending, wgl)
             dx = w.dZs if li == 0 else w.dY[li - 1]
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
             seed, mask_ptr = w._drop_seed[li - 1] if drop else (None, None)
@@ -761,6 +784,7 @@ class VAEEngine:
                 # dZ = dG W_ih_l0: [N, 8H] x [8H, Z] on the skinny NT kernel
                 check(l.mlvae_skinny_nt(N, Z, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[0]), 8 * H,
                                         _p(w.dZs), Z, s), "skinny_nt")
+                self._flush_side(pending)
                 fused = False
             elif dG_bf is not None and li in self.wih_t and din >= 256:
                 # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy
@@ -775,9 +799,11 @@ class VAEEngine:
             if drop and not fused:
                 check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
                       "dropout_bwd")
+            self._flush_side(pending)  # li == 0 without the fused encoder
             if li > 0:
-                self._side(wgl)
+                self._defer_side(pending, wgl)  # issued right after the next BPTT launch
             if li == cfg.L - 1 and self.world > 1 and self.bucket_allreduce:
+                self._flush_side(pending)  # the bucket waits on the side stream: issue it all
                 self._start_suffix_allreduce()
         # ---- encoder
         w_kl, _ = self.loss_weights()
