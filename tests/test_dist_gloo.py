@@ -41,10 +41,19 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _free_port():
+    """A port the OS reports free on 127.0.0.1 (a fixed base can collide with a lingering
+    socket of an earlier run)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def test_two_rank_allreduce_matches_global_masked_mean():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
+    port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
