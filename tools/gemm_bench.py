@@ -12,6 +12,7 @@ from mlvae_hip._lib import check, lib  # noqa: E402
 N, H, D = 16000, 512, 1024
 SHAPES = [  # name, ta, tb, M, Ncols, K
     ("fwd proj  Y=X W^T  ", 0, 1, N, 8 * H, D),
+    ("proj l0   Y=Z W^T  ", 0, 1, N, 8 * H, 32),
     ("dgrad     dX=dG W  ", 0, 0, N, D, 8 * H),
     ("dgrad     dX=dG W^T", 0, 1, N, D, 8 * H),
     ("wgrad ih  dG^T X   ", 1, 0, 8 * H, D, N),
