@@ -119,8 +119,8 @@ def main():
     cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=args.prec)
     eng = VAEEngine(cfg, device=f"cuda:{local}")
     eng.init_default(seed=123456)
-    if os.environ.get("MLVAE_NO_PRIO"):  # A/B switch: critical path on the caller's stream
-        eng.prioritize = False
+    if os.environ.get("MLVAE_PRIO") is not None:  # A/B switch: critical path on a high-priority stream
+        eng.prioritize = os.environ["MLVAE_PRIO"] == "1"
     if world > 1:
         from mlvae_hip import dist as mdist
         mdist.attach(eng, rank=rank, world=world, batch_per_rank=B)
