@@ -1,22 +1,37 @@
 """Benchmark: spectrogram frames/s of the VAE training step (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--prec bf16|fp32] [--config c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--prec bf16|fp32] [--config c3]
 
-N=1 workload = BASELINE.json configs[1]: full ML-VAE enc/dec on 80-d log-mel, T=500, B=32
-per GPU, train mode (dropout 0.15), Adam + clip 5.0 -- one step = one full fit_batch of the
-fused HIP path.  For N>1 (torch.distributed.run) every rank trains its own B=32 shard
-(weak scaling; N=8 is configs[2]: global B=256) and the gradients are all-reduced over RCCL.
+Headline workload (``--config c3``, the default) = the metric's configuration: the full ML-VAE
+(VanillaVAE enc [80,64,64] z=32, BiLSTM 2x512 decoder with dropout 0.15, dec-FC
+[1024,64,64,80]) on 80-d log-mel at T=500 with a GLOBAL batch of 256 utterances, trained data
+parallel over N GPUs (strong scaling: 256/N utterances per GPU; N=1 trains all 256 on one
+MI355X).  One step = one full fit_batch of the fused HIP path: forward, Gaussian-NLL ELBO,
+backward, global-norm clip 5.0, Adam.  The other configs (c1, c2 = configs[1] B=32/GPU, c4) are
+per-GPU workloads (weak scaling) for A/B runs.
+
+Process model: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) every process
+is one rank.  Without it, ``--gpus N`` (N > 1) makes this process a launcher that starts N
+worker processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment)
+before it touches the GPU, waits for them and exits with their worst status.
 
 Rank 0 prints ONE JSON line.  Besides the contract fields it carries
-  roofline      the dominant kernel (the persistent BiLSTM BPTT recurrence), timed with HIP
-                events on its stream during the timed region; algorithmic bytes per launch;
-                traffic from the committed rocprofv3 PMC run (profiles/), or null
-  cpu_baseline  the CPU oracle (oracle/vae_cpu.py, pinned to reference fixtures) timed on
-                this host's cores on a bounded sample of the same workload (rank 0, N=1)
+  roofline          the dominant kernel (the persistent BiLSTM BPTT recurrence): HIP-event time
+                    of its launches on their stream, algorithmic bytes per launch, PMC traffic
+                    from the committed rocprofv3 passes (profiles/pmc_traffic.json) or null, and
+                    its per-step latency against the inter-CU hand-off floor
+  kernels           secondary rooflines: the two big GEMMs against the bf16 MFMA peak, the fused
+                    encoder (+reparameterisation + KL) and decoder-heads (+NLL) kernels against HBM
+  cpu_baseline      the CPU oracle (oracle/vae_cpu.py, pinned to reference fixtures) timed on this
+                    host's cores on a bounded sample of the same model (rank 0, N=1)
+  extra (N=1 only)  c2 (configs[1], B=32, bf16) and the fp32 parity mode on the headline batch
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,18 +39,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ml-vae_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 
 METRIC = "spectrogram frames/sec + ELBO; 80-d log-mel B=256 at 1/2/4/8 MI355X"
+GLOBAL_BATCH = 256
+# name: (F, E, Z, H, L, C, batch, T, batch_is_global)
 CONFIGS = {
-    # name: (F, E, Z, H, L, C, B_per_gpu, T)
-    "c1": (64, 128, 16, 128, 2, 128, 8, 200),
-    "c2": (80, 64, 32, 512, 2, 64, 32, 500),
-    "c4": (80, 64, 32, 512, 2, 64, 64, 2000),
+    "c1": (64, 128, 16, 128, 2, 128, 8, 200, False),
+    "c2": (80, 64, 32, 512, 2, 64, 32, 500, False),
+    "c3": (80, 64, 32, 512, 2, 64, GLOBAL_BATCH, 500, True),
+    "c4": (80, 64, 32, 512, 2, 64, 64, 2000, False),
 }
-TIMER_EVERY = 4          # time the recurrence launches on every 4th timed step
+TIMER_EVERY = 4          # time kernels with HIP events on every 4th timed step
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+HANDOFF_FLOOR_US = 0.8   # MI355X_MICROARCH.md handoff-1to1, idle, 8 B
 
 
 def macs_per_frame(F, E, Z, H, L, C):
@@ -58,10 +76,42 @@ def lstm_launch_flops(B, T, H):
     return 2 * B * T * 2 * 4 * H * H
 
 
-def cpu_baseline(cfg_name, prec, budget_s=12.0):
-    """The CPU oracle (torch CPU, ATen LSTM as the reference calls it) on this host."""
+def encoder_fwd_bytes(N, F, E, Z):
+    """encoder_fwd_kernel: reads x (F fp32); writes E1, E2 (bf16, the backward's operands),
+    [mu | log_var] (2Z fp32), z (Z fp32), z as bf16 [z | 1 | 0..] (Z+16 bf16) and eps (Z fp32)."""
+    return N * (4 * F + 2 * 2 * E + 4 * 2 * Z + 4 * Z + 2 * (Z + 16) + 4 * Z)
+
+
+def encoder_bwd_bytes(N, F, E, Z):
+    """encoder_bwd_kernel: reads dz, [mu | log_var], eps (fp32), E1, E2 (bf16), x (fp32);
+    writes per-block weight-gradient partials (negligible per frame)."""
+    return N * (4 * Z + 4 * 2 * Z + 4 * Z + 2 * 2 * E + 4 * F)
+
+
+def heads_bytes(N, F, C, H):
+    """heads_kernel (train): reads h (2H bf16) and x (F fp32); writes P1 (2C), P2m, P2v (C each),
+    mu_x, log_var_x (F each), d mu_x, d log_var_x (F each), dP2m, dP2v (C each), dP1 (2C) fp32
+    and dY (2H fp32)."""
+    return N * (2 * 2 * H + 4 * F + 4 * (2 * C + 2 * C + 2 * F + 2 * F + 2 * C + 2 * C) + 4 * 2 * H)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg_name, budget_s=12.0):
+    """The CPU oracle (torch CPU, ATen LSTM as the reference calls it) on this host, on a
+    bounded sample: full train steps of the same model and T at B=32 (configs[1])."""
     from oracle import vae_cpu as O
-    F, E, Z, H, L, C, B, T = CONFIGS[cfg_name]
+    F, E, Z, H, L, C, _, T, _ = CONFIGS[cfg_name]
+    B = 32 if cfg_name in ("c2", "c3") else CONFIGS[cfg_name][6]
     threads = os.cpu_count() or 1
     cap = int(os.environ.get("OMP_NUM_THREADS", threads))
     torch.set_num_threads(max(1, min(threads, cap)))
@@ -81,19 +131,165 @@ def cpu_baseline(cfg_name, prec, budget_s=12.0):
         if dt > budget_s or steps >= 20:
             break
     return {"value": steps * B * T / dt, "unit": "frames/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{steps} full {cfg_name} train steps (B={B}, T={T}, fp32, ATen LSTM, clip+Adam) "
-                      f"in {dt:.1f} s on {torch.get_num_threads()} host threads"}
+            "kind": "port", "cpu": cpu_model(),
+            "sample": f"{steps} full train steps of the same model (B={B}, T={T}, fp32, ATen LSTM, "
+                      f"dropout 0.15, clip+Adam) in {dt:.1f} s on {torch.get_num_threads()} host threads"}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_workers(n, argv):
+    """Launcher mode: N worker processes of this script, one per GPU (started before this
+    process touches the GPU; no exec).  Returns the worst exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):  # one rank failed: stop the others
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc]
+    return bad[0] if bad else 0
+
+
+def dry_run(rank, world):
+    """Process-model check without a GPU: gloo group, one all-reduce, rank 0 reports."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.tensor([float(rank + 1)])
+        dist.all_reduce(t)
+        total = t.item()
+        dist.destroy_process_group()
+    else:
+        total = 1.0
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "world": world, "rank_sum": total,
+                          "per_rank_batch": GLOBAL_BATCH // world}))
+
+
+def make_engine(cfg_name, prec, device, world, rank, B):
+    from mlvae_hip.engine import VAEConfig, VAEEngine
+    F, E, Z, H, L, C, _, T, _ = CONFIGS[cfg_name]
+    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=prec)
+    eng = VAEEngine(cfg, device=device)
+    eng.init_default(seed=123456)
+    if world > 1:
+        from mlvae_hip import dist as mdist
+        mdist.attach(eng, rank=rank, world=world, batch_per_rank=B)
+    return eng
+
+
+def global_batch_shard(B, T, F, rank, device):
+    """This rank's utterances of the synthetic global batch (seeded, identical for every N)."""
+    g = torch.Generator(device=device).manual_seed(123456)
+    xg = torch.randn(B * (rank + 1), T, F, device=device, generator=g)  # rows < rank*B discarded
+    return xg[rank * B:].contiguous()
+
+
+def timed_run(eng, x, lens, steps, warmup, world, timers=None):
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(warmup):
+        eng.train_step(x, lens)
+    barrier()
+    eng.check_errors()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(steps):
+        eng.kernel_timers = timers if (timers is not None and i % TIMER_EVERY == 0) else None
+        loss = eng.train_step(x, lens)
+    barrier()
+    dt = time.perf_counter() - t0
+    eng.kernel_timers = None
+    eng.check_errors()
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], device=x.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    return dt, loss
+
+
+def secondary(kern, B, T, cfg_name):
+    """Per-kernel rooflines of the timed secondary launches (HIP events, main stream)."""
+    F, E, Z, H, L, C, _, _, _ = CONFIGS[cfg_name]
+    N = B * T
+    out = {}
+    gemm_flops = 2.0 * N * 8 * H * 2 * H
+    for name, what in (("proj_l1", "layer-1 input projection [N x 2H] x [2H x 8H] (gemm256)"),
+                       ("dgrad_l1", "layer-1 dgrad [N x 8H] x [8H x 2H] + dropout bwd (gemm256)")):
+        if name in kern:
+            tf = gemm_flops / (kern[name] * 1e-3) / 1e12
+            out[name] = {"what": what, "bound": "mfma", "avg_launch_ms": kern[name],
+                         "achieved": tf, "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
+                         "frac": tf / MFMA_PEAK_TFLOPS["bf16"]}
+    for name, nbytes, key in (("encoder_fwd", encoder_fwd_bytes(N, F, E, Z), "encoder_fwd"),
+                              ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), "encoder_bwd"),
+                              ("heads", heads_bytes(N, F, C, H), "heads")):
+        if name in kern:
+            gbs = nbytes / (kern[name] * 1e-3) / 1e9
+            out[name] = {"bound": "hbm", "avg_launch_ms": kern[name], "achieved": gbs,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch": nbytes,
+                         "traffic": pmc_traffic(f"{cfg_name}/{key}")}
+    return out
+
+
+def extra_runs(args, device):
+    """N=1 extras: configs[1] (c2, B=32 bf16) and the fp32 parity mode on the headline batch."""
+    out = {}
+    runs = [("c2_bf16", "c2", "bf16", 10, 2)]
+    if args.prec != "fp32":
+        runs.append((f"{args.config}_fp32", args.config, "fp32", 3, 1))
+    for key, cname, prec, steps, warm in runs:
+        F, E, Z, H, L, C, B, T, _ = CONFIGS[cname]
+        eng = make_engine(cname, prec, device, 1, 0, B)
+        x = global_batch_shard(B, T, F, 0, device)
+        lens = torch.ones(B, device=device)
+        dt, loss = timed_run(eng, x, lens, steps, warm, 1)
+        lv = loss.tolist()
+        out[key] = {"global_batch": B, "seq_len": T, "dtype": prec, "steps": steps,
+                    "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
+                    "loss": lv[2]}
+        del eng, x
+        torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -102,69 +298,51 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--prec", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--config", default="c2", choices=list(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=list(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the N=1 c2 / fp32 extra runs")
+    ap.add_argument("--dry-run", action="store_true", help="process model only (gloo, no GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_workers(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(rank, world)
+
     torch.cuda.set_device(local)
+    device = f"cuda:{local}"
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from mlvae_hip.engine import VAEConfig, VAEEngine
-    F, E, Z, H, L, C, B, T = CONFIGS[args.config]
-    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=args.prec)
-    eng = VAEEngine(cfg, device=f"cuda:{local}")
-    eng.init_default(seed=123456)
-    if os.environ.get("MLVAE_PRIO") is not None:  # A/B switch: critical path on a high-priority stream
-        eng.prioritize = os.environ["MLVAE_PRIO"] == "1"
-    if world > 1:
-        from mlvae_hip import dist as mdist
-        mdist.attach(eng, rank=rank, world=world, batch_per_rank=B)
-    g = torch.Generator(device="cuda").manual_seed(123456 + rank)
-    x = torch.randn(B, T, F, device="cuda", generator=g)   # synthetic normalised log-mel
-    lens = torch.ones(B, device="cuda")
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        eng.train_step(x, lens)
-    barrier()
-    eng.check_errors()
-    # HIP events around the recurrence launches (roofline timing) on one step in TIMER_EVERY:
-    # each timing event costs the stream ~6 us at a dependent boundary (rocprofv3 trace), so
-    # timing every step would charge the throughput ~80 us/step of measurement overhead
+    F, E, Z, H, L, C, batch, T, is_global = CONFIGS[args.config]
+    if is_global:
+        if batch % world:
+            raise SystemExit(f"global batch {batch} does not split over {world} GPUs")
+        B = batch // world
+    else:
+        B = batch
+    eng = make_engine(args.config, args.prec, device, world, rank, B)
+    x = global_batch_shard(B, T, F, rank, device)   # synthetic normalised log-mel
+    lens = torch.ones(B, device=device)
     timers = {}
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        eng.kernel_timers = timers if i % TIMER_EVERY == 0 else None
-        loss = eng.train_step(x, lens)
-    barrier()
-    dt = time.perf_counter() - t0
-    eng.check_errors()
-    eng.kernel_timers = None
-    if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([dt], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = tt.item()
+    dt, loss = timed_run(eng, x, lens, args.steps, args.warmup, world, timers)
     ms = dt / args.steps * 1e3
     value = B * T * world * args.steps / dt
     lv = loss.tolist()
     kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
+    launches = {k: len(v) for k, v in timers.items()}
+    del eng
+    torch.cuda.empty_cache()
     if rank == 0:
         dom = "lstm_bwd"
         dur_s = kern[dom] * 1e-3
         nbytes = lstm_launch_bytes(B, T, H)
         achieved = nbytes / dur_s / 1e9
-        traffic = pmc_traffic(dom)
+        step_us = kern[dom] * 1e3 / T
         out = {
             "metric": METRIC,
             "value": value,
@@ -174,33 +352,43 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if is_global else "weak",
             "vs_baseline": None,
             "dtype": args.prec,
             "data": "synthetic N(0,1) 80-d frames (normalised log-mel stand-in), lens=1, "
                     "random-init weights (PyTorch default init, seed 123456)",
             "config": {"workload": f"{args.config}: VanillaVAE enc [{F},{E},{E}] z={Z}, BiLSTM "
                                    f"{L}x{H} (dropout 0.15), dec-FC [{2 * H},{C},{C},{F}], T={T}, "
-                                   f"B={B}/GPU, Gaussian-NLL ELBO, clip 5.0 + Adam 1e-3",
-                       "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+                                   f"global batch {B * world} = {B}/GPU x {world}, Gaussian-NLL ELBO, "
+                                   f"clip 5.0 + Adam 1e-3",
+                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": T,
+                       "parallelism": f"dp{world}"},
             "elbo": {"kld_loss": lv[0], "recon_loss": lv[1], "loss": lv[2]},
             "train_tflops": value * 6 * macs_per_frame(F, E, Z, H, L, C) / 1e12,
-            "roofline": {"kernel": "lstm_bwd_kernel (persistent BiLSTM BPTT, both directions)",
+            "roofline": {"kernel": "lstm_bwd (persistent BiLSTM BPTT recurrence, both directions, "
+                                   "all batch chunks of one layer)",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(f"{args.config}/lstm_bwd"),
                          "algorithmic_bytes_per_launch": nbytes,
-                         "avg_launch_ms": kern[dom], "launches": len(timers[dom]),
+                         "avg_launch_ms": kern[dom], "launches": launches[dom],
                          "mfma_frac": lstm_launch_flops(B, T, H) / dur_s / 1e12 /
-                         MFMA_PEAK_TFLOPS[args.prec]},
+                         MFMA_PEAK_TFLOPS[args.prec],
+                         "step_latency_us": step_us, "handoff_floor_us": HANDOFF_FLOOR_US,
+                         "latency_frac": HANDOFF_FLOOR_US / step_us},
+            "kernels": secondary(kern, B, T, args.config) if args.prec == "bf16" else {},
             "kernel_ms": kern,
         }
+        if world == 1 and not args.no_extra:
+            out["extra"] = extra_runs(args, device)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.config, args.prec)
+            out["cpu_baseline"] = cpu_baseline(args.config)
         else:
             out["cpu_baseline"] = None
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -1,4 +1,7 @@
-"""EpochCounter: iterable over epochs 1..limit, checkpointable (SpeechBrain semantics)."""
+"""EpochCounter: iterable over epochs 1..limit, checkpointable (SpeechBrain semantics).
+
+Its checkpoint file is SpeechBrain's: the current epoch as plain text; recovering from a
+checkpoint that was not written at the end of an epoch replays that epoch (current - 1)."""
 
 
 class EpochCounter:
@@ -20,3 +23,13 @@ class EpochCounter:
 
     def load_state_dict(self, sd):
         self.current = int(sd["current"])
+
+    # SpeechBrain's saver / recoverer pair for this object (plain-text file)
+    def ckpt_save(self, path):
+        with open(path, "w") as f:
+            f.write(str(self.current))
+
+    def ckpt_recover(self, path, end_of_epoch=True):
+        with open(path) as f:
+            saved = int(f.read().strip())
+        self.current = saved if end_of_epoch else saved - 1

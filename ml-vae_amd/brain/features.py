@@ -4,8 +4,8 @@
 SpeechBrain 0.5 semantics restated (parity unpinned): per-utterance mean/std over the first
 round(len*T) frames, averaged over the batch; in train mode the global statistics are set on
 the first batch and then running-averaged with weight 1/(count+1) while
-epoch < update_until_epoch; x <- (x - mean) / std.  Host-side torch ops (outside the fused
-train step, which takes already normalised features)."""
+epoch < update_until_epoch; x <- (x - mean) / std.  Device-side torch ops with no host
+synchronisation (outside the fused train step, which takes already normalised features)."""
 import torch
 
 
@@ -26,14 +26,18 @@ class InputNormalization(torch.nn.Module):
 
     @torch.no_grad()
     def forward(self, x, lengths, spk_ids=None, epoch=0):
-        means, stds = [], []
-        for b in range(x.shape[0]):
-            n = int(torch.round(lengths[b] * x.shape[1]).item())
-            seg = x[b, :n]
-            means.append(seg.mean(0))
-            stds.append(torch.clamp(seg.std(0), min=self.eps))
-        cur_mean = torch.stack(means).mean(0)
-        cur_std = torch.stack(stds).mean(0)
+        # per-utterance statistics over the first round(len*T) frames, as one masked device
+        # reduction (no per-utterance host sync); std is the unbiased torch.std
+        B, T = x.shape[0], x.shape[1]
+        n = torch.round(lengths.to(x.device, torch.float32) * T)
+        mask = (torch.arange(T, device=x.device, dtype=torch.float32).unsqueeze(0) < n.unsqueeze(1))
+        mask = mask.to(x.dtype).reshape(B, T, *([1] * (x.dim() - 2)))
+        nb = n.to(x.dtype).reshape(B, *([1] * (x.dim() - 2)))
+        means = (x * mask).sum(1) / nb
+        var = (((x - means.unsqueeze(1)) * mask) ** 2).sum(1) / (nb - 1)
+        stds = torch.clamp(var.sqrt(), min=self.eps)
+        cur_mean = means.mean(0)
+        cur_std = stds.mean(0)
         if self.training:
             if self.count == 0:
                 self.glob_mean, self.glob_std = cur_mean, cur_std

@@ -1,0 +1,111 @@
+// Shared pieces of the persistent LSTM recurrences (lstm.hip: the batch-group kernels;
+// lstm_wide.hip: the wide-batch kernels): launch arguments, the tagged-granule hand-off
+// (MI355X_MICROARCH.md "Valid forms" R2) and diagnostics stamps.
+#pragma once
+#include "common.h"
+#include <type_traits>
+
+namespace {
+
+constexpr int BG = 16;             // utterances per batch group (= MFMA N/M tile)
+constexpr int NSLOT = 4;           // exchange slots (step mod 4)
+constexpr unsigned SPIN_LIMIT = 1u << 20;
+constexpr int MIN_LDS = 82 * 1024; // > half of 160 KiB: one workgroup per CU (residency)
+
+struct LstmArgs {
+  int B, T, H;        // B = utterances handled by this launch (<= NB*16)
+  int NB, NJ, HJ;     // batch groups, hidden slices per group, hidden units per slice
+  int Kp;             // H padded (pow2 >= 128): fwd exchange row stride / MFMA K
+  int K4p;            // 4H padded (pow2 >= 128): bwd exchange row stride / MFMA K
+  const float* W0;    // W_hh forward dir  [4H, H]
+  const float* W1;    // W_hh reverse dir  [4H, H]
+  float* G;           // [B*T, 8H] fwd: in x-proj(+biases) out activated gates; bwd: in gates, out dG
+  float* Cs;          // [B*T, 2H] cell states (fwd writes, bwd reads)
+  float* Y;           // [B*T, 2H] fwd: out h; bwd: in dY (grad wrt layer output)
+  void* xbuf;         // exchange buffer [2 dirs][NB][NSLOT][16][Kp or K4p]
+  int* err;
+  unsigned long long* dbg;  // optional per-step phase stamps of workgroup 0 (diagnostics)
+  int dbg_mode;             // diagnostics: bit0 = skip saved-activation stores (timing only)
+  int xcd_local;            // group g = blocks b with b % 8 == g (one XCD each, when the
+                            // dispatcher deals round-robin); others exit at once
+  unsigned* xtab;           // [ngroups][NJ] XCC id + 1 of every member (zeroed per launch)
+  unsigned short* Yb;       // optional bf16 copy of h [B*T, 2H] (fwd; GEMM operand)
+  unsigned short* dGb;      // optional: bwd writes dG as bf16 [B*T, 8H] here instead of into G
+};
+
+// XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
+__device__ __forceinline__ unsigned xcc_id() {
+  return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;
+}
+
+// One-time placement check of an XCD-local group: every member publishes its XCC id, then
+// reads all members' ids.  Returns true (uniformly across the group: all read the same
+// table) iff the whole group runs on one XCD -- then hand-off stores may be plain (the line
+// stays in that XCD's L2, which every member's sc1 loads read); otherwise they stay
+// write-through sc1, which is correct at any placement.  Bounded spin; false on timeout.
+__device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratch) {
+  const int tid = threadIdx.x;
+  const unsigned mine = xcc_id() + 1;
+  if (tid == 0) { *scratch = 0; st_flag(tab + me, mine); }
+  __syncthreads();
+  if (tid < members) {
+    unsigned v = 0, spins = 0;
+    while ((v = ld_flag(tab + tid)) == 0 && ++spins < (1u << 16)) __builtin_amdgcn_s_sleep(2);
+    if (v != mine) atomicOr(scratch, 1);
+  }
+  __syncthreads();
+  return *scratch == 0;
+}
+
+// Phase stamps (s_memtime) of workgroup 0, thread 0: dbg[s*16 + phase]
+#define STAMP(ph)                                                              \
+  do {                                                                         \
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                          \
+      a.dbg[(size_t)s * 16 + (ph)] = __builtin_amdgcn_s_memtime();             \
+  } while (0)
+// per-wave stamp (lane 0 of every wave of workgroup 0): dbg[s*16 + slot + wave]
+#define WSTAMP(slot)                                                           \
+  do {                                                                         \
+    if (a.dbg && blockIdx.x == 0 && (threadIdx.x & 63) == 0)                   \
+      a.dbg[(size_t)s * 16 + (slot) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+template <int PREC> struct Elt;
+template <> struct Elt<PREC_F32> { typedef float T; static constexpr int GE = 2; };   // per granule
+template <> struct Elt<PREC_BF16> { typedef short T; static constexpr int GE = 4; };
+
+__device__ __forceinline__ unsigned step_tag(int s) { return (unsigned)(((s >> 2) + 1) & 1); }
+
+// Granule packing: value 0 carries the tag in its least significant bit.
+__device__ __forceinline__ unsigned long long pack_bf16(float v0, float v1, float v2, float v3,
+                                                        unsigned tag) {
+  const unsigned e0 = ((unsigned)(unsigned short)f2bf(v0) & ~1u) | tag;
+  const unsigned lo = e0 | ((unsigned)(unsigned short)f2bf(v1) << 16);
+  const unsigned hi = (unsigned)(unsigned short)f2bf(v2) | ((unsigned)(unsigned short)f2bf(v3) << 16);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long pack_f32(float v0, float v1, unsigned tag) {
+  const unsigned e0 = (__float_as_uint(v0) & ~1u) | tag;
+  return ((unsigned long long)__float_as_uint(v1) << 32) | e0;
+}
+// one 8-byte write-through store per granule (buffer_store_dwordx2 ... sc1)
+__device__ __forceinline__ void st_granule(__amdgpu_buffer_rsrc_t r, unsigned byte_off,
+                                           unsigned long long v) {
+  u32x2 w = {(unsigned)v, (unsigned)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, byte_off, 0, 16 /*sc1*/);
+}
+// a 16-byte load holds two granules; their tags sit in dwords 0 and 2
+__device__ __forceinline__ bool tags_ok(u32x4 v, unsigned tag, bool g0, bool g1) {
+  return (!g0 || (v[0] & 1u) == tag) && (!g1 || (v[2] & 1u) == tag);
+}
+
+}  // namespace
+
+// Wide-batch recurrences (lstm_wide.hip): one launch covers every utterance of a layer when
+// the batch-group kernels would need several chunks.  Return -1 when the shape is not
+// supported (the caller then falls back to chunked batch-group launches), else a status.
+int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
+                  float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
+                  unsigned short* yb, unsigned short* dgb, unsigned long long* dbg, int dbg_mode);
+// exchange bytes the wide kernels need at (B, H), or 0 when they do not apply
+size_t lstm_wide_xbytes(int B, int H, bool fwd);

@@ -2,6 +2,7 @@
 
     python -m mlvae_hip.build          (from ml-vae_amd/)
 """
+import glob
 import os
 import subprocess
 import sys
@@ -12,7 +13,7 @@ PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(HERE, "libmlvae.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["capi.cpp", "gemm.hip", "gemm_bf16.hip", "gemm_fast.hip", "heads.hip", "skinny.hip", "encoder.hip", "lstm.hip", "elbo.hip", "gmm.hip", "optim.hip"]
+SOURCES = ["capi.cpp", "gemm.hip", "gemm_bf16.hip", "gemm_fast.hip", "heads.hip", "skinny.hip", "encoder.hip", "lstm.hip", "lstm_wide.hip", "elbo.hip", "gmm.hip", "optim.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
          "-I" + CSRC]
 
@@ -25,7 +26,7 @@ def _stale(src):
     o = _obj(src)
     if not os.path.exists(o):
         return True
-    deps = [os.path.join(CSRC, src), os.path.join(CSRC, "common.h")]
+    deps = [os.path.join(CSRC, src)] + glob.glob(os.path.join(CSRC, "*.h"))
     return any(os.path.getmtime(d) > os.path.getmtime(o) for d in deps)
 
 

@@ -133,67 +133,104 @@ class ParamLayout:
         return n
 
 
-class _Work:
-    """Activation/gradient workspaces for one (B, T): allocated once, reused every step."""
+class _Pool:
+    """Named device buffers that only grow: a _Work for a new (B, T) takes views of them, so a
+    recipe whose padded length changes every batch reuses one allocation (sized by the largest
+    B*T seen, grown by >= 25 % at a time) instead of reallocating ~GBs per batch."""
 
-    def __init__(self, cfg, B, T, device, enc_fused=False):
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+
+    def __call__(self, name, shape, dtype=torch.float32):
+        if isinstance(shape, int):
+            shape = (shape,)
+        n = 1
+        for d in shape:
+            n *= int(d)
+        key = (name, dtype)
+        cur = self.bufs.get(key)
+        if cur is None or cur.numel() < n:
+            cap = n if cur is None else max(n, cur.numel() * 5 // 4)
+            cur = torch.empty(max(cap, 1), device=self.device, dtype=dtype)
+            self.bufs[key] = cur
+        return cur[:n].view(shape)
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in self.bufs.values())
+
+
+class _Work:
+    """Activation/gradient workspaces for one (B, T): views of the engine's growing pool."""
+
+    def __init__(self, cfg, B, T, device, enc_fused=False, pool=None):
         N = B * T
         F, E, Z, H, L, C = cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C
-        f = dict(device=device, dtype=torch.float32)
+        pool = pool or _Pool(device)
         self.B, self.T, self.N = B, T, N
-        self.E1 = torch.empty(N, E, **f)
-        self.E2 = torch.empty(N, E, **f)
-        self.ML = torch.empty(N, 2 * Z, **f)
-        self.Zs = torch.empty(N, Z, **f)
-        self.eps = torch.empty(N, Z, **f)
-        self.G = [torch.empty(N, 8 * H, **f) for _ in range(L)]
-        self.Cs = [torch.empty(N, 2 * H, **f) for _ in range(L)]
-        self.Y = [torch.empty(N, 2 * H, **f) for _ in range(L)]
-        self.Yd = [torch.empty(N, 2 * H, **f) if cfg.dropout > 0 else None for _ in range(L - 1)]
+
+        class _Alloc:  # torch.empty-like front end of the pool: every buffer gets its own name
+            def __init__(self):
+                self.i = 0
+
+            def __call__(self, *shape, dtype=torch.float32, **_):
+                self.i += 1
+                return pool(f"w{self.i}", shape, dtype)
+        empty = _Alloc()
+        f = dict(dtype=torch.float32)
+        self.E1 = empty(N, E, **f)
+        self.E2 = empty(N, E, **f)
+        self.ML = empty(N, 2 * Z, **f)
+        self.Zs = empty(N, Z, **f)
+        self.eps = empty(N, Z, **f)
+        self.G = [empty(N, 8 * H, **f) for _ in range(L)]
+        self.Cs = [empty(N, 2 * H, **f) for _ in range(L)]
+        self.Y = [empty(N, 2 * H, **f) for _ in range(L)]
+        self.Yd = [empty(N, 2 * H, **f) if cfg.dropout > 0 else None for _ in range(L - 1)]
         # bf16 mode: bf16 copies of the big GEMM operands (h, dropout output, dG)
         self.bf = cfg.prec == "bf16"
-        b16 = dict(device=device, dtype=torch.bfloat16)
-        self.Yb = [torch.empty(N, 2 * H, **b16) for _ in range(L)] if self.bf else None
-        self.Ydb = ([torch.empty(N, 2 * H, **b16) if cfg.dropout > 0 else None for _ in range(L - 1)]
+        b16 = dict(dtype=torch.bfloat16)
+        self.Yb = [empty(N, 2 * H, **b16) for _ in range(L)] if self.bf else None
+        self.Ydb = ([empty(N, 2 * H, **b16) if cfg.dropout > 0 else None for _ in range(L - 1)]
                     if self.bf else None)
-        self.dGb = [torch.empty(N, 8 * H, **b16) for _ in range(L)] if self.bf else None
+        self.dGb = [empty(N, 8 * H, **b16) for _ in range(L)] if self.bf else None
         # fused encoder (encoder.hip): z as bf16 [N, Z + 16] = [z | 1 | 0 ...], the ones column
         # feeding the bottom layer's bias gradient (skinny.hip); bf16 hidden activations
         self.enc_fused = self.bf and enc_fused
         self.ZA = Z + 16 if self.enc_fused else Z
-        self.Zb = torch.empty(N, self.ZA, **b16) if self.bf else None  # first layer's GEMM operand
-        self.E1b = torch.empty(N, E, **b16) if self.enc_fused else None
-        self.E2b = torch.empty(N, E, **b16) if self.enc_fused else None
+        self.Zb = empty(N, self.ZA, **b16) if self.bf else None  # first layer's GEMM operand
+        self.E1b = empty(N, E, **b16) if self.enc_fused else None
+        self.E2b = empty(N, E, **b16) if self.enc_fused else None
         if self.bf:
             self.Yd = [None] * (L - 1)  # the dropout output exists as bf16 only
-        self.P1 = torch.empty(N, 2 * C, **f)
-        self.P2m = torch.empty(N, C, **f)
-        self.P2v = torch.empty(N, C, **f)
-        self.MUX = torch.empty(N, F, **f)
-        self.LVX = torch.empty(N, F, **f)
+        self.P1 = empty(N, 2 * C, **f)
+        self.P2m = empty(N, C, **f)
+        self.P2v = empty(N, C, **f)
+        self.MUX = empty(N, F, **f)
+        self.LVX = empty(N, F, **f)
         # backward
-        self.dMUX = torch.empty(N, F, **f)
-        self.dLVX = torch.empty(N, F, **f)
-        self.dP2m = torch.empty(N, C, **f)
-        self.dP2v = torch.empty(N, C, **f)
-        self.dP1 = torch.empty(N, 2 * C, **f)
-        self.dY = [torch.empty(N, 2 * H, **f) for _ in range(L)]
-        self.dZs = torch.empty(N, Z, **f)
-        self.dML = torch.empty(N, 2 * Z, **f)
-        self.dE2 = torch.empty(N, E, **f)
-        self.dE1 = torch.empty(N, E, **f)
+        self.dMUX = empty(N, F, **f)
+        self.dLVX = empty(N, F, **f)
+        self.dP2m = empty(N, C, **f)
+        self.dP2v = empty(N, C, **f)
+        self.dP1 = empty(N, 2 * C, **f)
+        self.dY = [empty(N, 2 * H, **f) for _ in range(L)]
+        self.dZs = empty(N, Z, **f)
+        self.dML = empty(N, 2 * Z, **f)
+        self.dE2 = empty(N, E, **f)
+        self.dE1 = empty(N, E, **f)
         l = lib()
         self.nk = l.mlvae_elbo_partials_count(B, T, Z)
         self.nr = l.mlvae_elbo_partials_count(B, T, F)
-        self.pk = torch.empty(self.nk, **f)
-        self.pr = torch.empty(self.nr, **f)
+        self.pk = empty(self.nk, **f)
+        self.pr = empty(self.nr, **f)
         self.nh = l.mlvae_heads_partials_count(B, T)
-        self.ph = torch.empty(self.nh, **f)   # fused heads' recon partials
+        self.ph = empty(self.nh, **f)   # fused heads' recon partials
         self.nke = l.mlvae_encoder_partials_count(B, T) if self.enc_fused else 0
-        self.pke = torch.empty(max(self.nke, 1), **f)  # fused encoder's KL partials
+        self.pke = empty(max(self.nke, 1), **f)  # fused encoder's KL partials
         ewb = l.mlvae_encoder_workspace_size(B, T, F, E, Z) if self.enc_fused else 0
-        self.enc_ws = torch.empty(ewb // 4 + 1, **f)
-        self.loss = torch.zeros(3, **f)   # [kld_loss, recon_loss, total]
+        self.enc_ws = empty(ewb // 4 + 1, **f)
+        self.loss = torch.zeros(3, device=device, dtype=torch.float32)  # own tensor: returned to the caller   # [kld_loss, recon_loss, total]
         self.count = torch.zeros(1, device=device, dtype=torch.int32)
         # GEMM split-K workspace: the largest any call of the step asks for
         shapes = [(N, E, F), (N, E, E), (N, 2 * Z, E), (N, 2 * C, 2 * H), (N, C, C), (N, F, C),
@@ -209,13 +246,12 @@ class _Work:
         if self.enc_fused:
             ws = max(ws, l.mlvae_skinny_tn_workspace_size(8 * H, self.ZA, N))
         cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
-        self.gws = torch.empty(max(ws, cs, 16) // 4 + 1, **f)
-        self.gws_side = torch.empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
+        self.gws = empty(max(ws, cs, 16) // 4 + 1, **f)
+        self.gws_side = empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
         self.gws_bytes = self.gws.numel() * 4
         xb = _lib.SZ()
         check(l.mlvae_lstm_workspace_size(B, H, PREC[cfg.prec], _lib.C.byref(xb)), "lstm_workspace_size")
-        self.xbuf = torch.empty(max(xb.value, 16), device=device, dtype=torch.uint8)
-        self.err = torch.zeros(1, device=device, dtype=torch.int32)
+        self.xbuf = empty(max(xb.value, 16), dtype=torch.uint8)
 
 
 def _aligned(ptr, ld, bf):
@@ -251,6 +287,10 @@ class VAEEngine:
         self.nonfinite_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
         self.grad_norm = torch.zeros(1, **f)
         self.hyp = torch.zeros(4, **f)
+        # spin-timeout word of the persistent recurrences (set on a hand-off timeout; the
+        # launch then completes with undefined outputs): checked by check_errors()
+        self.err = torch.zeros(1, device=self.device, dtype=torch.int32)
+        self._nonfinite_seen = 0   # nonfinite_ctr value at the last check_health()
         # bf16 mode: bf16 copy of the weights, refreshed at the start of every forward
         self.flat_bf = torch.empty(n, device=self.device, dtype=torch.bfloat16) if cfg.prec == "bf16" else None
         # bf16 mode: k-contiguous W_ih^T [din, 8H] of the layers whose dgrad runs on the 256² GEMM
@@ -273,6 +313,7 @@ class VAEEngine:
         self.seed = seed
         self.rng_step = 0
         self._work = {}
+        self._pool = _Pool(self.device)
         self.overlap = True         # weight-gradient GEMMs on a side stream
         # split-K workgroup targets of the weight-gradient GEMMs (mlvae_gemm_bf16): those that
         # overlap a recurrence / those in the step's tail (env overrides for A/B sweeps)
@@ -371,8 +412,8 @@ class VAEEngine:
     def work(self, B, T):
         key = (B, T)
         if key not in self._work:
-            self._work = {key: _Work(self.cfg, B, T, self.device,  # keep one shape resident
-                                     enc_fused=self.fused_encoder)}
+            self._work = {key: _Work(self.cfg, B, T, self.device,  # views of the growing pool
+                                     enc_fused=self.fused_encoder, pool=self._pool)}
         return self._work[key]
 
     # ------------------------------------------------------------------ launch helpers
@@ -526,12 +567,13 @@ class VAEEngine:
             # ---- encoder + reparameterisation noise + z + KL partial sums, one launch
             # (encoder.hip; ref:src/modules/vanilla_vae.py:21-45)
             ep = lambda n: self._ptr(f"encoder.{n}")
-            check(l.mlvae_encoder_fwd(B, T, Fd, E, Z, X, ep("fc.0.blocks.0.weight"), ep("fc.0.blocks.0.bias"),
-                                      ep("fc.0.blocks.2.weight"), ep("fc.0.blocks.2.bias"),
-                                      ep("mean_fc.weight"), ep("mean_fc.bias"),
-                                      None if eps_t is None else _p(eps_t), self.seed, eps_off, _p(lens),
-                                      _pb(w.E1b), _pb(w.E2b), _p(w.ML), _p(w.Zs), _pb(w.Zb), w.ZA,
-                                      _p(w.eps) if eps_t is None else None, _p(w.pke), s), "encoder_fwd")
+            with self._timed("encoder_fwd"):
+                check(l.mlvae_encoder_fwd(B, T, Fd, E, Z, X, ep("fc.0.blocks.0.weight"), ep("fc.0.blocks.0.bias"),
+                                        ep("fc.0.blocks.2.weight"), ep("fc.0.blocks.2.bias"),
+                                        ep("mean_fc.weight"), ep("mean_fc.bias"),
+                                        None if eps_t is None else _p(eps_t), self.seed, eps_off, _p(lens),
+                                        _pb(w.E1b), _pb(w.E2b), _p(w.ML), _p(w.Zs), _pb(w.Zb), w.ZA,
+                                        _p(w.eps) if eps_t is None else None, _p(w.pke), s), "encoder_fwd")
             w.kl_parts = (w.pke, w.nke)
         else:
             # ---- reparameterisation noise
@@ -565,9 +607,10 @@ class VAEEngine:
                                           self._ptr(f"decoder.rnn.bias_hh_l{li}"), _p(w.G[li]), 8 * H,
                                           s), "skinny_proj")
             elif w.bf and din % 8 == 0:  # input projection on the 256² GEMM
-                self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), ldx, wb(f"decoder.rnn.weight_ih_l{li}"),
-                           din, _p(w.G[li]), 8 * H, bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
-                           bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+                with self._timed(f"proj_l{li}"):
+                    self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), ldx, wb(f"decoder.rnn.weight_ih_l{li}"),
+                               din, _p(w.G[li]), 8 * H, bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                               bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
             else:
                 self._mm(w, 0, 1, N, 8 * H, din, _p(xin) if xin is not None else None, din,
                          self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
@@ -579,7 +622,7 @@ class VAEEngine:
                 check(l.mlvae_lstm_fwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
                                           _p(w.Cs[li]), _p(w.Y[li]), _pb(w.Yb[li]) if w.bf else None,
-                                          _p(w.xbuf), w.xbuf.numel(), _p(w.err), s), "lstm_fwd")
+                                          _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd")
             xin, xin_bf, din, ldx = w.Y[li], (w.Yb[li] if w.bf else None), 2 * H, 2 * H
             if li < cfg.L - 1 and train and cfg.dropout > 0:
                 xin, xin_bf = w.Yd[li], (w.Ydb[li] if w.bf else None)
@@ -594,18 +637,19 @@ class VAEEngine:
             # both heads forward + recon loss (+ gradient) + heads backward + dY in one launch
             hp = lambda name: self._ptr(f"decoder.{name}")
             tr = 1 if train else 0
-            check(l.mlvae_heads_fused(
-                B, T, Fd, C, 2 * H, lt, tr, _pb(w.rnn_out_bf), wb("decoder.mean_fc.blocks.0.weight"),
-                _pb(self.w1_t) if train else None, hp("mean_fc.blocks.0.bias"),
-                hp("mean_fc.blocks.2.weight"), hp("mean_fc.blocks.2.bias"),
-                hp("mean_fc.blocks.4.weight"), hp("mean_fc.blocks.4.bias"),
-                hp("log_var_fc.blocks.2.weight"), hp("log_var_fc.blocks.2.bias"),
-                hp("log_var_fc.blocks.4.weight"), hp("log_var_fc.blocks.4.bias"),
-                X, _p(lens), count, w_rec, _p(w.P1), _p(w.P2m), _p(w.P2v), _p(w.MUX), _p(w.LVX),
-                _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
-                _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
-                _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
-                _p(w.ph), s), "heads_fused")
+            with self._timed("heads"):
+                check(l.mlvae_heads_fused(
+                  B, T, Fd, C, 2 * H, lt, tr, _pb(w.rnn_out_bf), wb("decoder.mean_fc.blocks.0.weight"),
+                  _pb(self.w1_t) if train else None, hp("mean_fc.blocks.0.bias"),
+                  hp("mean_fc.blocks.2.weight"), hp("mean_fc.blocks.2.bias"),
+                  hp("mean_fc.blocks.4.weight"), hp("mean_fc.blocks.4.bias"),
+                  hp("log_var_fc.blocks.2.weight"), hp("log_var_fc.blocks.2.bias"),
+                  hp("log_var_fc.blocks.4.weight"), hp("log_var_fc.blocks.4.bias"),
+                  X, _p(lens), count, w_rec, _p(w.P1), _p(w.P2m), _p(w.P2v), _p(w.MUX), _p(w.LVX),
+                  _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
+                  _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
+                  _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
+                  _p(w.ph), s), "heads_fused")
             check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w
@@ -717,7 +761,7 @@ class VAEEngine:
                 check(l.mlvae_lstm_bwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
                                           _p(w.Cs[li]), _p(w.dY[li]), _pb(dGb) if dGb is not None else None,
-                                          _p(w.xbuf), w.xbuf.numel(), _p(w.err), s), "lstm_bwd")
+                                          _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
             self._flush_side(pending)
             # dG: fp32 in G (fp32 mode) or bf16 in dGb (bf16 mode)
             dG, dG_bf = (None, dGb) if dGb is not None else (Gl, None)
@@ -788,8 +832,9 @@ class VAEEngine:
                 fused = False
             elif dG_bf is not None and li in self.wih_t and din >= 256:
                 # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy
-                self._fast(w, 0, 1, N, din, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[li]), 8 * H,
-                           _p(dx), din, drop_seed=seed if (drop and mask_ptr is None) else None)
+                with self._timed(f"dgrad_l{li}"):
+                    self._fast(w, 0, 1, N, din, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[li]), 8 * H,
+                               _p(dx), din, drop_seed=seed if (drop and mask_ptr is None) else None)
                 fused = drop and mask_ptr is None
             else:
                 fused = self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
@@ -811,12 +856,13 @@ class VAEEngine:
             # reparam/KL gradient, both LReLU dgrads and the six encoder gradients (encoder.hip)
             ep = lambda n: self._ptr(f"encoder.{n}")
             ge = lambda n: gp(f"encoder.{n}")
-            check(l.mlvae_encoder_bwd(B, T, Fd, E, Z, _p(w.dZs), _p(w.ML), _p(w.eps_used), _pb(w.E1b),
-                                      _pb(w.E2b), _p(w.x), ep("mean_fc.weight"), ep("fc.0.blocks.2.weight"),
-                                      _p(w.lens), count, w_kl, ge("mean_fc.weight"), ge("mean_fc.bias"),
-                                      ge("fc.0.blocks.2.weight"), ge("fc.0.blocks.2.bias"),
-                                      ge("fc.0.blocks.0.weight"), ge("fc.0.blocks.0.bias"), _p(w.enc_ws),
-                                      w.enc_ws.numel() * 4, s), "encoder_bwd")
+            with self._timed("encoder_bwd"):
+                check(l.mlvae_encoder_bwd(B, T, Fd, E, Z, _p(w.dZs), _p(w.ML), _p(w.eps_used), _pb(w.E1b),
+                                        _pb(w.E2b), _p(w.x), ep("mean_fc.weight"), ep("fc.0.blocks.2.weight"),
+                                        _p(w.lens), count, w_kl, ge("mean_fc.weight"), ge("mean_fc.bias"),
+                                        ge("fc.0.blocks.2.weight"), ge("fc.0.blocks.2.bias"),
+                                        ge("fc.0.blocks.0.weight"), ge("fc.0.blocks.0.bias"), _p(w.enc_ws),
+                                        w.enc_ws.numel() * 4, s), "encoder_bwd")
             # dW_ih_l0 | db_ih_l0 = db_hh_l0 = dG^T [z | 1] (skinny.hip), on the main stream
             # while the side stream finishes dW_hh_l0 (the step's two tails run side by side)
             check(l.mlvae_skinny_tn(8 * H, w.ZA, N, _pb(w.dGb[0]), 8 * H, _pb(w.Zb), w.ZA, Z,
@@ -921,6 +967,20 @@ class VAEEngine:
 
     def check_errors(self):
         """Host-synchronising check of the persistent kernels' spin-timeout word."""
-        for w in self._work.values():
-            if int(w.err.item()) != 0:
-                raise RuntimeError("LSTM recurrence hand-off timed out (err word set)")
+        if int(self.err.item()) != 0:
+            raise RuntimeError("LSTM recurrence hand-off timed out (err word set): the outputs "
+                               "and gradients of the affected steps are undefined")
+
+    def check_health(self, nonfinite_patience=3, where=""):
+        """Once-per-stage host check (Brain.fit calls it at every stage end): the recurrence
+        err word, and SpeechBrain's non-finite patience (check_gradients semantics,
+        ref:src/models/md_model.py:82) on the device counter of skipped steps -- more than
+        `nonfinite_patience` non-finite losses since the last check raises ValueError."""
+        self.check_errors()
+        ctr = int(self.nonfinite_ctr.item())
+        new = ctr - self._nonfinite_seen
+        self._nonfinite_seen = ctr
+        if new > nonfinite_patience:
+            raise ValueError(f"Loss is not finite and patience is exhausted ({new} non-finite "
+                             f"steps skipped{where}, patience {nonfinite_patience})")
+        return new

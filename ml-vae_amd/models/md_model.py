@@ -134,7 +134,9 @@ class MDModel(Brain):
         feats, lens = batch["feat"]
         norm = getattr(self.hparams, "normalizer", None)
         if norm is not None:
-            norm.train(stage == Stage.TRAIN)
+            # called exactly as SBModel.compute_forward does (ref:src/models/test_vanilla_vae/
+            # model.py:24-25): the normaliser is not one of the Brain's modules, so it stays in
+            # train mode and its global statistics also update on VALID/TEST batches
             feats = norm(feats, lens, epoch=self.hparams.epoch_counter.current)
         return feats.contiguous(), lens
 
@@ -197,6 +199,12 @@ class MDModel(Brain):
         return log
 
     def on_stage_end(self, stage, stage_loss, epoch=None):
+        if self.engine is not None:
+            # the fused step's device-side failure words, read once per stage (no per-step
+            # sync): recurrence hand-off timeout -> RuntimeError; more than nonfinite_patience
+            # skipped non-finite steps -> ValueError (SpeechBrain check_gradients semantics)
+            self.engine.check_health(self.nonfinite_patience,
+                                     where=f" in {stage.name} stage, epoch {epoch}")
         name = stage.name.lower()
         if epoch is None:
             epoch = self.hparams.epoch_counter.current

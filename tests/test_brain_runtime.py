@@ -1,0 +1,201 @@
+"""CPU tests of the recipe runtime around the fused step: SpeechBrain checkpoint layout,
+device-side InputNormalization, the normaliser's call on the fused path, bench.py's process
+model."""
+import json
+import os
+import subprocess
+import sys
+import types
+import warnings
+
+import pytest
+import torch
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ------------------------------------------------------------------ checkpoints
+def test_checkpoint_layout_is_speechbrains(tmp_path):
+    from brain import Checkpointer, EpochCounter
+    lin = torch.nn.Linear(3, 2)
+    ec = EpochCounter(5)
+    next(ec), next(ec)
+    ck = Checkpointer(tmp_path, {"encoder": lin, "epoch_counter": ec})
+    d = ck.save_and_keep_only(meta={"loss": torch.tensor(1.25), "kld_loss.loss": 0.5},
+                              min_keys=["loss"])
+    name = os.path.basename(d)
+    assert name.startswith("CKPT+") and len(name.split("+")) == 4   # CKPT+date+time+NN
+    files = sorted(os.listdir(d))
+    assert files == ["CKPT.yaml", "encoder.ckpt", "epoch_counter.ckpt"]
+    text = open(os.path.join(d, "CKPT.yaml")).read()
+    assert text.startswith("# yamllint disable\n")
+    meta = yaml.safe_load(text)
+    assert meta["loss"] == 1.25 and meta["end-of-epoch"] is True and "unixtime" in meta
+    assert open(os.path.join(d, "epoch_counter.ckpt")).read() == "2"
+    sd = torch.load(os.path.join(d, "encoder.ckpt"), weights_only=True)
+    assert set(sd) == {"weight", "bias"} and torch.equal(sd["weight"], lin.weight.detach())
+
+
+def test_recover_from_a_speechbrain_written_directory(tmp_path):
+    """A directory laid out the way SpeechBrain's Checkpointer writes it (built by hand here)
+    recovers, and min_key picks the lowest meta value."""
+    from brain import Checkpointer, EpochCounter
+    ref = {}
+    for i, (loss, stamp) in enumerate(((2.0, "2024-01-01+10-00-00+00"), (0.5, "2024-01-01+11-00-00+00"),
+                                       (1.0, "2024-01-01+12-00-00+00"))):
+        d = tmp_path / f"CKPT+{stamp}"
+        d.mkdir()
+        (d / "CKPT.yaml").write_text("# yamllint disable\n" +
+                                     yaml.safe_dump({"end-of-epoch": True, "loss": loss,
+                                                     "unixtime": 1.7e9 + i}))
+        w = {"weight": torch.full((2, 3), float(i)), "bias": torch.full((2,), float(i))}
+        torch.save(w, d / "encoder.ckpt")
+        (d / "epoch_counter.ckpt").write_text(str(10 + i))
+        ref[loss] = w
+    (tmp_path / "CKPT+broken").mkdir()  # no meta file: reported, not silently skipped
+    lin, ec = torch.nn.Linear(3, 2), EpochCounter(50)
+    ck = Checkpointer(tmp_path, {"encoder": lin, "epoch_counter": ec})
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        d = ck.recover_if_possible(min_key="loss")
+    assert any("CKPT+broken" in str(r.message) for r in rec)
+    assert d.endswith("11-00-00+00")
+    assert torch.equal(lin.weight.detach(), ref[0.5]["weight"]) and ec.current == 11
+    ck.recover_if_possible()  # most recent
+    assert ec.current == 12
+    assert ck.find_checkpoint(max_key="loss").endswith("10-00-00+00")
+
+
+def test_mid_epoch_checkpoint_replays_the_epoch(tmp_path):
+    from brain import Checkpointer, EpochCounter
+    ec = EpochCounter(9)
+    ec.current = 4
+    ck = Checkpointer(tmp_path, {"epoch_counter": ec})
+    ck.save_checkpoint(end_of_epoch=False)
+    ec.current = 0
+    ck.recover_if_possible()
+    assert ec.current == 3
+
+
+def test_optimizer_state_dict_is_torch_adam_layout():
+    """EngineOptimizer's state_dict must load into torch.optim.Adam (and back)."""
+    from mlvae_hip.engine import ParamLayout, VAEConfig
+    from mlvae_hip.optim import EngineOptimizer
+    cfg = VAEConfig(F=8, E=8, Z=4, H=8, L=2, C=8)
+    lay = ParamLayout(cfg)
+
+    class FakeEngine:  # host tensors standing in for the device buffers
+        def __init__(self):
+            self.cfg, self.layout = cfg, lay
+            self.exp_avg = torch.randn(lay.total)
+            self.exp_avg_sq = torch.rand(lay.total)
+            self.step_ctr = torch.tensor([7], dtype=torch.int32)
+
+        def view(self, name, buf):
+            o = lay.offsets[name]
+            return buf[o:o + lay.numel(name)].view(lay.shapes[name])
+    e = FakeEngine()
+    sd = EngineOptimizer(e).state_dict()
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in lay.shapes.values()]
+    opt = torch.optim.Adam(params, lr=1e-3)
+    opt.load_state_dict(sd)
+    st = opt.state[params[5]]
+    name5 = list(lay.shapes)[5]
+    assert torch.equal(st["exp_avg"], e.view(name5, e.exp_avg)) and float(st["step"]) == 7.0
+    e2 = FakeEngine()
+    EngineOptimizer(e2).load_state_dict(opt.state_dict())
+    for name in lay.shapes:
+        assert torch.equal(e2.view(name, e2.exp_avg), e.view(name, e.exp_avg))
+    assert int(e2.step_ctr) == 7
+
+
+# ------------------------------------------------------------------ normaliser
+def _norm_loop(x, lens, eps=1e-10):
+    """Per-utterance loop (SpeechBrain 0.5 _compute_current_stats, restated)."""
+    means, stds = [], []
+    for b in range(x.shape[0]):
+        n = int(torch.round(lens[b] * x.shape[1]).item())
+        seg = x[b, :n]
+        means.append(seg.mean(0))
+        stds.append(torch.clamp(seg.std(0), min=eps))
+    return torch.stack(means).mean(0), torch.stack(stds).mean(0)
+
+
+def test_input_normalization_matches_per_utterance_loop():
+    from brain import InputNormalization
+    g = torch.Generator().manual_seed(0)
+    norm = InputNormalization()
+    state_mean = state_std = None
+    for step in range(4):
+        x = torch.randn(5, 37, 6, generator=g) * 3 + 1
+        lens = torch.tensor([1.0, 0.6, 0.31, 0.9, 0.5])
+        cm, cs = _norm_loop(x, lens)
+        if step == 0:
+            state_mean, state_std = cm, cs
+        else:
+            w = 1.0 / (step + 1)
+            state_mean = (1 - w) * state_mean + w * cm
+            state_std = (1 - w) * state_std + w * cs
+        out = norm(x, lens, epoch=1)
+        assert torch.allclose(norm.glob_mean, state_mean, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(norm.glob_std, state_std, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(out, (x - state_mean) / state_std, rtol=1e-5, atol=1e-5)
+    assert norm.count == 4
+
+
+def test_fused_path_calls_the_normaliser_like_compute_forward():
+    """MDModel._normalised_feats (the fused path) must leave the normaliser in train mode on
+    VALID batches, as the reference's SBModel.compute_forward does: after the same TRAIN and
+    VALID batches, both routes hold the same global statistics and count."""
+    from brain import InputNormalization, Stage
+    from models.md_model import MDModel
+
+    class Batch(dict):
+        def to(self, device):
+            return self
+    g = torch.Generator().manual_seed(1)
+    batches = [(Stage.TRAIN if i % 2 == 0 else Stage.VALID,
+                Batch(feat=(torch.randn(3, 11, 4, generator=g), torch.tensor([1.0, 0.7, 0.5]))))
+               for i in range(4)]
+    n_fused, n_ref = InputNormalization(), InputNormalization()
+    fake = types.SimpleNamespace(device="cpu", hparams=types.SimpleNamespace(
+        normalizer=n_fused, epoch_counter=types.SimpleNamespace(current=1)))
+    for stage, b in batches:
+        MDModel._normalised_feats(fake, b, stage)
+        feats, lens = b["feat"]
+        n_ref(feats, lens, epoch=1)   # compute_forward: ref:src/models/test_vanilla_vae/model.py:24-25
+    assert n_fused.count == n_ref.count == 4
+    assert torch.equal(n_fused.glob_mean, n_ref.glob_mean)
+    assert torch.equal(n_fused.glob_std, n_ref.glob_std)
+
+
+# ------------------------------------------------------------------ bench process model
+def test_bench_spawns_one_rank_per_gpu():
+    """`bench.py --gpus 2` without torch.distributed.run starts two worker ranks itself
+    (checked with the gloo dry run: no GPU touched)."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["world"] == 2 and lines[0]["rank_sum"] == 3.0 and lines[0]["per_rank_batch"] == 128
+
+
+# ------------------------------------------------------------------ loss weights
+def test_weight_for_matches_reference_fixture():
+    """MDModel._weight_for / compute_and_save_losses (the product's restatement of
+    ref:src/models/md_model.py:189-213, incl. the '_kld' 2249/batch_size rule) against the
+    totals the reference's own compute_and_save_losses produced (tests/golden/loss_weights.json)."""
+    from models.md_model import MDModel
+    cases = json.load(open(os.path.join(ROOT, "tests", "golden", "loss_weights.json")))
+    for case in cases:
+        fake = types.SimpleNamespace(hparams=types.SimpleNamespace(**case["hparams"]), stats_loggers={})
+        fake._weight_for = types.MethodType(MDModel._weight_for, fake)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            total = MDModel.compute_and_save_losses(
+                fake, {k: torch.tensor(v) for k, v in zip(case["keys"], case["values"])})
+        assert abs(float(total) - case["total"]) <= 1e-6 * abs(case["total"]), case

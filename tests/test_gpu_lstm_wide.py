@@ -1,0 +1,91 @@
+"""Wide-batch BiLSTM recurrence (csrc/lstm_wide.hip) against an fp64 loop: forward h / c / saved
+gates and the BPTT's dG (fp32 and bf16 outputs) at batches past one batch-group launch (the
+metric's B = 256, B = 128, a ragged B = 200) and, forced through debug mode bit 12, at a small
+ragged batch.  Reference op: nn.LSTM bidirectional at ref:src/modules/decoder.py:14-15,22."""
+import ctypes
+
+import pytest
+import torch
+
+from gpu_utils import P, need_gpu, norm_rel, rel_err, stream
+from mlvae_hip._lib import check, lib
+
+pytestmark = pytest.mark.gpu
+
+H = 512
+# bf16 operands (h, dG exchanged as bf16): max-abs relative bounds as test_gpu_kernels' bf16 row
+TOL_Y, TOL_DG = 3e-2, 1.5e-1
+
+
+def _reference(B, T, seed):
+    torch.manual_seed(seed)
+    k = 1.0 / H ** 0.5
+    w = [(torch.rand(4 * H, H, dtype=torch.float64) * 2 - 1) * k for _ in range(2)]
+    gx = torch.randn(B, T, 8 * H, dtype=torch.float64) * 0.5
+    gxl = gx.clone().requires_grad_(True)
+    outs, cs, gates = [], [], []
+    for d, rev in ((0, False), (1, True)):
+        g4 = gxl[..., d * 4 * H:(d + 1) * 4 * H]
+        h = torch.zeros(B, H, dtype=torch.float64)
+        c = torch.zeros(B, H, dtype=torch.float64)
+        o, cc, ga = [None] * T, [None] * T, [None] * T
+        for t in (range(T - 1, -1, -1) if rev else range(T)):
+            gg = g4[:, t] + h @ w[d].t()
+            i, f, gc, og = gg.split(H, 1)
+            i, f, gc, og = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(gc), torch.sigmoid(og)
+            c = f * c + i * gc
+            h = og * torch.tanh(c)
+            o[t], cc[t], ga[t] = h, c, torch.cat([i, f, gc, og], 1)
+        outs.append(torch.stack(o, 1))
+        cs.append(torch.stack(cc, 1))
+        gates.append(torch.stack(ga, 1))
+    y = torch.cat(outs, -1)
+    dy = torch.randn_like(y)
+    (dG,) = torch.autograd.grad((y * dy).sum(), [gxl])
+    return w, gx, y.detach(), torch.cat(cs, -1).detach(), torch.cat(gates, -1).detach(), dy, dG
+
+
+@pytest.mark.parametrize("B,T,force", [(256, 16, False), (128, 20, False), (200, 12, False),
+                                       (20, 15, True), (48, 9, True)])
+def test_wide_recurrence_matches_fp64_loop(B, T, force):
+    need_gpu()
+    w, gx, y, cs, gates, dy, dG = _reference(B, T, B + T)
+    N = B * T
+    G = gx.float().reshape(N, 8 * H).cuda().contiguous()
+    Cs = torch.empty(N, 2 * H, device="cuda")
+    Y = torch.empty(N, 2 * H, device="cuda")
+    Yb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+    W0, W1 = w[0].float().cuda(), w[1].float().cuda()
+    xb = ctypes.c_size_t()
+    check(lib().mlvae_lstm_workspace_size(B, H, 1, ctypes.byref(xb)))
+    xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    if force:
+        lib().mlvae_lstm_set_debug_mode(4096)
+    try:
+        check(lib().mlvae_lstm_fwd_ex(1, B, T, H, P(W0), P(W1), P(G), P(Cs), P(Y), Yb.data_ptr(),
+                                      P(xbuf), xb.value, P(err), stream()))
+        torch.cuda.synchronize()
+        assert err.item() == 0
+        assert rel_err(Y.view(B, T, 2 * H), y) < TOL_Y
+        assert rel_err(Cs.view(B, T, 2 * H), cs) < TOL_Y
+        assert rel_err(G.view(B, T, 8 * H), gates) < TOL_Y
+        assert torch.equal(Yb, Y.to(torch.bfloat16))
+        G2 = G.clone()
+        dGb = torch.empty(N, 8 * H, device="cuda", dtype=torch.bfloat16)
+        dY = dy.float().reshape(N, 2 * H).cuda().contiguous()
+        # fp32 dG into G, then the bf16 dG copy (the train step's form) from the same inputs
+        check(lib().mlvae_lstm_bwd(1, B, T, H, P(W0), P(W1), P(G), P(Cs), P(dY), P(xbuf), xb.value,
+                                   P(err), stream()))
+        check(lib().mlvae_lstm_bwd_ex(1, B, T, H, P(W0), P(W1), P(G2), P(Cs), P(dY), dGb.data_ptr(),
+                                      P(xbuf), xb.value, P(err), stream()))
+        torch.cuda.synchronize()
+        assert err.item() == 0
+        e1 = rel_err(G.view(B, T, 8 * H), dG)
+        e2 = norm_rel(G.view(B, T, 8 * H), dG)
+        print(f"\nB={B} T={T} force={force}: Y {rel_err(Y.view(B, T, 2 * H), y):.2e}  dG max-rel {e1:.2e} "
+              f"norm-rel {e2:.2e}")
+        assert e1 < TOL_DG and e2 < 2e-2
+        assert torch.equal(dGb.float(), G.to(torch.bfloat16).float())
+    finally:
+        lib().mlvae_lstm_set_debug_mode(0)
