@@ -45,7 +45,8 @@ int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, float alpha, co
                   int a_bf16, int lda, const void* B, int b_bf16, int ldb, float beta, float* C,
                   int ldc, const float* bias1, const float* bias2, int epi, const float* aux,
                   int ldaux, int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream);
-/* The same with epilogue 3 = inter-layer dropout backward: C *= mask(drop_seed, row*ldc + col)
+/* The same with epilogue 3 = inter-layer dropout backward: C *= mask(drop_seed, drop_offset +
+ * row*ldc + col)
  * with the mask of mlvae_dropout_ex (keep prob 1 - drop_p, scale 1/(1 - drop_p)), so the dgrad
  * of the layer above writes the gradient of the dropout input directly
  * (ref:src/modules/decoder.py:14, nn.LSTM dropout between layers in train mode). */
@@ -53,8 +54,8 @@ int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K, float alph
                        const void* A, int a_bf16, int lda, const void* B, int b_bf16, int ldb,
                        float beta, float* C, int ldc, const float* bias1, const float* bias2,
                        int epi, const float* aux, int ldaux, int kshift_T, int kshift,
-                       unsigned long long drop_seed, float drop_p, float* ws, size_t ws_bytes,
-                       void* stream);
+                       unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                       float* ws, size_t ws_bytes, void* stream);
 /* Large bf16 GEMMs (256 x 256 tiles, LDS-DMA staging, bf16 operands only, fp32 C):
  *   C_b = epi( op(A_b) op(B_b) + bias1 + bias2 + beta C_b ),  b = 0 .. batch-1
  * A_b = A + b*a_bstride (elements), likewise B_b, C_b.  trans_a = 0: A [M,K] k-contiguous;
@@ -75,8 +76,9 @@ int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch, co
                     int lda, long long a_bstride, const void* B, int ldb, long long b_bstride,
                     float* C, int ldc, long long c_bstride, float beta, const float* bias1,
                     const float* bias2, int epi, const float* aux, int ldaux, int kshift_T,
-                    int kshift, int kshift_bstep, unsigned long long drop_seed, float drop_p,
-                    float* ws, size_t ws_bytes, void* stream);
+                    int kshift, int kshift_bstep, unsigned long long drop_seed,
+                    unsigned long long drop_offset, float drop_p, float* ws, size_t ws_bytes,
+                    void* stream);
 /* y (bf16) = round-to-nearest-even(x), n elements. */
 int mlvae_cast_bf16(size_t n, const float* x, void* y, void* stream);
 /* y [cols, rows] (bf16) = transpose of x [rows, cols] (fp32, row-major): the k-contiguous copy of
@@ -238,9 +240,11 @@ int mlvae_colsum_ex(int N, int C, const void* in, int in_bf16, int ld, float* ou
  * Inter-layer dropout of nn.LSTM in train mode (ref:src/modules/decoder.py:14). */
 int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
                   unsigned long long seed, float p, void* stream);
-/* the same writing y (fp32, may be NULL) and/or y_bf16 (bf16, may be NULL) */
+/* the same writing y (fp32, may be NULL) and/or y_bf16 (bf16, may be NULL); element i takes the
+ * mask of index offset + i (offset a multiple of 4): a data-parallel shard passes the global
+ * index of its first element, so every rank count draws the single-GPU run's masks */
 int mlvae_dropout_ex(size_t n, const float* x, float* y, void* y_bf16, const float* mask,
-                     unsigned long long seed, float p, void* stream);
+                     unsigned long long seed, unsigned long long offset, float p, void* stream);
 
 /* GMM-VAE latent block (SURVEY 8(f) rank 1; replaces ref:src/modules/gmm_vae.py:24-67).
  * P = the five heads as one stacked GEMM output, rows of width >= 4*N*Z + N:

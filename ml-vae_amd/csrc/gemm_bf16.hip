@@ -33,7 +33,8 @@ struct G2Args {
   int kshiftT, kshift;
   int splits, kchunk;
   float* ws;
-  unsigned long long dseed;   // EPI_DROPOUT: mask of flat element row*ldc + col
+  unsigned long long dseed;   // EPI_DROPOUT: mask of flat element doff + row*ldc + col
+  unsigned long long doff;
   float dkeep, dscale;
 };
 
@@ -44,7 +45,7 @@ __device__ __forceinline__ float epi_apply(const G2Args& g, float val, int row, 
   if (g.beta != 0.f) val += g.beta * *cp;
   if (g.epi == EPI_LRELU) val = lrelu(val);
   else if (g.epi == EPI_DLRELU) val *= lrelu_d(g.aux[(size_t)row * g.ldaux + col]);
-  else if (g.epi == EPI_DROPOUT) val *= dropout_scale(g.dseed, (size_t)row * g.ldc + col, g.dkeep, g.dscale);
+  else if (g.epi == EPI_DROPOUT) val *= dropout_scale(g.dseed, g.doff + (size_t)row * g.ldc + col, g.dkeep, g.dscale);
   return val;
 }
 
@@ -372,7 +373,8 @@ extern "C" int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K,
                                   int ldb, float beta, float* C, int ldc, const float* bias1,
                                   const float* bias2, int epi, const float* aux, int ldaux,
                                   int kshift_T, int kshift, unsigned long long drop_seed,
-                                  float drop_p, float* ws, size_t ws_bytes, void* stream) {
+                                  unsigned long long drop_offset, float drop_p, float* ws,
+                                  size_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0 || !C || (K > 0 && (!A || !B))) {
     mlvae_set_error("mlvae_gemm_ex: bad shape/ptr");
     return 1;
@@ -399,7 +401,7 @@ extern "C" int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K,
   g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
   g.alpha = alpha; g.beta = beta; g.bias1 = bias1; g.bias2 = bias2; g.epi = epi; g.aux = aux;
   g.ldaux = ldaux; g.kshiftT = kshift_T; g.kshift = kshift; g.ws = ws;
-  g.dseed = drop_seed; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
+  g.dseed = drop_seed; g.doff = drop_offset; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
   int s, kc;
   gemm2_plan(M, N, K, &s, &kc);
   if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * sizeof(float))) {
@@ -434,7 +436,7 @@ extern "C" int mlvae_gemm_ex(int trans_a, int trans_b, int M, int N, int K, floa
                              int kshift_T, int kshift, float* ws, size_t ws_bytes, void* stream) {
   if (epi == EPI_DROPOUT) { mlvae_set_error("mlvae_gemm_ex: dropout epilogue needs mlvae_gemm_ex_drop"); return 1; }
   return mlvae_gemm_ex_drop(trans_a, trans_b, M, N, K, alpha, A, a_bf16, lda, B, b_bf16, ldb, beta,
-                            C, ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift, 0ull, 0.f, ws,
+                            C, ldc, bias1, bias2, epi, aux, ldaux, kshift_T, kshift, 0ull, 0ull, 0.f, ws,
                             ws_bytes, stream);
 }
 

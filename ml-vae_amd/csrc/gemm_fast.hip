@@ -43,7 +43,7 @@ struct GFArgs {
   int epi;
   const float* aux; int ldaux;
   int kshiftT, kshift, kshift_bstep;
-  unsigned long long dseed; float dkeep, dscale;
+  unsigned long long dseed, doff; float dkeep, dscale;  // mask of doff + row*ldc + col
   int splits, kchunk;
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
   float* ws;
@@ -109,7 +109,7 @@ __device__ __forceinline__ float epi_apply(const GFArgs& g, float val, int row, 
   if (g.beta != 0.f) val += g.beta * *cp;
   if (g.epi == EPI_LRELU) val = lrelu(val);
   else if (g.epi == EPI_DLRELU) val *= lrelu_d(g.aux[(size_t)row * g.ldaux + col]);
-  else if (g.epi == EPI_DROPOUT) val *= dropout_scale(g.dseed, (size_t)row * g.ldc + col, g.dkeep, g.dscale);
+  else if (g.epi == EPI_DROPOUT) val *= dropout_scale(g.dseed, g.doff + (size_t)row * g.ldc + col, g.dkeep, g.dscale);
   return val;
 }
 
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
         f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * LSR + 4 * c4) + b;
         if (!split && g.epi == EPI_DROPOUT) {  // one Philox call per 4 aligned columns
           unsigned w4[4];
-          philox4(g.dseed, ((size_t)row * g.ldc + col) >> 2, w4);
+          philox4(g.dseed, (g.doff + (size_t)row * g.ldc + col) >> 2, w4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
         }
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
         // the 4 columns are one aligned Philox counter (row*ldc + col is a multiple of 4):
         // one call gives all four mask words, as dropout_scale() does element by element
         unsigned w4[4];
-        philox4(g.dseed, ((size_t)row * g.ldc + col) >> 2, w4);
+        philox4(g.dseed, (g.doff + (size_t)row * g.ldc + col) >> 2, w4);
         f32x4 v = acc[i][j] + b;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
@@ -352,7 +352,8 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
                                long long b_bstride, float* C, int ldc, long long c_bstride,
                                float beta, const float* bias1, const float* bias2, int epi,
                                const float* aux, int ldaux, int kshift_T, int kshift,
-                               int kshift_bstep, unsigned long long drop_seed, float drop_p,
+                               int kshift_bstep, unsigned long long drop_seed,
+                               unsigned long long drop_offset, float drop_p,
                                float* ws, size_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0 || batch < 1 || !C || (K > 0 && (!A || !B))) {
     mlvae_set_error("mlvae_gemm_bf16: bad shape/ptr");
@@ -391,7 +392,7 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   g.C = C; g.ldc = ldc; g.c_bs = c_bstride; g.beta = beta;
   g.bias1 = bias1; g.bias2 = bias2; g.epi = epi; g.aux = aux; g.ldaux = ldaux;
   g.kshiftT = kshift_T; g.kshift = kshift; g.kshift_bstep = kshift_bstep;
-  g.dseed = drop_seed; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
+  g.dseed = drop_seed; g.doff = drop_offset; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
   g.ws = ws;
   int s, kc;
   fast_plan(M, N, K, batch, &s, &kc);

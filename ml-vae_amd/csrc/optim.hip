@@ -207,12 +207,13 @@ __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __r
                                                       float* __restrict__ y,
                                                       unsigned short* __restrict__ ybf,
                                                       const float* __restrict__ mask,
-                                                      unsigned long long seed, float p, bool vec) {
+                                                      unsigned long long seed,
+                                                      unsigned long long qoff, float p, bool vec) {
   const float keep = 1.f - p, scale = 1.f / keep;
   const size_t nq = (n + 3) / 4;
   for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (size_t)gridDim.x * 256) {
     unsigned r[4] = {0u, 0u, 0u, 0u};
-    if (!mask) philox4(seed, q, r);
+    if (!mask) philox4(seed, qoff + q, r);  // element offset 4*qoff: the shard's first row
     if (vec && q * 4 + 3 < n) {  // 16-byte load, 16- / 8-byte stores
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + q * 4);
       f32x4 v;
@@ -311,18 +312,19 @@ extern "C" int mlvae_colsum(int N, int C, const float* in, int ld, float* out, f
 }
 
 extern "C" int mlvae_dropout_ex(size_t n, const float* x, float* y, void* y_bf16,
-                                const float* mask, unsigned long long seed, float p,
-                                void* stream) {
+                                const float* mask, unsigned long long seed,
+                                unsigned long long offset, float p, void* stream) {
   if (p < 0.f || p >= 1.f) { mlvae_set_error("dropout: p=%f out of range", p); return 1; }
+  if (offset % 4) { mlvae_set_error("dropout: element offset %llu not a multiple of 4", offset); return 1; }
   if (!y && !y_bf16) { mlvae_set_error("dropout: no output"); return 1; }
   const bool vec = ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)y_bf16 % 8) == 0;
   dropout_kernel<<<grid_for(n, 2048), 256, 0, (hipStream_t)stream>>>(
-      n, x, y, static_cast<unsigned short*>(y_bf16), mask, seed, p, vec);
+      n, x, y, static_cast<unsigned short*>(y_bf16), mask, seed, offset / 4, p, vec);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int mlvae_dropout(size_t n, const float* x, float* y, const float* mask,
                              unsigned long long seed, float p, void* stream) {
-  return mlvae_dropout_ex(n, x, y, nullptr, mask, seed, p, stream);
+  return mlvae_dropout_ex(n, x, y, nullptr, mask, seed, 0ull, p, stream);
 }

@@ -25,14 +25,14 @@ _SIGS = {
     "mlvae_gemm": [I, I, I, I, I, I, F, P, I, P, I, F, P, I, P, P, I, P, I, I, I, P, SZ, P],
     "mlvae_gemm_ex_workspace_size": [I, I, I],
     "mlvae_gemm_ex": [I, I, I, I, I, F, P, I, I, P, I, I, F, P, I, P, P, I, P, I, I, I, P, SZ, P],
-    "mlvae_gemm_ex_drop": [I, I, I, I, I, F, P, I, I, P, I, I, F, P, I, P, P, I, P, I, I, I, U64, F,
-                           P, SZ, P],
+    "mlvae_gemm_ex_drop": [I, I, I, I, I, F, P, I, I, P, I, I, F, P, I, P, P, I, P, I, I, I, U64, U64,
+                           F, P, SZ, P],
     "mlvae_cast_bf16": [SZ, P, P, P],
     "mlvae_cast_bf16_t": [I, I, P, P, P],
     "mlvae_gemm_bf16_workspace_size": [I, I, I, I],
     "mlvae_gemm_bf16_set_split_target": [I],
     "mlvae_gemm_bf16": [I, I, I, I, I, I, P, I, C.c_longlong, P, I, C.c_longlong, P, I, C.c_longlong,
-                        F, P, P, I, P, I, I, I, I, U64, F, P, SZ, P],
+                        F, P, P, I, P, I, I, I, I, U64, U64, F, P, SZ, P],
     "mlvae_lstm_workspace_size": [I, I, I, C.POINTER(SZ)],
     "mlvae_lstm_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
@@ -66,7 +66,7 @@ _SIGS = {
     "mlvae_colsum": [I, I, P, I, P, P, F, P, SZ, P],
     "mlvae_colsum_ex": [I, I, P, I, I, P, P, F, P, SZ, P],
     "mlvae_dropout": [SZ, P, P, P, U64, F, P],
-    "mlvae_dropout_ex": [SZ, P, P, P, P, U64, F, P],
+    "mlvae_dropout_ex": [SZ, P, P, P, P, U64, U64, F, P],
     "mlvae_lrelu_bwd": [SZ, P, P, P, P],
     "mlvae_clip_scale": [P, SZ, P, I, F, P, P],
     "mlvae_masked_mean_bwd": [I, I, I, P, I, P, P, P],

@@ -313,6 +313,7 @@ class VAEEngine:
         self.seed = seed
         self.rng_step = 0
         self._work = {}
+        self._T = 0
         self._pool = _Pool(self.device)
         self.overlap = True         # weight-gradient GEMMs on a side stream
         # split-K workgroup targets of the weight-gradient GEMMs (mlvae_gemm_bf16): those that
@@ -443,7 +444,8 @@ class VAEEngine:
                 if drop_seed is not None:
                     check(lib().mlvae_gemm_ex_drop(ta, tb, M, N, K, 1.0, a, abf, lda, b, bbf, ldb, beta,
                                                    C, ldc, bias1, bias2, EPI_DROPOUT, aux, ldaux,
-                                                   kshift_T, kshift, drop_seed, self.cfg.dropout,
+                                                   kshift_T, kshift, drop_seed, self._drop_off,
+                                                   self.cfg.dropout,
                                                    _p(ws), w.gws_bytes, self._stream()),
                           "mlvae_gemm_ex_drop")
                     return True
@@ -464,7 +466,8 @@ class VAEEngine:
         epi, p = (EPI_DROPOUT, self.cfg.dropout) if drop_seed is not None else (EPI_NONE, 0.0)
         check(lib().mlvae_gemm_bf16(ta, tb, M, N, K, batch, A_bf, lda, a_bs, B_bf, ldb, b_bs, C, ldc,
                                     c_bs, 0.0, bias1, bias2, epi, None, 0, kshift_T, kshift, kstep,
-                                    drop_seed or 0, p, _p(ws), w.gws_bytes, self._stream()),
+                                    drop_seed or 0, self._drop_off, p, _p(ws), w.gws_bytes,
+                                    self._stream()),
               "mlvae_gemm_bf16")
 
     def _colsum(self, w, N, Cn, src, ld, out, out2=None):
@@ -543,6 +546,7 @@ class VAEEngine:
         lens = lens.to(device=self.device, dtype=torch.float32).contiguous()
         w = self.work(B, T)
         w.x, w.lens = x, lens
+        self._T = T
         N, E, Z, H, C, Fd = w.N, cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
         X = _p(x)
@@ -682,6 +686,13 @@ class VAEEngine:
     def _eps_offset(self, T):
         return self.global_offset * T * self.cfg.Z
 
+    @property
+    def _drop_off(self):
+        """Philox element offset of this shard's inter-layer dropout masks: the global index of
+        its first element of the [B*T, 2H] layer output, so a data-parallel run draws exactly
+        the masks of the single-GPU run on the global batch."""
+        return self.global_offset * self._T * 2 * self.cfg.H
+
     def _dropout(self, w, li, src, dst, masks):
         mask_ptr = None
         if masks is not None:
@@ -692,7 +703,7 @@ class VAEEngine:
         dst_bf = w.Ydb[li] if w.bf else None
         check(lib().mlvae_dropout_ex(src.numel(), _p(src), _p(dst) if dst is not None else None,
                                      _pb(dst_bf) if dst_bf is not None else None, mask_ptr, seed,
-                                     self.cfg.dropout, self._stream()), "dropout")
+                                     self._drop_off, self.cfg.dropout, self._stream()), "dropout")
         w.__dict__.setdefault("_drop_seed", {})[li] = (seed, mask_ptr)
 
     def _global_count(self, w):
@@ -842,7 +853,8 @@ class VAEEngine:
                                  A_bf=pgb(dG_bf), B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
                                  drop_seed=seed if (drop and mask_ptr is None) else None)
             if drop and not fused:
-                check(l.mlvae_dropout(dx.numel(), _p(dx), _p(dx), mask_ptr, seed, cfg.dropout, s),
+                check(l.mlvae_dropout_ex(dx.numel(), _p(dx), _p(dx), None, mask_ptr, seed, self._drop_off,
+                                         cfg.dropout, s),
                       "dropout_bwd")
             self._flush_side(pending)  # li == 0 without the fused encoder
             if li > 0:

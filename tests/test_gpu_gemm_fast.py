@@ -53,7 +53,7 @@ def _run(ta, tb, M, N, K, batch=1, kshift_T=0, kshift=0, kstep=0, epi=0, beta=0.
     check(l.mlvae_gemm_bf16(ta, tb, M, N, K, batch, dA.data_ptr(), lda, A[0].numel(), dB.data_ptr(),
                             ldb, B[0].numel(), P(C), N, M * N, beta,
                             P(db1) if bias else None, P(db2) if bias else None, epi,
-                            P(daux), N, kshift_T, kshift, kstep, 0, 0.0, P(ws),
+                            P(daux), N, kshift_T, kshift, kstep, 0, 0, 0.0, P(ws),
                             ws.numel() * 4, stream()))
     torch.cuda.synchronize()
     return C.cpu(), torch.stack(refs)
@@ -102,7 +102,7 @@ def test_dropout_epilogue_matches_dropout_kernel():
     ws = torch.empty(16, device="cuda")
     for C, epi in ((C0, 0), (C1, 3)):
         check(l.mlvae_gemm_bf16(0, 1, M, N, K, 1, A.data_ptr(), K, 0, B.data_ptr(), K, 0, P(C), N, 0,
-                                0.0, None, None, epi, None, 0, 0, 0, 0, seed, p, P(ws), 64, stream()))
+                                0.0, None, None, epi, None, 0, 0, 0, 0, seed, 0, p, P(ws), 64, stream()))
     check(l.mlvae_dropout(C0.numel(), P(C0), P(C0), None, seed, p, stream()))
     torch.cuda.synchronize()
     assert torch.equal(C0, C1)

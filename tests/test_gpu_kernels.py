@@ -252,7 +252,7 @@ def test_dropout_mask_statistics_and_fused_backward():
     M, N, K = 300, 136, 256
     x = torch.ones(M * N, device="cuda")
     y = torch.empty_like(x)
-    check(l.mlvae_dropout_ex(x.numel(), P(x), P(y), None, None, seed, p, stream()))
+    check(l.mlvae_dropout_ex(x.numel(), P(x), P(y), None, None, seed, 0, p, stream()))
     torch.cuda.synchronize()
     vals = sorted(set(torch.unique(y).tolist()))
     assert len(vals) == 2 and vals[0] == 0.0 and abs(vals[1] - 1.0 / (1.0 - p)) < 1e-6, vals
@@ -268,7 +268,7 @@ def test_dropout_mask_statistics_and_fused_backward():
                           None, None, 0, None, 0, 0, 0, P(ws), ws.numel() * 4, stream()))
     check(l.mlvae_dropout(C0.numel(), P(C0), P(C0), None, seed, p, stream()))
     check(l.mlvae_gemm_ex_drop(0, 0, M, N, K, 1.0, A.data_ptr(), 1, K, B.data_ptr(), 1, N, 0.0,
-                               P(C1), N, None, None, 3, None, 0, 0, 0, seed, p, P(ws),
+                               P(C1), N, None, None, 3, None, 0, 0, 0, seed, 0, p, P(ws),
                                ws.numel() * 4, stream()))
     torch.cuda.synchronize()
     assert torch.equal(C0, C1)
@@ -288,10 +288,47 @@ def test_dropout_vector_and_scalar_paths_agree():
         xs = x.clone()
         if off:
             xs[1:] = x[:n]
-        check(l.mlvae_dropout_ex(n, P(xs, off), P(y, off), yb.data_ptr() + 2 * off, None, seed, p,
+        check(l.mlvae_dropout_ex(n, P(xs, off), P(y, off), yb.data_ptr() + 2 * off, None, seed, 0, p,
                                  stream()))
         torch.cuda.synchronize()
         outs.append((y[off:off + n].cpu(), yb[off:off + n].view(torch.int16).cpu()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     kept = (outs[0][0] != 0).float().mean().item()
     assert abs(kept - (1 - p)) < 0.01
+
+
+def test_dropout_offset_is_the_shard_of_the_global_mask():
+    """A data-parallel shard passes the global index of its first element: its masks are the
+    matching slice of the single-GPU masks, in the dropout kernel and in both fused dgrad
+    epilogues (mlvae_gemm_ex_drop, mlvae_gemm_bf16)."""
+    need_gpu()
+    l = lib()
+    seed, p = 20241016, 0.15
+    M, N, K = 96, 64, 64
+    x = torch.randn(M * N, device="cuda")
+    full = torch.empty_like(x)
+    check(l.mlvae_dropout_ex(x.numel(), P(x), P(full), None, None, seed, 0, p, stream()))
+    r0 = 40   # shard = rows 40.. of the [M, N] layer output
+    part = torch.empty(M * N - r0 * N, device="cuda")
+    check(l.mlvae_dropout_ex(part.numel(), P(x, r0 * N), P(part), None, None, seed, r0 * N, p, stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(part, full[r0 * N:])
+    A = torch.randn(M - r0, K).to(torch.bfloat16).cuda()
+    Bt = torch.randn(N, K).to(torch.bfloat16).cuda()
+    Bk = Bt.t().contiguous()
+    ws = torch.empty(1 << 16, device="cuda")
+    C0, C1, C2, C3 = (torch.empty(M - r0, N, device="cuda") for _ in range(4))
+    check(l.mlvae_gemm_ex(0, 0, M - r0, N, K, 1.0, A.data_ptr(), 1, K, Bk.data_ptr(), 1, N, 0.0, P(C0), N,
+                          None, None, 0, None, 0, 0, 0, P(ws), ws.numel() * 4, stream()))
+    check(l.mlvae_dropout_ex(C0.numel(), P(C0), P(C0), None, None, seed, r0 * N, p, stream()))
+    check(l.mlvae_gemm_ex_drop(0, 0, M - r0, N, K, 1.0, A.data_ptr(), 1, K, Bk.data_ptr(), 1, N, 0.0,
+                               P(C1), N, None, None, 3, None, 0, 0, 0, seed, r0 * N, p, P(ws),
+                               ws.numel() * 4, stream()))
+    for C, epi in ((C2, 0), (C3, 3)):
+        check(l.mlvae_gemm_bf16(0, 1, M - r0, N, K, 1, A.data_ptr(), K, 0, Bt.data_ptr(), K, 0, P(C), N,
+                                0, 0.0, None, None, epi, None, 0, 0, 0, 0, seed, r0 * N, p, P(ws),
+                                ws.numel() * 4, stream()))
+    check(l.mlvae_dropout_ex(C2.numel(), P(C2), P(C2), None, None, seed, r0 * N, p, stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1)
+    assert torch.equal(C2, C3)

@@ -37,7 +37,7 @@ def run(ta, tb, M, Nc, K, fast, iters=10):
         if fast:
             check(l.mlvae_gemm_bf16(ta, tb, M, Nc, K, 1, A.data_ptr(), A.shape[1], 0, B.data_ptr(),
                                     B.shape[1], 0, C.data_ptr(), Nc, 0, 0.0, None, None, 0, None, 0,
-                                    0, 0, 0, 0, 0.0, ws.data_ptr(), ws.numel() * 4, s))
+                                    0, 0, 0, 0, 0, 0.0, ws.data_ptr(), ws.numel() * 4, s))
         else:
             check(l.mlvae_gemm_ex(ta, tb, M, Nc, K, 1.0, A.data_ptr(), 1, A.shape[1], B.data_ptr(),
                                   1, B.shape[1], 0.0, C.data_ptr(), Nc, None, None, 0, None, 0, 0, 0,
