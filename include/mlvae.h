@@ -110,6 +110,9 @@ int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, cons
 int mlvae_lstm_bwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                       float* gates, const float* cells, const float* dy, void* dg_bf16,
                       void* xbuf, size_t xbytes, int* err, void* stream);
+/* Workgroups (one per CU, co-resident) of the recurrence launch for this shape: B past one
+ * batch-group launch runs the wide-batch kernels (csrc/lstm_wide.hip), which fill the chip. */
+int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd);
 /* Diagnostics: record per-step phase stamps of workgroup 0 into buf (NULL disables). */
 int mlvae_lstm_set_debug(void* buf);
 

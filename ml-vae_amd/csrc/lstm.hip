@@ -1009,6 +1009,19 @@ extern "C" int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes)
   return 0;
 }
 
+// Workgroups one recurrence launch of this shape occupies (one per CU, all co-resident): the
+// engine keeps side-stream GEMMs away from recurrences that fill the chip.
+extern "C" int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd) {
+  if (B <= 0 || H <= 0 || H % 4) return 0;
+  const int bmax = max_batch_per_launch(H, fwd != 0, prec);
+  if (prec == PREC_BF16 && (B > bmax || (g_dbg_mode & 4096))) {
+    const int w = lstm_wide_workgroups(B, H, fwd != 0);
+    if (w > 0) return w;
+  }
+  Plan p = make_plan(bmax < B ? bmax : B, H, prec, fwd != 0);
+  return 2 * p.NB * p.NJ;
+}
+
 extern "C" int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd,
                                  const float* w_hh_rev, float* gates, float* cells, float* y,
                                  void* y_bf16, void* xbuf, size_t xbytes, int* err, void* stream) {

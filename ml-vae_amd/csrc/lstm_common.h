@@ -109,3 +109,5 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   unsigned short* yb, unsigned short* dgb, unsigned long long* dbg, int dbg_mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply
 size_t lstm_wide_xbytes(int B, int H, bool fwd);
+// workgroups of the wide launch at (B, H), or 0 when it does not apply
+int lstm_wide_workgroups(int B, int H, bool fwd);

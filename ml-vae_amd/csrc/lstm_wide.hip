@@ -163,6 +163,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
   };
   if (io) {
     io_load(0);
+    io_load(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
@@ -205,9 +206,16 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
         for (int i = 0; i < PL; ++i)
           *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
       }
-      __syncthreads();  // h image of step s complete; gx ring slot s & 1 written last step
+      __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
       STAMP(2);
       if (abort_flag) break;
+      if (io) {
+        // the step's HBM traffic right behind the barrier, while the pollers run MFMAs: it
+        // drains before their next poll (issued behind the publish it delayed the hand-off:
+        // 4.3 vs 3.x us/step at B = 256).  gx of step s+1 lands before barrier s+1.
+        io_load(s + 1);
+        io_store(s - 1);
+      }
 #pragma unroll
       for (int kc = 0; kc < NKC; ++kc) {
         const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
@@ -252,12 +260,6 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
       }
     }
     STAMP(4);
-    if (io) {
-      // after the hand-off: gx of step s+1 into the ring (lands before barrier s+1), then the
-      // saved activations of step s-1
-      io_load(s + 1);
-      io_store(s - 1);
-    }
   }
   __syncthreads();
   if (io) io_store(T - 1);
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
   const auto rC = make_rsrc(a.Cs + gbase * 2 * H, 0xffffffffu);
   const auto rY = make_rsrc(a.Y + gbase * 2 * H, 0xffffffffu);
   auto load_cell = [&](int s_, CellIn (&c)[CPG]) {
-    if (s_ >= T) return;
+    if (s_ >= T || (s_ > 1 && (a.dbg_mode & 2048))) return;  // bit 11: timing without the loads
     const int t_ = dir ? s_ : T - 1 - s_;
     const int tp_ = dir ? t_ + 1 : t_ - 1;
     const int tpc = tp_ < 0 ? 0 : (tp_ >= T ? T - 1 : tp_);
@@ -571,7 +573,7 @@ WidePlan wide_plan(int B, int H, bool fwd) {
     p.xbytes = (size_t)2 * p.NB * NSLOT * BG * H * 2;
   } else {
     p.lds = (size_t)2 * 16 * 4 * p.HJ * 2 +
-            (size_t)8 * (H / 64) * (p.HJ / 32) * 64 * 16;  // + LDS-resident B-fragments (KLB = KC/4)
+            (size_t)8 * (H / 128) * (p.HJ / 32) * 64 * 16;  // + LDS-resident B-fragments (KLB = KC/4)
     p.xbytes = (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * p.HJ * 16 * 2;
   }
   if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;  // one recurrence workgroup per CU
@@ -593,6 +595,11 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
 }
 
 }  // namespace
+
+int lstm_wide_workgroups(int B, int H, bool fwd) {
+  WidePlan p = wide_plan(B, H, fwd);
+  return p.ok ? 2 * p.NB * p.NJ : 0;
+}
 
 size_t lstm_wide_xbytes(int B, int H, bool fwd) {
   WidePlan p = wide_plan(B, H, fwd);

@@ -74,6 +74,7 @@ _SIGS = {
     "mlvae_gmm_latent_bwd": [I, I, I, P, I, P, P, F, P, P, P, P, I, P],
     "mlvae_apply_weight_fwd": [I, I, I, P, I, P, P, I, P],
     "mlvae_apply_weight_bwd": [I, I, I, P, I, P, P, I, P, I, P, P],
+    "mlvae_lstm_launch_workgroups": [I, I, I, I],
     "mlvae_lstm_set_debug": [P],
     "mlvae_lstm_set_debug_mode": [I],
 }
@@ -136,3 +137,15 @@ def device_check():
     buf = C.create_string_buffer(64)
     rc = lib().mlvae_device_check(buf, 64)
     return rc, buf.value.decode()
+
+
+_cus = None
+
+
+def device_cus():
+    """Compute units of the current HIP device (256 on MI355X)."""
+    global _cus
+    if _cus is None:
+        import torch
+        _cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return _cus

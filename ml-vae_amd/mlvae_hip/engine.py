@@ -315,7 +315,11 @@ class VAEEngine:
         self._work = {}
         self._T = 0
         self._pool = _Pool(self.device)
-        self.overlap = True         # weight-gradient GEMMs on a side stream
+        # weight-gradient GEMMs on a side stream, unless the recurrences fill the chip
+        # (_full_chip; env MLVAE_OVERLAP=0/1 forces the choice for A/B runs)
+        env = os.environ.get("MLVAE_OVERLAP")
+        self._env_overlap = None if env is None else env != "0"
+        self.overlap = True
         # split-K workgroup targets of the weight-gradient GEMMs (mlvae_gemm_bf16): those that
         # overlap a recurrence / those in the step's tail (env overrides for A/B sweeps)
         self.split_overlap = int(os.environ.get("MLVAE_SPLIT_OVERLAP", "128"))
@@ -713,9 +717,21 @@ class VAEEngine:
         return _p(w.count)
 
     # ------------------------------------------------------------------ backward
+    def _full_chip(self, B):
+        """True when this batch's BPTT launch fills (>= 3/4 of) the chip: a side-stream GEMM
+        would then only hold CUs the recurrence's co-resident workgroups wait for (measured at
+        B = 256: 17.7 ms/step overlapped vs 15.3 serialised with whole-chip split-K plans)."""
+        if self._env_overlap is not None:
+            return not self._env_overlap
+        wgs = lib().mlvae_lstm_launch_workgroups(B, self.cfg.H, PREC[self.cfg.prec], 0)
+        return wgs >= 0.75 * _lib.device_cus()
+
     def backward(self, w):
         cfg = self.cfg
         B, T, N = w.B, w.T, w.N
+        full = self._full_chip(B)
+        self.overlap = not full
+        split_overlap, split_tail = (256, 256) if full else (self.split_overlap, self.split_tail)
         E, Z, H, C, Fd = cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
         g = self.grad
@@ -785,8 +801,7 @@ class VAEEngine:
                 # they take half the CUs; the bottom layer's run in the step's tail, on 160 of
                 # the 256 CUs so the encoder backward beside them is not held off the chip
                 # (alone 26 us, behind a whole-chip GEMM 112 us; c2 5.85 -> 5.80 ms/step)
-                prev = l.mlvae_gemm_bf16_set_split_target(self.split_tail if li == 0 else
-                                                          self.split_overlap)
+                prev = l.mlvae_gemm_bf16_set_split_target(split_tail if li == 0 else split_overlap)
                 try:
                     wgl_body(li=li, **kw)
                 finally:
@@ -859,7 +874,9 @@ class VAEEngine:
             self._flush_side(pending)  # li == 0 without the fused encoder
             if li > 0:
                 self._defer_side(pending, wgl)  # issued right after the next BPTT launch
-            if li == cfg.L - 1 and self.world > 1 and self.bucket_allreduce:
+            # (not beside a whole-chip BPTT: the collective's kernel would hold CUs the
+            # recurrence's co-resident workgroups wait for; all of it then goes in optimizer_step)
+            if li == cfg.L - 1 and self.world > 1 and self.bucket_allreduce and not full:
                 self._flush_side(pending)  # the bucket waits on the side stream: issue it all
                 self._start_suffix_allreduce()
         # ---- encoder

@@ -1,11 +1,16 @@
-# same-box sweep of an environment knob over bench runs: bash tools/gpu_knob.sh VAR v1 v2 ...
-# (two alternating rounds; one log per run under gpurun_out/knob_<VAR>_<v>_<round>.log)
+# same-box sweep of environment knobs over bench runs (two alternating rounds):
+#   bash tools/gpu_knob.sh "<bench args>" "VAR=v1 VAR2=w1" "VAR=v2" ...
+# one log per setting and round under gpurun_out/knob/<i>_<round>.log
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export PYTHONDONTWRITEBYTECODE=1
-VAR=$1; shift
+mkdir -p gpurun_out/knob
+ARGS=$1; shift
 for r in 1 2; do
-  for v in "$@"; do
-    ( export "$VAR=$v"; timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 30 > gpurun_out/knob_${VAR}_${v}_$r.log 2>&1 ) || exit 1
+  i=0
+  for setting in "$@"; do
+    ( export $setting; timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-extra $ARGS > gpurun_out/knob/${i}_$r.log 2>&1 ) || exit 1
+    echo "$setting" > gpurun_out/knob/${i}.name
+    i=$((i+1))
   done
 done

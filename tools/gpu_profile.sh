@@ -1,8 +1,7 @@
-# bench + rocprofv3 kernel trace/stats of the default bench command (c2, bf16); outputs under gpurun_out/prof
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
+export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
 mkdir -p gpurun_out/prof
-timeout -k 10 120 python -u bench.py --no-cpu-baseline > gpurun_out/prof/bench_plain.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-  python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof/bench.log 2>&1
+  python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra $1 > gpurun_out/prof/bench.log 2>&1
+echo "prof rc=$?"
