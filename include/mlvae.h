@@ -61,7 +61,10 @@ int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K, float alph
  * A_b = A + b*a_bstride (elements), likewise B_b, C_b.  trans_a = 0: A [M,K] k-contiguous;
  * trans_a = 1: A stored [K,M].  trans_b = 1: B stored [N,K]; trans_b = 0: B stored [K,N].
  * kshift (+ b*kshift_bstep) time-shifts the rows of a [K,N] B operand as mlvae_gemm does.
- * epi as mlvae_gemm_ex_drop (3 = dropout mask of (drop_seed, row*ldc + col)).  Operands need
+ * epi as mlvae_gemm_ex_drop (3 = dropout mask of (drop_seed, row*ldc + col)); epi | 16
+ * (EPI_OUT_F16) stores C as IEEE fp16 (C then points at fp16; beta 0, epi 0 or 3, N, ldc and
+ * c_bstride multiples of 4 / 8, aligned C and biases): the input projection into the wide
+ * recurrence's fp16 gate buffer (mlvae_lstm_gates_fp16).  Operands need
  * 16-byte aligned bases, lda/ldb and the contiguous extent multiples of 8.  Long-K products
  * split K into fp32 partial slabs (workspace: mlvae_gemm_bf16_workspace_size) reduced in a fixed
  * order.  Replaces the LSTM input projection, its dgrad and the weight gradients
@@ -110,8 +113,29 @@ int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, cons
 int mlvae_lstm_bwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                       float* gates, const float* cells, const float* dy, void* dg_bf16,
                       void* xbuf, size_t xbytes, int* err, void* stream);
-/* Workgroups (one per CU, co-resident) of the recurrence launch for this shape: B past one
- * batch-group launch runs the wide-batch kernels (csrc/lstm_wide.hip), which fill the chip. */
+/* Wide-batch recurrence (csrc/lstm_wide.hip): one launch per layer for the whole batch when B is
+ * past one batch-group launch (bf16, H = 512).  mlvae_lstm_gates_fp16(B, H, prec) = 1 for such
+ * shapes; their gate buffer is IEEE fp16 [B*T, 8H] (half the projection's write and the
+ * recurrences' reads) and they run only through the _ex2 entry points with gates_fp16 = 1.
+ * gates_fp16 = 0 (and every entry point above) always runs the batch-group kernels on fp32
+ * gates, batch-chunked.
+ * fwd_ex2: y (fp32) may be NULL on the wide path; y_bf16 as _ex; y_drop_bf16 (wide path only,
+ *   may be NULL) = bf16 dropout(h) for the next layer, mask of element drop_offset + row*2H + col
+ *   from Philox(drop_seed) with keep 1 - drop_p -- the same mask mlvae_dropout_ex and the
+ *   dropout epilogues (epi 3) draw, so the dgrad GEMM's epilogue recomputes it.
+ * bwd_ex2: gates are the forward's (fp16 when gates_fp16); the wide backward writes dG only as
+ *   bf16 into dg_bf16 (required). */
+int mlvae_lstm_gates_fp16(int B, int H, int prec);
+int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                       void* gates, int gates_fp16, float* cells, float* y, void* y_bf16,
+                       void* y_drop_bf16, unsigned long long drop_seed,
+                       unsigned long long drop_offset, float drop_p, void* xbuf, size_t xbytes,
+                       int* err, void* stream);
+int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                       void* gates, int gates_fp16, const float* cells, const float* dy,
+                       void* dg_bf16, void* xbuf, size_t xbytes, int* err, void* stream);
+/* Workgroups (one per CU, co-resident) of the recurrence launch for this shape as the engine
+ * runs it (fp16 gates where mlvae_lstm_gates_fp16): the wide kernels fill the chip. */
 int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd);
 /* Diagnostics: record per-step phase stamps of workgroup 0 into buf (NULL disables). */
 int mlvae_lstm_set_debug(void* buf);
@@ -163,6 +187,10 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
  * input projection z W_ih^T + b_ih + b_hh (ref:src/modules/decoder.py:14-15,22), K = latent. */
 int mlvae_skinny_proj(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
                       const float* bias1, const float* bias2, float* C, int ldc, void* stream);
+/* The same with C fp32 (c_fp16 = 0) or IEEE fp16 (c_fp16 = 1: the wide recurrence's gates). */
+int mlvae_skinny_proj_ex(int M, int N, int K, const void* A, int lda, const void* B, int ldb,
+                         const float* bias1, const float* bias2, void* C, int ldc, int c_fp16,
+                         void* stream);
 int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                     float* C, int ldc, void* stream);
 size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K);

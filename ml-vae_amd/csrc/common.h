@@ -47,6 +47,18 @@ __device__ __forceinline__ short f2bf(float x) {
   __hip_bfloat16 h = __float2bfloat16(x);
   return *reinterpret_cast<short*>(&h);
 }
+// IEEE fp16 (round to nearest even): the wide-batch recurrence's gate buffer G
+__device__ __forceinline__ unsigned short f2h(float x) {
+  _Float16 h = (_Float16)x;
+  return __builtin_bit_cast(unsigned short, h);
+}
+__device__ __forceinline__ float h2f(unsigned short s) {
+  return (float)__builtin_bit_cast(_Float16, s);
+}
+__device__ __forceinline__ u32x2 f2h4(f32x4 v) {
+  return u32x2{(unsigned)f2h(v[0]) | ((unsigned)f2h(v[1]) << 16),
+               (unsigned)f2h(v[2]) | ((unsigned)f2h(v[3]) << 16)};
+}
 __device__ __forceinline__ float bf2f(short s) {
   unsigned u = ((unsigned)(unsigned short)s) << 16;
   return __uint_as_float(u);

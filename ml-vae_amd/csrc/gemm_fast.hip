@@ -46,10 +46,12 @@ struct GFArgs {
   unsigned long long dseed, doff; float dkeep, dscale;  // mask of doff + row*ldc + col
   int splits, kchunk;
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
+  int c16;            // C stored as fp16 (epi bit EPI_OUT_F16)
   float* ws;
 };
 
 enum { EPI_NONE = 0, EPI_LRELU = 1, EPI_DLRELU = 2, EPI_DROPOUT = 3 };
+constexpr int EPI_OUT_F16 = 16;  // flag bit of the ABI's epi: C is fp16 (staged epilogue only)
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(3))) bf16x4* lds_b4_t;
@@ -105,6 +107,62 @@ __device__ __forceinline__ bf16x8 frag(const short* img, int base, int kk, int l
   }
 }
 
+// ---- deep-pipelined variant: BK = 32, four LDS buffers (4 x 32 KB), three K-steps in flight.
+// The 2-buffer loop above drains vmcnt(0) at every K-step, so each 64-deep step waits for the
+// next step's loads issued only one step earlier; at B*T = 128,000 rows (the metric's batch)
+// that latency, not the MFMA, set the projection's 37 % of peak.  Here K-step it+3 is staged
+// right after the barrier that retires K-step it, and the wait before each step is a counted
+// vmcnt that leaves the two younger steps in flight (raw s_barrier: no implicit drain).
+constexpr int DBK = 32, DNB = 4;
+constexpr int DIMG = TBM * DBK;  // elements per operand image (16 KB)
+
+__device__ __forceinline__ int kc_swz(int row) { return ((row >> 2) & 1) << 1; }  // 32-k rows
+
+template <bool KC>
+__device__ __forceinline__ void stage32(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
+                                        int k0, int kend, int shT, int sh, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int piece = wave * 2 + j;
+    const int p = piece * 64 + lane;
+    unsigned off;
+    if constexpr (KC) {  // [256 rows][32 k]: 4 chunks per row, chunk c at slot c ^ kc_swz(row)
+      const int row = p >> 2, c = (p & 3) ^ kc_swz(row);
+      const int gr = r0 + row, gk = k0 + 8 * c;
+      off = (gr < R && gk < kend) ? (unsigned)(((size_t)gr * ld + gk) * 2) : OOB;
+    } else {             // [32 k][256 rows]: 32 chunks per k-row, as the 64-deep image
+      const int kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr);
+      int gk = k0 + kr;
+      const int gr = r0 + 8 * c;
+      bool ok = gk < kend && gr < R;
+      if (sh != 0 && ok) {
+        const int t = gk % shT + sh;
+        ok = t >= 0 && t < shT;
+        gk += sh;
+      }
+      off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag32(const short* img, int base, int lane) {
+  if constexpr (KC) {
+    const int row = base + (lane & 15), c = lane >> 4;
+    return *reinterpret_cast<const bf16x8*>(img + row * DBK + ((c ^ kc_swz(row)) << 3));
+  } else {
+    const int g = lane >> 4, i4 = lane & 15, q = i4 >> 2, pp = i4 & 3;
+    const int r1 = 8 * g + q, r2 = r1 + 4;
+    const int c = (base >> 3) + (pp >> 1);
+    const short* a1 = img + r1 * TBM + ((c ^ (int)mc_swz(r1)) << 3) + 4 * (pp & 1);
+    const short* a2 = img + r2 * TBM + ((c ^ (int)mc_swz(r2)) << 3) + 4 * (pp & 1);
+    const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_t)a1);
+    const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_t)a2);
+    return bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  }
+}
+
 __device__ __forceinline__ float epi_apply(const GFArgs& g, float val, int row, int col, float* cp) {
   if (g.beta != 0.f) val += g.beta * *cp;
   if (g.epi == EPI_LRELU) val = lrelu(val);
@@ -113,7 +171,7 @@ __device__ __forceinline__ float epi_apply(const GFArgs& g, float val, int row, 
   return val;
 }
 
-template <bool AKC, bool BKC>
+template <bool AKC, bool BKC, bool DEEP>
 __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   short* lds = reinterpret_cast<short*>(smem);   // [buf][A image, B image]
@@ -141,7 +199,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   const auto rb = make_rsrc(Bp, OOB);
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+  const int nk = kend > kbeg ? (kend - kbeg + (DEEP ? DBK : TBK) - 1) / (DEEP ? DBK : TBK) : 0;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -149,6 +207,38 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (DEEP) {
+    auto stage4 = [&](int it) {  // K-step it into buffer it & 3
+      const int buf = it & (DNB - 1), k0 = kbeg + it * DBK;
+      stage32<AKC>(lds + (buf * 2 + 0) * DIMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+      stage32<BKC>(lds + (buf * 2 + 1) * DIMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+    };
+    for (int it = 0; it < 3 && it < nk; ++it) stage4(it);
+    for (int it = 0; it < nk; ++it) {
+      // K-step it's pieces (4 per wave) have landed once at most the younger steps' remain
+      const int younger = min(2, nk - 1 - it);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // ... everyone's; and step it-1's buffer is free
+      if (it + 3 < nk) stage4(it + 3);
+      const short* As = lds + ((it & (DNB - 1)) * 2 + 0) * DIMG;
+      const short* Bs = lds + ((it & (DNB - 1)) * 2 + 1) * DIMG;
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag32<BKC>(Bs, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = frag32<AKC>(As, wm * 128 + i * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
+  } else {
   auto stage_both = [&](int buf, int k0) {
     stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
     stage<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
@@ -181,10 +271,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile it+1 has landed (this wave's pieces)
     __syncthreads();                                 // ... everyone's; buffer cur is free
   }
+  }
 
   // epilogue: lane holds C[m0 + wm*128 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
   const bool split = g.splits > 1;
-  float* Cb = g.C + bz * g.c_bs;
+  float* Cb = g.c16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(g.C) + bz * g.c_bs)
+                    : g.C + bz * g.c_bs;
   float* wsz = split ? g.ws + ((size_t)bz * g.splits + blockIdx.z) * (size_t)g.M * g.N : nullptr;
   const bool vec = (g.ldc % 4) == 0 && (((uintptr_t)Cb) % 16) == 0;
   // Row-contiguous epilogue through the (now free) LDS: four passes of 64 tile rows; every
@@ -226,7 +318,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
         }
-        *reinterpret_cast<f32x4*>(dst + (size_t)row * ldd + col) = v;
+        if (!split && g.c16)
+          *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(Cb) + (size_t)row * ldd + col) = f2h4(v);
+        else
+          *reinterpret_cast<f32x4*>(dst + (size_t)row * ldd + col) = v;
       }
       __syncthreads();  // the staging rows are rewritten by the next pass
     }
@@ -279,21 +374,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
   const size_t MN = (size_t)g.M * g.N;
   const int bz = blockIdx.y;
   const float* ws = g.ws + (size_t)bz * g.splits * MN;
-  float* Cb = g.C + bz * g.c_bs;
+  float* Cb = g.c16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(g.C) + bz * g.c_bs)
+                    : g.C + bz * g.c_bs;
   for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < MN; idx += (size_t)gridDim.x * 256) {
     float s = 0.f;
     for (int z = 0; z < g.splits; ++z) s += ws[z * MN + idx];
     const int row = (int)(idx / g.N), col = (int)(idx % g.N);
     if (g.bias1) s += g.bias1[col];
     if (g.bias2) s += g.bias2[col];
+    if (g.c16) {  // beta == 0, epi NONE / DROPOUT (checked on the host)
+      if (g.epi == EPI_DROPOUT) s *= dropout_scale(g.dseed, g.doff + (size_t)row * g.ldc + col, g.dkeep, g.dscale);
+      reinterpret_cast<unsigned short*>(Cb)[(size_t)row * g.ldc + col] = f2h(s);
+      continue;
+    }
     float* cp = Cb + (size_t)row * g.ldc + col;
     *cp = epi_apply(g, s, row, col, cp);
   }
 }
 
-template <bool AKC, bool BKC>
+template <bool AKC, bool BKC, bool DEEP>
 int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s) {
-  auto k = gemm256_kernel<AKC, BKC>;
+  auto k = gemm256_kernel<AKC, BKC, DEEP>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -360,6 +461,13 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     return 1;
   }
   if (M == 0 || N == 0) return 0;
+  const int c16 = (epi & EPI_OUT_F16) ? 1 : 0;
+  epi &= ~EPI_OUT_F16;
+  if (c16 && (beta != 0.f || (epi != EPI_NONE && epi != EPI_DROPOUT) || N % 4 || ldc % 4 ||
+              ((uintptr_t)C % 16) || (c_bstride % 8) || ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16))) {
+    mlvae_set_error("mlvae_gemm_bf16: fp16 C needs beta 0, epilogue none/dropout, N and ldc %% 4, aligned C/bias");
+    return 1;
+  }
   if (epi < EPI_NONE || epi > EPI_DROPOUT) { mlvae_set_error("mlvae_gemm_bf16: bad epilogue %d", epi); return 1; }
   if (epi == EPI_DLRELU && !aux) { mlvae_set_error("mlvae_gemm_bf16: DLRELU needs aux"); return 1; }
   if (epi == EPI_DROPOUT && !(drop_p >= 0.f && drop_p < 1.f)) {
@@ -409,13 +517,27 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     return e ? atoi(e) : 4;
   }();
   g.group_m = group_m;
+  g.c16 = c16;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), batch, s);
   int rc;
-  if (akc && bkc) rc = launch_fast<true, true>(g, grid, st);
-  else if (akc) rc = launch_fast<true, false>(g, grid, st);
-  else if (bkc) rc = launch_fast<false, true>(g, grid, st);
-  else rc = launch_fast<false, false>(g, grid, st);
+  // deep-pipelined main loop (BK 32, 3 K-steps in flight) only with MLVAE_GEMM_DEEP=1: measured
+  // slower inside the c3 step (16.0 vs 15.3 ms), kept for A/B
+  static const bool deep = [] {
+    const char* e = getenv("MLVAE_GEMM_DEEP");
+    return e && atoi(e) != 0;
+  }();
+  if (deep) {
+    if (akc && bkc) rc = launch_fast<true, true, true>(g, grid, st);
+    else if (akc) rc = launch_fast<true, false, true>(g, grid, st);
+    else if (bkc) rc = launch_fast<false, true, true>(g, grid, st);
+    else rc = launch_fast<false, false, true>(g, grid, st);
+  } else {
+    if (akc && bkc) rc = launch_fast<true, true, false>(g, grid, st);
+    else if (akc) rc = launch_fast<true, false, false>(g, grid, st);
+    else if (bkc) rc = launch_fast<false, true, false>(g, grid, st);
+    else rc = launch_fast<false, false, false>(g, grid, st);
+  }
   if (rc) return rc;
   MLVAE_CHECK_LAUNCH();
   if (s > 1) {

@@ -930,20 +930,46 @@ int launch_rs(const LstmArgs& a, const Plan& p, hipStream_t s) {
   return 0;
 }
 
+// bf16 past one batch-group launch's batch: one wide-batch launch per direction pair
+// (lstm_wide.hip) instead of sequential batch chunks, forward AND backward (they share the
+// fp16 gate buffer); debug mode bit 12 forces it at any batch (A/B timing)
+bool use_wide(int B, int H, int prec) {
+  if (prec != PREC_BF16 || H <= 0 || H % 4) return false;
+  const int bf = max_batch_per_launch(H, true, prec), bb = max_batch_per_launch(H, false, prec);
+  if (!(B > (bf < bb ? bf : bb) || (g_dbg_mode & 4096))) return false;
+  return lstm_wide_workgroups(B, H, true) > 0 && lstm_wide_workgroups(B, H, false) > 0;
+}
+
+struct WideExtra {  // forward-only outputs of the wide kernels
+  unsigned short* ydb = nullptr;
+  unsigned long long seed = 0, off = 0;
+  float p = 0.f;
+};
+
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
         float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
-        unsigned short* yb = nullptr, unsigned short* dgb = nullptr) {
+        unsigned short* yb = nullptr, unsigned short* dgb = nullptr, int gates_fp16 = 0,
+        const WideExtra& ex = WideExtra()) {
   if (B <= 0 || T <= 0) return 0;
   if (H <= 0 || H % 4 != 0) { mlvae_set_error("lstm: H=%d must be a positive multiple of 4", H); return 1; }
   if (prec != PREC_F32 && prec != PREC_BF16) { mlvae_set_error("lstm: bad prec %d", prec); return 1; }
-  const int bmax = max_batch_per_launch(H, fwd, prec);
-  // bf16: one wide-batch launch (lstm_wide.hip) instead of sequential batch chunks; debug
-  // mode bit 12 forces it at any batch (A/B timing)
-  if (prec == PREC_BF16 && (B > bmax || (g_dbg_mode & 4096))) {
-    const int rc = lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb,
-                                 g_dbg, g_dbg_mode);
-    if (rc >= 0) return rc;
+  // fp16 gates select the wide-batch kernels; fp32 gates the batch-group kernels (chunked)
+  const bool wide = gates_fp16 != 0;
+  if (wide && !use_wide(B, H, prec)) {
+    mlvae_set_error("lstm: B=%d H=%d prec=%d: fp16 gates only where mlvae_lstm_gates_fp16() = 1", B, H, prec);
+    return 1;
   }
+  if (wide) {
+    if (!fwd && !dgb) { mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 (NULL)"); return 1; }
+    if (ex.ydb && !(ex.p >= 0.f && ex.p < 1.f)) { mlvae_set_error("lstm: dropout p=%g", ex.p); return 1; }
+    return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.ydb,
+                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode);
+  }
+  if (ex.ydb || !Y) {
+    mlvae_set_error("lstm: fused dropout output / Y = NULL only on the wide-batch path");
+    return 1;
+  }
+  const int bmax = max_batch_per_launch(H, fwd, prec);
   if (bmax < BG) { mlvae_set_error("lstm: H=%d too large for one resident launch", H); return 1; }
   Plan full = make_plan(bmax < B ? bmax : B, H, prec, fwd);
   const size_t need_x = fwd ? full.xbytes_fwd : full.xbytes_bwd;
@@ -1014,12 +1040,36 @@ extern "C" int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes)
 extern "C" int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd) {
   if (B <= 0 || H <= 0 || H % 4) return 0;
   const int bmax = max_batch_per_launch(H, fwd != 0, prec);
-  if (prec == PREC_BF16 && (B > bmax || (g_dbg_mode & 4096))) {
-    const int w = lstm_wide_workgroups(B, H, fwd != 0);
-    if (w > 0) return w;
-  }
+  if (use_wide(B, H, prec)) return lstm_wide_workgroups(B, H, fwd != 0);  // with fp16 gates
   Plan p = make_plan(bmax < B ? bmax : B, H, prec, fwd != 0);
   return 2 * p.NB * p.NJ;
+}
+
+// 1 when this shape can run the wide-batch kernels (one launch for the whole batch), whose
+// gate buffer is fp16 [B*T, 8H]: the caller then passes fp16 gates to the _ex2 entry points.
+// fp32 gates (every other entry point) always run the batch-group kernels, batch-chunked.
+extern "C" int mlvae_lstm_gates_fp16(int B, int H, int prec) { return use_wide(B, H, prec) ? 1 : 0; }
+
+extern "C" int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd,
+                                  const float* w_hh_rev, void* gates, int gates_fp16, float* cells,
+                                  float* y, void* y_bf16, void* y_drop_bf16,
+                                  unsigned long long drop_seed, unsigned long long drop_offset,
+                                  float drop_p, void* xbuf, size_t xbytes, int* err, void* stream) {
+  WideExtra ex;
+  ex.ydb = static_cast<unsigned short*>(y_drop_bf16);
+  ex.seed = drop_seed; ex.off = drop_offset; ex.p = drop_p;
+  return run(true, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, y, xbuf,
+             xbytes, err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr,
+             gates_fp16, ex);
+}
+
+extern "C" int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd,
+                                  const float* w_hh_rev, void* gates, int gates_fp16,
+                                  const float* cells, const float* dy, void* dg_bf16, void* xbuf,
+                                  size_t xbytes, int* err, void* stream) {
+  return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
+             const_cast<float*>(cells), const_cast<float*>(dy), xbuf, xbytes, err,
+             (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), gates_fp16);
 }
 
 extern "C" int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd,

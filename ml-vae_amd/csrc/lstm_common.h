@@ -31,6 +31,11 @@ struct LstmArgs {
   unsigned* xtab;           // [ngroups][NJ] XCC id + 1 of every member (zeroed per launch)
   unsigned short* Yb;       // optional bf16 copy of h [B*T, 2H] (fwd; GEMM operand)
   unsigned short* dGb;      // optional: bwd writes dG as bf16 [B*T, 8H] here instead of into G
+  // wide-batch forward only: bf16 dropout(h) [B*T, 2H] for the next layer (Philox mask of
+  // element doff + row*2H + col, keep prob dkeep, scale dscale; NULL = none)
+  unsigned short* Ydb;
+  unsigned long long dseed, doff;
+  float dkeep, dscale;
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -106,7 +111,9 @@ __device__ __forceinline__ bool tags_ok(u32x4 v, unsigned tag, bool g0, bool g1)
 // supported (the caller then falls back to chunked batch-group launches), else a status.
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
-                  unsigned short* yb, unsigned short* dgb, unsigned long long* dbg, int dbg_mode);
+                  unsigned short* yb, unsigned short* dgb, unsigned short* ydb,
+                  unsigned long long dseed, unsigned long long doff, float dp,
+                  unsigned long long* dbg, int dbg_mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply
 size_t lstm_wide_xbytes(int B, int H, bool fwd);
 // workgroups of the wide launch at (B, H), or 0 when it does not apply

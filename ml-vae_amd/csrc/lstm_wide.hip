@@ -26,6 +26,7 @@
 //             each workgroup sums its NJ producers' partials with a DPP reduce-scatter.
 // Hand-off protocol, slots and tags: lstm_common.h / lstm.hip header.
 #include "lstm_common.h"
+#include <type_traits>
 
 namespace {
 
@@ -57,8 +58,10 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int PL = NKC / 4;                 // poll loads (k-chunks) per lane, waves 0-3
   constexpr int ROWB = H * 2;                 // bytes of one h-image row (bf16)
   constexpr int HIMG = 16 * ROWB;
-  constexpr int GXU = 4 * HJ + 4;             // gx ring floats per utterance: [gate][unit] + 16 B
-  constexpr int OUU = 6 * HJ + 4;             // out ring floats per utterance: [i f g o c h][unit]
+  constexpr int GXU = 4 * HJ + 8;             // gx ring halfs per utterance: [gate][unit] + 16 B
+  // out ring bytes per utterance: gates fp16 [i f g o][HJ] | c fp32 [HJ] | h fp32 [HJ] | 16 B
+  constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;
+  constexpr int NC8 = 16 * HJ / 8;            // 8-unit chunks of h per step
   constexpr int KLF = 2;                      // k-chunks whose A-fragments live in LDS (VGPR budget)
   constexpr int KR = NKC - KLF;               // ... and in registers
   constexpr int NQ = 16 * 4 * HJ / 4;         // 16-byte quads of gx / gates per step
@@ -66,16 +69,18 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
   static_assert(NQ % 256 == 0, "io split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* himg = smem;                                        // [2][16][ROWB], swizzled slots
-  float* gxr = reinterpret_cast<float*>(smem + 2 * HIMG);   // [2][16][GXU]
-  float* outr = gxr + 2 * 16 * GXU;                          // [2][16][OUU]
-  bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUU);  // [wave][TPW][KLF][lane]
+  unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2][16][GXU] fp16
+  char* outr = reinterpret_cast<char*>(gxr + 2 * 16 * GXU);                 // [2][16][OUB]
+  bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUB);  // [wave][TPW][KLF][lane]
+  unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);  // [2][NC8] keep bits
   __shared__ int abort_flag;
 
   const int ngroups = 2 * a.NB;
   const int gid = blockIdx.x % ngroups, js = blockIdx.x / ngroups;
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int T = a.T, j0 = js * HJ;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
   const int bglob = grp * BG + bi;
@@ -110,12 +115,15 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
   short* xb = reinterpret_cast<short*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
   auto xr = make_rsrc(xb, (unsigned)(NSLOT * xslot * sizeof(short)));
 
-  // ---- io role (waves 4-7).  The input projection of a step goes HBM -> LDS by LDS-DMA
-  // (buffer_load ... lds: 1 KB per wave-instruction = one utterance's 4 gates x 64 units, no
-  // registers); the saved activations go LDS -> registers -> 16-byte stores.
+  // ---- io role (waves 4-7).  G is fp16 in the wide path.  The input projection of a step goes
+  // HBM -> LDS by LDS-DMA (buffer_load ... lds: one utterance's 4 gates x HJ units = 8 HJ bytes
+  // per wave-instruction, no registers); the saved activations go LDS -> registers -> 16-byte
+  // stores: gates (fp16), c (fp32), h (bf16 GEMM operand), the next layer's dropout(h) (bf16,
+  // Philox mask: replaces a separate dropout pass) and -- only when asked -- h in fp32.
   const int iot = tid - 256;
   const bool io = wave >= 4;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
   auto io_load = [&](int s_) {  // input projection of step s_ into gx ring slot s_ & 1
     if (s_ >= T || (s_ > 0 && (a.dbg_mode & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
@@ -124,145 +132,196 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
     for (int i = 0; i < UPW; ++i) {
       const int u = (wave - 4) * UPW + i, b = grp * BG + u;
       if (b >= a.B) continue;
-      // lane l < HJ -> gate l / (HJ/4), units 4 (l % (HJ/4)) .. + 3: 4 gates x HJ units in one
-      // instruction (HJ = 64: all lanes; HJ = 32: lanes 0-31)
-      const float* base = a.G + (size_t)b * T * 8 * H;
-      const auto rs = make_rsrc(base, (unsigned)((size_t)T * 8 * H * sizeof(float)));
-      const int g = lane / (HJ / 4), uu = (lane % (HJ / 4)) * 4;
-      const unsigned off = (unsigned)((((size_t)t_ * 8 * H + dir * 4 * H + g * H + j0 + uu)) * sizeof(float));
-      float* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
-      if (lane < HJ) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, 0);
+      // lane l < HJ/2 -> gate l / (HJ/8), units 8 (l % (HJ/8)) .. + 7
+      const auto rs = make_rsrc(G16 + (size_t)b * T * 8 * H, (unsigned)((size_t)T * 8 * H * 2));
+      const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
+      const unsigned off = (unsigned)(((size_t)t_ * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
+      unsigned short* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
+      if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, 0);
     }
+  };
+  // Philox keep bits (bit e = element e) of h chunk c8 (8 units) at step s_: one call per 4
+  // aligned elements, as dropout_scale in common.h
+  auto drop_bits = [&](int s_, int c8) -> unsigned {
+    const int u = c8 / (HJ / 8), uu = (c8 % (HJ / 8)) * 8;
+    const int t_ = dir ? T - 1 - s_ : s_;
+    const size_t o = ((size_t)(grp * BG + u) * T + t_) * 2 * H + dir * H + j0 + uu;
+    unsigned w0[4], w1[4];
+    philox4(a.dseed, (a.doff + o) >> 2, w0);
+    philox4(a.dseed, (a.doff + o + 4) >> 2, w1);
+    unsigned bits = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bits |= (dropout_word_scale(w0[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
+      bits |= (dropout_word_scale(w1[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
+    }
+    return bits;
   };
   auto io_store = [&](int s_) {  // saved activations of step s_ from out ring slot s_ & 1
     if (s_ < 0 || s_ >= T || (a.dbg_mode & 1)) return;
     const int t_ = dir ? T - 1 - s_ : s_;
-    const float* src = outr + (s_ & 1) * 16 * OUU;
-    // activated gates: NQ quads
-#pragma unroll
-    for (int i = 0; i < QPT; ++i) {
-      const int qi = iot + 256 * i, row = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4;
+    const char* src = outr + (s_ & 1) * 16 * OUB;
+    // activated gates (fp16 in the ring already): 16 utt x 4 gates x HJ/8 chunks, LDS -> HBM
+    constexpr int NG8 = 16 * 4 * HJ / 8;
+    for (int ci = iot; ci < NG8; ci += 256) {
+      const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
       const int u = row >> 2, g = row & 3, b = grp * BG + u;
-      if (b < a.B)
-        *reinterpret_cast<f32x4*>(a.G + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
-            *reinterpret_cast<const f32x4*>(src + u * OUU + g * HJ + uu);
+      if (b >= a.B) continue;
+      *reinterpret_cast<u32x4*>(G16 + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
+          *reinterpret_cast<const u32x4*>(src + u * OUB + (g * HJ + uu) * 2);
     }
-    // c, h (fp32) and h (bf16): 16 x HJ each
+    // c (fp32) and, when asked, h (fp32): 16 x HJ/4 quads
     constexpr int NQ2 = 16 * HJ / 4;
     for (int qi = iot; qi < NQ2; qi += 256) {
       const int u = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4, b = grp * BG + u;
       if (b >= a.B) continue;
       const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
-      const f32x4 cv = *reinterpret_cast<const f32x4*>(src + u * OUU + 4 * HJ + uu);
-      const f32x4 hv = *reinterpret_cast<const f32x4*>(src + u * OUU + 5 * HJ + uu);
-      *reinterpret_cast<f32x4*>(a.Cs + o) = cv;
-      *reinterpret_cast<f32x4*>(a.Y + o) = hv;
-      if (a.Yb)
-        *reinterpret_cast<bf16x4*>(a.Yb + o) = bf16x4{f2bf(hv[0]), f2bf(hv[1]), f2bf(hv[2]), f2bf(hv[3])};
+      const float* cf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ);
+      *reinterpret_cast<f32x4*>(a.Cs + o) = *reinterpret_cast<const f32x4*>(cf + uu);
+      if (a.Y) *reinterpret_cast<f32x4*>(a.Y + o) = *reinterpret_cast<const f32x4*>(cf + HJ + uu);
+    }
+    // h (bf16) by io threads [0, NC8), dropout(h) (bf16) by the next NC8: chunks of 8 units
+    static_assert(2 * NC8 <= 256, "one h chunk per io thread");
+    const bool drop8 = iot >= NC8;
+    const int ci8 = drop8 ? iot - NC8 : iot;
+    if (ci8 < NC8 && (drop8 ? a.Ydb != nullptr : a.Yb != nullptr)) {
+      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8, b = grp * BG + u;
+      if (b < a.B) {
+        const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
+        f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
+        f32x4 v1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
+        const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
+        if (drop8) {  // keep bits drawn by the pollers at the end of step s_
+          const unsigned bits = dbl[(s_ & 1) * NC8 + ci8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v0[e] = (bits >> e) & 1 ? v0[e] * a.dscale : 0.f;
+            v1[e] = (bits >> (4 + e)) & 1 ? v1[e] * a.dscale : 0.f;
+          }
+        }
+        *reinterpret_cast<bf16x8*>((drop8 ? a.Ydb : a.Yb) + o) =
+            bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
+                   f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+      }
     }
   };
-  if (io) {
-    io_load(0);
-    io_load(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-
-  float c[TPW];
+  // The step loop, instantiated once per role (IO: waves 4-7 move the step's HBM traffic;
+  // else waves 0-3 poll the hand-off): each instance keeps only its own role's state live,
+  // and both pass the same barriers.
+  auto run = [&](auto io_tag) {
+    constexpr bool IO = decltype(io_tag)::value;
+    if (IO) {
+      io_load(0);
+      io_load(1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    float c[TPW];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) c[t] = 0.f;
-  for (int s = 0; s < T; ++s) {
-    STAMP(0);
-    f32x4 acc[TPW];
+    for (int t = 0; t < TPW; ++t) c[t] = 0.f;
+    for (int s = 0; s < T; ++s) {
+      STAMP(0);
+      f32x4 acc[TPW];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    char* hb = himg + (s & 1) * HIMG;
-    if (s > 0) {
-      if (io) {
-        if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
-      } else {
-        // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
-        // granule carries step s-1's tag; then into the swizzled LDS image
-        const unsigned tag = step_tag(s - 1);
-        const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * H + wave * PL * 32 + 8 * q;
-        u32x4 hv[PL];
-        unsigned spins = 0;
-        while (true) {
+      for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      char* hb = himg + (s & 1) * HIMG;
+      if (s > 0) {
+        if (IO) {
+          if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
+        } else {
+          // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
+          // granule carries step s-1's tag; then into the swizzled LDS image
+          const unsigned tag = step_tag(s - 1);
+          const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * H + wave * PL * 32 + 8 * q;
+          u32x4 hv[PL];
+          unsigned spins = 0;
+          while (true) {
 #pragma unroll
-          for (int i = 0; i < PL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
-          bool ok = true;
+            for (int i = 0; i < PL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
+            bool ok = true;
 #pragma unroll
-          for (int i = 0; i < PL; ++i) ok &= tags_ok(hv[i], tag, true, true);
-          if (__all(ok)) break;
-          if (++spins > SPIN_LIMIT) {
-            if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
-            break;
+            for (int i = 0; i < PL; ++i) ok &= tags_ok(hv[i], tag, true, true);
+            if (__all(ok)) break;
+            if (++spins > SPIN_LIMIT) {
+              if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
           }
-          __builtin_amdgcn_s_sleep(2);
+          STAMP(1);
+#pragma unroll
+          for (int i = 0; i < PL; ++i)
+            *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
         }
-        STAMP(1);
+        __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
+        STAMP(2);
+        if (abort_flag) break;
+        // gx of step s+1 right behind the barrier (it lands before barrier s+1)
+        if (IO) io_load(s + 1);
 #pragma unroll
-        for (int i = 0; i < PL; ++i)
-          *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
-      }
-      __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
-      STAMP(2);
-      if (abort_flag) break;
-      if (io) {
-        // the step's HBM traffic right behind the barrier, while the pollers run MFMAs: it
-        // drains before their next poll (issued behind the publish it delayed the hand-off:
-        // 4.3 vs 3.x us/step at B = 256).  gx of step s+1 lands before barrier s+1.
-        io_load(s + 1);
-        io_store(s - 1);
-      }
+        for (int kc = 0; kc < NKC; ++kc) {
+          const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
 #pragma unroll
-      for (int kc = 0; kc < NKC; ++kc) {
-        const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
-                                    : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag, acc[t], 0, 0, 0);
+          for (int t = 0; t < TPW; ++t) {
+            const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
+                                      : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag, acc[t], 0, 0, 0);
+          }
         }
+        STAMP(3);
       }
-      STAMP(3);
-    }
-    // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
-    const float* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
-    float* ob = outr + (s & 1) * 16 * OUU + bi * OUU;
-    float hvals[TPW];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const int u = 4 * (wave * TPW + t) + q;
-      const float ig = sigmoid_fast(acc[t][0] + gx[u]);
-      const float fg = sigmoid_fast(acc[t][1] + gx[HJ + u]);
-      const float gg = tanh_fast(acc[t][2] + gx[2 * HJ + u]);
-      const float og = sigmoid_fast(acc[t][3] + gx[3 * HJ + u]);
-      c[t] = valid ? fg * c[t] + ig * gg : 0.f;
-      const float h = valid ? og * tanh_fast(c[t]) : 0.f;
-      hvals[t] = h;
-      ob[u] = ig; ob[HJ + u] = fg; ob[2 * HJ + u] = gg; ob[3 * HJ + u] = og;
-      ob[4 * HJ + u] = c[t]; ob[5 * HJ + u] = h;
-    }
-    if (s + 1 < T) {
-      // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
-      const unsigned tag = step_tag(s);
-      const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * H + j0;
+      // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
+      const unsigned short* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
+      char* ob = outr + (s & 1) * 16 * OUB + bi * OUB;
+      float hvals[TPW], gates[TPW][4];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
-        const float h1 = __shfl(hvals[t], lane + 16, 64);
-        const float h2 = __shfl(hvals[t], lane + 32, 64);
-        const float h3 = __shfl(hvals[t], lane + 48, 64);
-        if (q == 0)
-          publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)),
-                  pack_bf16(hvals[t], h1, h2, h3, tag), same_xcd);
+        const int u = 4 * (wave * TPW + t) + q;
+        const float ig = sigmoid_fast(acc[t][0] + h2f(gx[u]));
+        const float fg = sigmoid_fast(acc[t][1] + h2f(gx[HJ + u]));
+        const float gg = tanh_fast(acc[t][2] + h2f(gx[2 * HJ + u]));
+        const float og = sigmoid_fast(acc[t][3] + h2f(gx[3 * HJ + u]));
+        c[t] = valid ? fg * c[t] + ig * gg : 0.f;
+        hvals[t] = valid ? og * tanh_fast(c[t]) : 0.f;
+        gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
       }
+      if (s + 1 < T) {
+        // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
+        const unsigned tag = step_tag(s);
+        const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * H + j0;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const float h1 = __shfl(hvals[t], lane + 16, 64);
+          const float h2 = __shfl(hvals[t], lane + 32, 64);
+          const float h3 = __shfl(hvals[t], lane + 48, 64);
+          if (q == 0)
+            publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)),
+                    pack_bf16(hvals[t], h1, h2, h3, tag), same_xcd);
+        }
+      }
+      STAMP(4);
+      // Behind the publish, off the hand-off's path: the io waves store step s-1's saved
+      // activations (right after the barrier they delayed the io waves' own publish: 4.2 vs
+      // 3.7 us/step at B = 256); every wave puts step s's into the out ring (gates as fp16);
+      // the pollers draw step s's dropout bits before polling for step s+1.
+      if (IO && s > 0) io_store(s - 1);
+      unsigned short* og = reinterpret_cast<unsigned short*>(ob);
+      float* of = reinterpret_cast<float*>(ob + 8 * HJ);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int u = 4 * (wave * TPW + t) + q;
+        og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
+        og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
+        of[u] = c[t]; of[HJ + u] = hvals[t];
+      }
+      if (!IO && a.Ydb && tid < NC8) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
     }
-    STAMP(4);
-  }
-  __syncthreads();
-  if (io) io_store(T - 1);
+    __syncthreads();
+    if (IO) io_store(T - 1);
+  };
+  if (io) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------------------
@@ -285,13 +344,19 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* aimg = smem;  // [2][16][4HJ] bf16 own dG, gate-major k = g*HJ + u, swizzled slots
   bf16x8* wlds = reinterpret_cast<bf16x8*>(smem + 2 * AIMG);  // [wave][NTW][KLB][lane]
+  // cell inputs of a step, staged: [2][16 utt][ gates fp16 4*HJ (+16 B) | c_{t-1} HJ | dy HJ (fp32, +32 B) ]
+  constexpr int CG_B = 4 * HJ * 2 + 16;       // gate row bytes (padded: 8 utterances -> 32 banks)
+  constexpr int CF_B = HJ * 4 + 32;           // c / dy row bytes (padded likewise)
+  constexpr int CUTT = CG_B + 2 * CF_B;       // bytes per utterance
+  char* cst = smem + 2 * AIMG + (size_t)8 * NTW * KLB * 64 * 16;  // [2][16][CUTT]
   __shared__ int abort_flag;
 
   const int ngroups = 2 * a.NB;
   const int gid = blockIdx.x % ngroups, js = blockIdx.x / ngroups;
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int T = a.T, j0 = js * HJ;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
 
@@ -336,30 +401,56 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
     cu[ci] = (cb & 1) * 8 + pg;
     bv[ci] = grp * BG + cu[ci] < a.B;
   }
-  struct CellIn { float gi, gf, gg, go, cp, dy; };
-  // cell inputs through buffer loads: one 32-bit offset per cell (the group's rows are within
-  // 4 GB of its base), the four gates at scalar offsets 0, H, 2H, 3H
+  // Cell inputs (gates, c_{t-1}, dy) of step s_ in 16-byte row chunks -- whole 128-byte lines
+  // per wave instruction instead of each lane's scattered words -- into registers, two steps
+  // ahead; staged to LDS one step ahead (cst slot s_ & 1).  Chunks: 16 x 4 x HJ/8 gate chunks
+  // (8 fp16 units), 16 x HJ/4 c chunks, 16 x HJ/4 dy chunks (4 fp32 units).
+  constexpr int NGC = 16 * 4 * HJ / 8, NFC = 16 * HJ / 4, NCH = NGC + 2 * NFC;
+  constexpr int CPT = (NCH + 511) / 512;      // chunks per thread
   const size_t gbase = (size_t)grp * BG * T;  // first row (utterance grp*16, t = 0) of the group
-  const auto rG = make_rsrc(a.G + gbase * 8 * H, 0xffffffffu);
+  const auto rG = make_rsrc(reinterpret_cast<const unsigned short*>(a.G) + gbase * 8 * H, 0xffffffffu);
   const auto rC = make_rsrc(a.Cs + gbase * 2 * H, 0xffffffffu);
   const auto rY = make_rsrc(a.Y + gbase * 2 * H, 0xffffffffu);
-  auto load_cell = [&](int s_, CellIn (&c)[CPG]) {
+  u32x4 creg[CPT];
+  auto chunk_lds = [&](int c) -> int {  // LDS byte offset of chunk c within a slot
+    if (c < NGC) {
+      const int u = c / (4 * HJ / 8), k = c % (4 * HJ / 8);
+      return u * CUTT + k * 16;
+    }
+    const int f = c - NGC, which = f / NFC, r = f % NFC;
+    const int u = r / (HJ / 4), k = r % (HJ / 4);
+    return u * CUTT + CG_B + which * CF_B + k * 16;
+  };
+  auto load_cell = [&](int s_) {
     if (s_ >= T || (s_ > 1 && (a.dbg_mode & 2048))) return;  // bit 11: timing without the loads
     const int t_ = dir ? s_ : T - 1 - s_;
     const int tp_ = dir ? t_ + 1 : t_ - 1;
     const int tpc = tp_ < 0 ? 0 : (tp_ >= T ? T - 1 : tp_);
 #pragma unroll
-    for (int ci = 0; ci < CPG; ++ci) {
-      if (!bv[ci]) continue;
-      const unsigned r = (unsigned)(cu[ci] * T + t_), rp = (unsigned)(cu[ci] * T + tpc);
-      const unsigned og = (r * 8 * H + dir * 4 * H + j0 + uc[ci]) * 4u;
-      c[ci].gi = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rG, og, 0, 0));
-      c[ci].gf = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rG, og, 4 * H, 0));
-      c[ci].gg = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rG, og, 8 * H, 0));
-      c[ci].go = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rG, og, 12 * H, 0));
-      const unsigned oc = (dir * H + j0 + uc[ci]) * 4u;
-      c[ci].cp = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rC, rp * 2 * H * 4 + oc, 0, 0));
-      c[ci].dy = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rY, r * 2 * H * 4 + oc, 0, 0));
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + 512 * i;
+      if (c >= NCH) continue;
+      if (c < NGC) {
+        const int u = c / (4 * HJ / 8), k = c % (4 * HJ / 8), g = k / (HJ / 8), uu = (k % (HJ / 8)) * 8;
+        if (grp * BG + u >= a.B) continue;
+        const unsigned o = ((unsigned)(u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2u;
+        creg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rG, o, 0, 0));
+      } else {
+        const int f = c - NGC, which = f / NFC, r = f % NFC;
+        const int u = r / (HJ / 4), uu = (r % (HJ / 4)) * 4;
+        if (grp * BG + u >= a.B) continue;
+        const unsigned o = ((unsigned)(u * T + (which ? t_ : tpc)) * 2 * H + dir * H + j0 + uu) * 4u;
+        creg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(which ? rY : rC, o, 0, 0));
+      }
+    }
+  };
+  auto stage_cell = [&](int s_) {  // registers -> LDS slot s_ & 1 (visible after the next barrier)
+    if (s_ >= T) return;
+    char* dst = cst + (s_ & 1) * 16 * CUTT;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + 512 * i;
+      if (c < NCH) *reinterpret_cast<u32x4*>(dst + chunk_lds(c)) = creg[i];
     }
   };
   float dc[CPG], cc[CPG];
@@ -372,19 +463,33 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
       cc[ci] = a.Cs[((size_t)(grp * BG + cu[ci]) * T + t0) * 2 * H + dir * H + j0 + uc[ci]];
     }
   }
-  CellIn cin[2][CPG];
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int ci = 0; ci < CPG; ++ci) cin[r][ci] = CellIn{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  load_cell(0, cin[0]);
+  for (int i = 0; i < CPT; ++i) creg[i] = u32x4{0u, 0u, 0u, 0u};
+  load_cell(0);
+  stage_cell(0);   // (waits for the loads: prologue only)
+  load_cell(1);
+  __syncthreads();
 
-  auto step = [&](int s, CellIn (&cur)[CPG], CellIn (&fill)[CPG]) -> bool {
+  auto step = [&](int s) -> bool {
     STAMP(0);
+    // this step's cell inputs (staged in LDS last step) into registers before the poll, so
+    // the LDS latency hides behind the hand-off wait
+    float xi[CPG], xf[CPG], xgg[CPG], xo[CPG], xcp[CPG], xdy[CPG];
+#pragma unroll
+    for (int ci = 0; ci < CPG; ++ci) {
+      const char* cu_row = cst + (s & 1) * 16 * CUTT + cu[ci] * CUTT;
+      const unsigned short* xg = reinterpret_cast<const unsigned short*>(cu_row) + uc[ci];
+      xi[ci] = h2f(xg[0]); xf[ci] = h2f(xg[HJ]); xgg[ci] = h2f(xg[2 * HJ]); xo[ci] = h2f(xg[3 * HJ]);
+      xcp[ci] = reinterpret_cast<const float*>(cu_row + CG_B)[uc[ci]];
+      xdy[ci] = reinterpret_cast<const float*>(cu_row + CG_B + CF_B)[uc[ci]];
+    }
     float dh[CPG];
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) dh[ci] = 0.f;
-    if (s == 0) load_cell(1, fill);
+    if (s == 0) {  // step 1's inputs to LDS, step 2's loads issued
+      stage_cell(1);
+      load_cell(2);
+    }
     if (s > 0) {
       const unsigned tag = step_tag(s - 1);
       const size_t sb = (size_t)((s - 1) & (NSLOT - 1)) * xslot + (size_t)js * NJ * HJ * 16;
@@ -412,7 +517,10 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
         __builtin_amdgcn_s_sleep(2);
       }
       STAMP(1);
-      load_cell(s + 1, fill);  // next step's cell inputs, right behind this step's hand-off
+      // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
+      // s+2's loads issued right behind this step's hand-off
+      stage_cell(s + 1);
+      load_cell(s + 2);
       const bool b2 = pg & 4, b1 = pg & 2, b0 = pg & 1;
 #pragma unroll
       for (int ci = 0; ci < CPG; ++ci) {
@@ -450,20 +558,19 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) {
       float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
-      const CellIn& x = cur[ci];
-      const float cpv = s + 1 < T ? x.cp : 0.f;  // c_{t-1}; none at the sequence start
+      const float cpv = s + 1 < T ? xcp[ci] : 0.f;  // c_{t-1}; none at the sequence start
       if (bv[ci]) {
-        const float dht = x.dy + dh[ci];
+        const float dht = xdy[ci] + dh[ci];
         const float tc = tanh_fast(cc[ci]);
         const float d_o = dht * tc;
-        const float dcs = dc[ci] + dht * x.go * (1.f - tc * tc);
-        dc[ci] = dcs * x.gf;
-        d0 = dcs * x.gg * x.gi * (1.f - x.gi);
-        d1 = dcs * cpv * x.gf * (1.f - x.gf);
-        d2 = dcs * x.gi * (1.f - x.gg * x.gg);
-        d3 = d_o * x.go * (1.f - x.go);
+        const float dcs = dc[ci] + dht * xo[ci] * (1.f - tc * tc);
+        dc[ci] = dcs * xf[ci];
+        d0 = dcs * xgg[ci] * xi[ci] * (1.f - xi[ci]);
+        d1 = dcs * cpv * xf[ci] * (1.f - xf[ci]);
+        d2 = dcs * xi[ci] * (1.f - xgg[ci] * xgg[ci]);
+        d3 = d_o * xo[ci] * (1.f - xo[ci]);
       }
-      cc[ci] = x.cp;  // c_{t-1} is the next step's c_t
+      cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
       const int u = uc[ci], r = cu[ci];
       const float dg[4] = {d0, d1, d2, d3};
 #pragma unroll
@@ -513,24 +620,13 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
         const int k = kslot * 8, g = k / HJ, u = k % HJ;
         const u32x4 v = *reinterpret_cast<const u32x4*>(ab + r * ROWB + swz(r, kslot) * 16);
         const size_t o = ((size_t)b * T + t) * 8 * H + dir * 4 * H + g * H + j0 + u;
-        if (a.dGb) {
-          *reinterpret_cast<u32x4*>(a.dGb + o) = v;
-        } else {
-          float* gp = a.G + o;
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            gp[2 * d] = __uint_as_float(v[d] << 16);
-            gp[2 * d + 1] = __uint_as_float(v[d] & 0xffff0000u);
-          }
-        }
+        *reinterpret_cast<u32x4*>(a.dGb + o) = v;  // G is fp16 here: dG always goes to dGb
       }
     }
     return true;
   };
-  for (int s = 0; s < T; s += 2) {
-    if (!step(s, cin[0], cin[1])) break;
-    if (s + 1 < T && !step(s + 1, cin[1], cin[0])) break;
-  }
+  for (int s = 0; s < T; ++s)
+    if (!step(s)) break;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -568,12 +664,15 @@ WidePlan wide_plan(int B, int H, bool fwd) {
   }
   if (!p.ok) return p;
   if (fwd) {
-    p.lds = (size_t)2 * 16 * H * 2 + (size_t)2 * 16 * (4 * p.HJ + 4) * 4 + (size_t)2 * 16 * (6 * p.HJ + 4) * 4 +
-            (size_t)8 * p.tpw * 2 * 64 * 16;  // + the LDS-resident A-fragments (KLF = 2)
+    p.lds = (size_t)2 * 16 * H * 2 + (size_t)2 * 16 * (4 * p.HJ + 8) * 2 +  // h image, gx ring
+            (size_t)2 * 16 * (4 * p.HJ * 2 + 2 * p.HJ * 4 + 16) +              // out ring
+            (size_t)8 * p.tpw * 2 * 64 * 16 +  // + the LDS-resident A-fragments (KLF = 2)
+            (size_t)2 * (16 * p.HJ / 8) * 4;   // + dropout keep bits
     p.xbytes = (size_t)2 * p.NB * NSLOT * BG * H * 2;
   } else {
     p.lds = (size_t)2 * 16 * 4 * p.HJ * 2 +
-            (size_t)8 * (H / 128) * (p.HJ / 32) * 64 * 16;  // + LDS-resident B-fragments (KLB = KC/4)
+            (size_t)8 * (H / 128) * (p.HJ / 32) * 64 * 16 +  // + LDS-resident B-fragments (KLB = KC/4)
+            (size_t)2 * 16 * ((4 * p.HJ * 2 + 16) + 2 * (p.HJ * 4 + 32));  // + staged cell inputs
     p.xbytes = (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * p.HJ * 16 * 2;
   }
   if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;  // one recurrence workgroup per CU
@@ -608,7 +707,9 @@ size_t lstm_wide_xbytes(int B, int H, bool fwd) {
 
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
-                  unsigned short* yb, unsigned short* dgb, unsigned long long* dbg, int dbg_mode) {
+                  unsigned short* yb, unsigned short* dgb, unsigned short* ydb,
+                  unsigned long long dseed, unsigned long long doff, float dp,
+                  unsigned long long* dbg, int dbg_mode) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return -1;
   if (!xbuf || xbytes < p.xbytes || !err) {
@@ -619,6 +720,8 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.B = B; a.T = T; a.H = H; a.NB = p.NB; a.NJ = p.NJ; a.HJ = p.HJ; a.Kp = H; a.K4p = 4 * H;
   a.W0 = W0; a.W1 = W1; a.G = G; a.Cs = Cs; a.Y = Y; a.xbuf = xbuf; a.err = err;
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;
+  a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
+  a.dscale = dp < 1.f ? 1.f / (1.f - dp) : 0.f;
   a.xtab = reinterpret_cast<unsigned*>(static_cast<char*>(xbuf) + p.xtab_off);
   // zero fill = a stale tag in every granule (and an empty placement table)
   if (hipMemsetAsync(xbuf, 0, p.xbytes, st) != hipSuccess) {

@@ -211,12 +211,13 @@ __global__ __launch_bounds__(256) void skinny_reduce(int M, int NB, int S, int n
 
 constexpr int PROJ_CN = 512;  // output columns per workgroup (64 rows x 512 cols)
 
+template <bool F16>  // C stored as fp16 (the wide-batch recurrence's gate buffer) or fp32
 __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
                                                           const unsigned short* __restrict__ A, int lda,
                                                           const unsigned short* __restrict__ B, int ldb,
                                                           const float* __restrict__ b1,
                                                           const float* __restrict__ b2,
-                                                          float* __restrict__ C, int ldc) {
+                                                          void* __restrict__ C, int ldc) {
   constexpr int LS = 64 + 4;  // staging row stride (floats)
   __shared__ __attribute__((aligned(16))) float stg[4][16 * LS];  // per wave: 16 rows x 64 cols
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -250,7 +251,11 @@ __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
       for (int q = 0; q < 4; ++q) {
         const int r = 4 * q + (lane >> 4);
         const f32x4 v = *reinterpret_cast<const f32x4*>(sw + r * LS + 4 * (lane & 15));
-        if (r0 + r < M) *reinterpret_cast<f32x4*>(C + (size_t)(r0 + r) * ldc + col) = v + bias;
+        if (r0 + r >= M) continue;
+        if constexpr (F16)
+          *reinterpret_cast<u32x2*>(static_cast<unsigned short*>(C) + (size_t)(r0 + r) * ldc + col) = f2h4(v + bias);
+        else
+          *reinterpret_cast<f32x4*>(static_cast<float*>(C) + (size_t)(r0 + r) * ldc + col) = v + bias;
       }
     }
     __syncthreads();  // the staging tile is rewritten by the next chunk
@@ -300,9 +305,9 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
   return 0;
 }
 
-extern "C" int mlvae_skinny_proj(int M, int N, int K, const void* A, int lda, const void* B,
-                                 int ldb, const float* bias1, const float* bias2, float* C, int ldc,
-                                 void* stream) {
+extern "C" int mlvae_skinny_proj_ex(int M, int N, int K, const void* A, int lda, const void* B,
+                                    int ldb, const float* bias1, const float* bias2, void* C,
+                                    int ldc, int c_fp16, void* stream) {
   if (M <= 0 || N <= 0) return 0;
   if (!A || !B || !C || K < 8 || K > 32 || K % 8 || N % 16 || lda % 8 || ldb % 8 || ldc % 4 ||
       ((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16) ||
@@ -311,11 +316,18 @@ extern "C" int mlvae_skinny_proj(int M, int N, int K, const void* A, int lda, co
     return 1;
   }
   dim3 grid((M + 63) / 64, (N + PROJ_CN - 1) / PROJ_CN);
-  skinny_proj_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(
+  auto k = c_fp16 ? skinny_proj_kernel<true> : skinny_proj_kernel<false>;
+  k<<<grid, 256, 0, (hipStream_t)stream>>>(
       M, N, K, static_cast<const unsigned short*>(A), lda, static_cast<const unsigned short*>(B),
       ldb, bias1, bias2, C, ldc);
   MLVAE_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int mlvae_skinny_proj(int M, int N, int K, const void* A, int lda, const void* B,
+                                 int ldb, const float* bias1, const float* bias2, float* C, int ldc,
+                                 void* stream) {
+  return mlvae_skinny_proj_ex(M, N, K, A, lda, B, ldb, bias1, bias2, C, ldc, 0, stream);
 }
 
 extern "C" size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K) {

@@ -38,12 +38,16 @@ _SIGS = {
     "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_fwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_lstm_gates_fp16": [I, I, I],
+    "mlvae_lstm_fwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, U64, U64, F, P, SZ, P, P],
+    "mlvae_lstm_bwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, SZ, P, P],
     "mlvae_elbo_partials_count": [I, I, I],
     "mlvae_heads_partials_count": [I, I],
     "mlvae_heads_supported": [I, I, I],
     "mlvae_heads_fused": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
                           P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mlvae_skinny_proj": [I, I, I, P, I, P, I, P, P, P, I, P],
+    "mlvae_skinny_proj_ex": [I, I, I, P, I, P, I, P, P, P, I, I, P],
     "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],
     "mlvae_skinny_tn_workspace_size": [I, I, I],
     "mlvae_skinny_tn": [I, I, I, P, I, P, I, I, P, P, P, P, SZ, P],

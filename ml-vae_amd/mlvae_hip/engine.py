@@ -30,6 +30,7 @@ from ._lib import check, lib
 PREC = {"fp32": 0, "bf16": 1}
 LOSS = {"likelihood": 0, "mse": 1}
 EPI_NONE, EPI_LRELU, EPI_DLRELU, EPI_DROPOUT = 0, 1, 2, 3
+EPI_OUT_F16 = 16  # flag: mlvae_gemm_bf16 stores C as fp16
 
 
 @dataclass
@@ -183,7 +184,10 @@ class _Work:
         self.ML = empty(N, 2 * Z, **f)
         self.Zs = empty(N, Z, **f)
         self.eps = empty(N, Z, **f)
-        self.G = [empty(N, 8 * H, **f) for _ in range(L)]
+        # gate buffer [N, 8H]: fp32, or fp16 where the recurrence runs the wide-batch kernels
+        # (halves the projection's write and the recurrences' reads; include/mlvae.h)
+        self.g16 = bool(lib().mlvae_lstm_gates_fp16(B, H, PREC[cfg.prec]))
+        self.G = [empty(N, 8 * H, dtype=torch.float16 if self.g16 else torch.float32) for _ in range(L)]
         self.Cs = [empty(N, 2 * H, **f) for _ in range(L)]
         self.Y = [empty(N, 2 * H, **f) for _ in range(L)]
         self.Yd = [empty(N, 2 * H, **f) if cfg.dropout > 0 else None for _ in range(L - 1)]
@@ -326,6 +330,8 @@ class VAEEngine:
         self.split_tail = int(os.environ.get("MLVAE_SPLIT_TAIL", "160"))
         # layer-0 input projection (K = latent width) on skinny_proj instead of the 256² GEMM
         self.skinny_proj = os.environ.get("MLVAE_PROJ0", "skinny") == "skinny"
+        # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
+        self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
         self.side_stream = torch.cuda.Stream(self.device)
         # the step's critical path (recurrences, dgrads) runs on a high-priority stream so the
         # dispatcher prefers its workgroups over the side stream's weight-gradient GEMMs
@@ -464,10 +470,14 @@ class VAEEngine:
         return False
 
     def _fast(self, w, ta, tb, M, N, K, A_bf, lda, B_bf, ldb, C, ldc, batch=1, a_bs=0, b_bs=0,
-              c_bs=0, bias1=None, bias2=None, kshift_T=0, kshift=0, kstep=0, drop_seed=None):
-        """bf16 256² LDS-DMA GEMM (mlvae_gemm_bf16) over bf16 operands: the step's big products."""
+              c_bs=0, bias1=None, bias2=None, kshift_T=0, kshift=0, kstep=0, drop_seed=None,
+              out_f16=False):
+        """bf16 256² LDS-DMA GEMM (mlvae_gemm_bf16) over bf16 operands: the step's big products.
+        out_f16: C is fp16 (the wide recurrence's gate buffer)."""
         ws = w.gws_side if self._on_side else w.gws
         epi, p = (EPI_DROPOUT, self.cfg.dropout) if drop_seed is not None else (EPI_NONE, 0.0)
+        if out_f16:
+            epi |= EPI_OUT_F16
         check(lib().mlvae_gemm_bf16(ta, tb, M, N, K, batch, A_bf, lda, a_bs, B_bf, ldb, b_bs, C, ldc,
                                     c_bs, 0.0, bias1, bias2, epi, None, 0, kshift_T, kshift, kstep,
                                     drop_seed or 0, self._drop_off, p, _p(ws), w.gws_bytes,
@@ -609,32 +619,47 @@ class VAEEngine:
             w.layer_in.append((xin, xin_bf, din, ldx))
             if w.bf and din <= 32 and din % 8 == 0 and self.skinny_proj:
                 # K = latent width: the write-bound skinny projection kernel (skinny.hip)
-                check(l.mlvae_skinny_proj(N, 8 * H, din, _pb(xin_bf), ldx,
-                                          wb(f"decoder.rnn.weight_ih_l{li}"), din,
-                                          self._ptr(f"decoder.rnn.bias_ih_l{li}"),
-                                          self._ptr(f"decoder.rnn.bias_hh_l{li}"), _p(w.G[li]), 8 * H,
-                                          s), "skinny_proj")
+                check(l.mlvae_skinny_proj_ex(N, 8 * H, din, _pb(xin_bf), ldx,
+                                             wb(f"decoder.rnn.weight_ih_l{li}"), din,
+                                             self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                                             self._ptr(f"decoder.rnn.bias_hh_l{li}"), _p(w.G[li]), 8 * H,
+                                             int(w.g16), s), "skinny_proj")
             elif w.bf and din % 8 == 0:  # input projection on the 256² GEMM
                 with self._timed(f"proj_l{li}"):
                     self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), ldx, wb(f"decoder.rnn.weight_ih_l{li}"),
                                din, _p(w.G[li]), 8 * H, bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
-                               bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+                               bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"), out_f16=w.g16)
             else:
+                if w.g16:
+                    raise RuntimeError("fp16 gate buffer needs a bf16 layer input with din % 8 == 0")
                 self._mm(w, 0, 1, N, 8 * H, din, _p(xin) if xin is not None else None, din,
                          self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(w.G[li]), 8 * H,
                          A_bf=_pb(xin_bf) if xin_bf is not None else None,
                          B_bf=wb(f"decoder.rnn.weight_ih_l{li}"),
                          bias1=self._ptr(f"decoder.rnn.bias_ih_l{li}"),
                          bias2=self._ptr(f"decoder.rnn.bias_hh_l{li}"))
+            drop = li < cfg.L - 1 and train and cfg.dropout > 0
+            # the wide kernels also write the next layer's dropout(h) (same Philox masks as
+            # mlvae_dropout_ex) and skip the fp32 h nothing reads
+            fuse_drop = w.g16 and drop and dropout_masks is None and self._fuse_drop
+            need_y = (not w.g16 or (drop and not fuse_drop) or
+                      (li == cfg.L - 1 and not (self.fused_heads and w.bf)))
+            seed = self._drop_seed(li) if fuse_drop else 0
             with self._timed("lstm_fwd"):
-                check(l.mlvae_lstm_fwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                          self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                          _p(w.Cs[li]), _p(w.Y[li]), _pb(w.Yb[li]) if w.bf else None,
-                                          _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd")
+                check(l.mlvae_lstm_fwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                           int(w.g16), _p(w.Cs[li]), _p(w.Y[li]) if need_y else None,
+                                           _pb(w.Yb[li]) if w.bf else None,
+                                           _pb(w.Ydb[li]) if fuse_drop else None, seed, self._drop_off,
+                                           cfg.dropout if fuse_drop else 0.0,
+                                           _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd")
             xin, xin_bf, din, ldx = w.Y[li], (w.Yb[li] if w.bf else None), 2 * H, 2 * H
-            if li < cfg.L - 1 and train and cfg.dropout > 0:
+            if drop:
                 xin, xin_bf = w.Yd[li], (w.Ydb[li] if w.bf else None)
-                self._dropout(w, li, w.Y[li], xin, dropout_masks)
+                if fuse_drop:
+                    w.__dict__.setdefault("_drop_seed", {})[li] = (seed, None)
+                else:
+                    self._dropout(w, li, w.Y[li], xin, dropout_masks)
         w.rnn_out = w.Y[cfg.L - 1]
         w.rnn_out_bf = w.Yb[cfg.L - 1] if w.bf else None
         # ---- heads (ref:src/modules/decoder.py:24-25, FCBlock ref:src/modules/fc_block.py:9-16)
@@ -697,13 +722,17 @@ class VAEEngine:
         the masks of the single-GPU run on the global batch."""
         return self.global_offset * self._T * 2 * self.cfg.H
 
+    def _drop_seed(self, li):
+        """Philox key of the dropout after layer li in this step."""
+        return (self.seed * 1000003 + self.rng_step * 131 + li) & ((1 << 63) - 1)
+
     def _dropout(self, w, li, src, dst, masks):
         mask_ptr = None
         if masks is not None:
             m = masks[li].to(self.device, torch.float32).contiguous()
             w.__dict__.setdefault("_masks", {})[li] = m
             mask_ptr = _p(m)
-        seed = (self.seed * 1000003 + self.rng_step * 131 + li) & ((1 << 63) - 1)
+        seed = self._drop_seed(li)
         dst_bf = w.Ydb[li] if w.bf else None
         check(lib().mlvae_dropout_ex(src.numel(), _p(src), _p(dst) if dst is not None else None,
                                      _pb(dst_bf) if dst_bf is not None else None, mask_ptr, seed,
@@ -785,10 +814,11 @@ class VAEEngine:
             Gl = w.G[li]
             dGb = w.dGb[li] if w.bf else None
             with self._timed("lstm_bwd"):
-                check(l.mlvae_lstm_bwd_ex(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                          self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                          _p(w.Cs[li]), _p(w.dY[li]), _pb(dGb) if dGb is not None else None,
-                                          _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
+                check(l.mlvae_lstm_bwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
+                                           int(w.g16), _p(w.Cs[li]), _p(w.dY[li]),
+                                           _pb(dGb) if dGb is not None else None,
+                                           _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
             self._flush_side(pending)
             # dG: fp32 in G (fp32 mode) or bf16 in dGb (bf16 mode)
             dG, dG_bf = (None, dGb) if dGb is not None else (Gl, None)

@@ -106,3 +106,29 @@ def test_dropout_epilogue_matches_dropout_kernel():
     check(l.mlvae_dropout(C0.numel(), P(C0), P(C0), None, seed, p, stream()))
     torch.cuda.synchronize()
     assert torch.equal(C0, C1)
+
+
+@pytest.mark.parametrize("K", [512, 8000])
+def test_fp16_output(K):
+    """EPI_OUT_F16 (the input projection into the wide recurrence's fp16 gate buffer): the fp32
+    result + biases rounded once to fp16, through the staged epilogue and the split-K reduce."""
+    need_gpu()
+    l = lib()
+    torch.manual_seed(K)
+    M, N = 600, 4096 if K == 512 else 256
+    A = torch.randn(M, K).to(torch.bfloat16).cuda()
+    B = torch.randn(N, K).to(torch.bfloat16).cuda()
+    b1, b2 = torch.randn(N, device="cuda"), torch.randn(N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    C16 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    ws = torch.empty(l.mlvae_gemm_bf16_workspace_size(M, N, K, 1) // 4 + 1, device="cuda")
+    for out, epi in ((C, 0), (C16, 16)):
+        check(l.mlvae_gemm_bf16(0, 1, M, N, K, 1, A.data_ptr(), K, 0, B.data_ptr(), K, 0, out.data_ptr(), N,
+                                0, 0.0, P(b1), P(b2), epi, None, 0, 0, 0, 0, 0, 0, 0.0, P(ws),
+                                ws.numel() * 4, stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(C16, C.to(torch.float16))
+    # fp16 C with an activation epilogue is refused
+    assert l.mlvae_gemm_bf16(0, 1, M, N, K, 1, A.data_ptr(), K, 0, B.data_ptr(), K, 0, C16.data_ptr(), N,
+                             0, 0.0, None, None, 16 | 1, None, 0, 0, 0, 0, 0, 0, 0.0, P(ws),
+                             ws.numel() * 4, stream()) != 0

@@ -1,14 +1,17 @@
 """Wide-batch BiLSTM recurrence (csrc/lstm_wide.hip) against an fp64 loop: forward h / c / saved
-gates and the BPTT's dG (fp32 and bf16 outputs) at batches past one batch-group launch (the
-metric's B = 256, B = 128, a ragged B = 200) and, forced through debug mode bit 12, at a small
-ragged batch.  Reference op: nn.LSTM bidirectional at ref:src/modules/decoder.py:14-15,22."""
+gates (fp16 gate buffer), the fused bf16 h and dropout(h) outputs, and the BPTT's bf16 dG, at
+batches past one batch-group launch (the metric's B = 256, B = 128, a ragged B = 200) and, forced
+through debug mode bit 12, at small ragged batches.  Reference op: nn.LSTM bidirectional at
+ref:src/modules/decoder.py:14-15,22; dropout between layers ref:src/modules/decoder.py:15."""
 import ctypes
 
+import numpy as np
 import pytest
 import torch
 
 from gpu_utils import P, need_gpu, norm_rel, rel_err, stream
 from mlvae_hip._lib import check, lib
+from philox_np import dropout_mask
 
 pytestmark = pytest.mark.gpu
 
@@ -51,41 +54,80 @@ def test_wide_recurrence_matches_fp64_loop(B, T, force):
     need_gpu()
     w, gx, y, cs, gates, dy, dG = _reference(B, T, B + T)
     N = B * T
-    G = gx.float().reshape(N, 8 * H).cuda().contiguous()
+    G = gx.reshape(N, 8 * H).to(torch.float16).cuda().contiguous()   # fp16 gate buffer
     Cs = torch.empty(N, 2 * H, device="cuda")
     Y = torch.empty(N, 2 * H, device="cuda")
     Yb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+    Ydb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
     W0, W1 = w[0].float().cuda(), w[1].float().cuda()
     xb = ctypes.c_size_t()
     check(lib().mlvae_lstm_workspace_size(B, H, 1, ctypes.byref(xb)))
     xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    seed, doff, p = 0x5EED + B, 4 * 2 * H, 0.15
     if force:
         lib().mlvae_lstm_set_debug_mode(4096)
     try:
-        check(lib().mlvae_lstm_fwd_ex(1, B, T, H, P(W0), P(W1), P(G), P(Cs), P(Y), Yb.data_ptr(),
-                                      P(xbuf), xb.value, P(err), stream()))
+        assert lib().mlvae_lstm_gates_fp16(B, H, 1) == 1
+        G0 = G.clone()
+        check(lib().mlvae_lstm_fwd_ex2(1, B, T, H, P(W0), P(W1), P(G), 1, P(Cs), P(Y), Yb.data_ptr(),
+                                       Ydb.data_ptr(), seed, doff, p, P(xbuf), xb.value, P(err), stream()))
         torch.cuda.synchronize()
         assert err.item() == 0
         assert rel_err(Y.view(B, T, 2 * H), y) < TOL_Y
         assert rel_err(Cs.view(B, T, 2 * H), cs) < TOL_Y
-        assert rel_err(G.view(B, T, 8 * H), gates) < TOL_Y
+        assert rel_err(G.float().view(B, T, 8 * H), gates) < TOL_Y
         assert torch.equal(Yb, Y.to(torch.bfloat16))
-        G2 = G.clone()
+        mask = torch.from_numpy(dropout_mask(seed, doff + N * 2 * H, p)[doff:]).cuda().view(N, 2 * H)
+        assert torch.equal(Ydb, (Y * mask).to(torch.bfloat16))
+        # the same launch without the fp32 h (the train step's form): identical bf16 outputs
+        G1, Yb1 = G0.clone(), torch.empty_like(Yb)
+        check(lib().mlvae_lstm_fwd_ex2(1, B, T, H, P(W0), P(W1), P(G1), 1, P(Cs), None, Yb1.data_ptr(),
+                                       None, 0, 0, 0.0, P(xbuf), xb.value, P(err), stream()))
+        torch.cuda.synchronize()
+        assert err.item() == 0 and torch.equal(Yb1, Yb) and torch.equal(G1, G)
         dGb = torch.empty(N, 8 * H, device="cuda", dtype=torch.bfloat16)
         dY = dy.float().reshape(N, 2 * H).cuda().contiguous()
-        # fp32 dG into G, then the bf16 dG copy (the train step's form) from the same inputs
-        check(lib().mlvae_lstm_bwd(1, B, T, H, P(W0), P(W1), P(G), P(Cs), P(dY), P(xbuf), xb.value,
-                                   P(err), stream()))
-        check(lib().mlvae_lstm_bwd_ex(1, B, T, H, P(W0), P(W1), P(G2), P(Cs), P(dY), dGb.data_ptr(),
-                                      P(xbuf), xb.value, P(err), stream()))
+        check(lib().mlvae_lstm_bwd_ex2(1, B, T, H, P(W0), P(W1), P(G), 1, P(Cs), P(dY), dGb.data_ptr(),
+                                       P(xbuf), xb.value, P(err), stream()))
         torch.cuda.synchronize()
         assert err.item() == 0
-        e1 = rel_err(G.view(B, T, 8 * H), dG)
-        e2 = norm_rel(G.view(B, T, 8 * H), dG)
+        e1 = rel_err(dGb.float().view(B, T, 8 * H), dG)
+        e2 = norm_rel(dGb.float().view(B, T, 8 * H), dG)
         print(f"\nB={B} T={T} force={force}: Y {rel_err(Y.view(B, T, 2 * H), y):.2e}  dG max-rel {e1:.2e} "
               f"norm-rel {e2:.2e}")
         assert e1 < TOL_DG and e2 < 2e-2
-        assert torch.equal(dGb.float(), G.to(torch.bfloat16).float())
     finally:
         lib().mlvae_lstm_set_debug_mode(0)
+
+
+def test_gate_buffer_format_is_checked():
+    """fp16 gates only where the wide kernels run; the wide backward needs the bf16 dG output."""
+    need_gpu()
+    l = lib()
+    assert l.mlvae_lstm_gates_fp16(256, H, 1) == 1
+    assert l.mlvae_lstm_gates_fp16(32, H, 1) == 0      # c2: one batch-group launch
+    assert l.mlvae_lstm_gates_fp16(256, H, 0) == 0     # fp32 parity mode
+    assert l.mlvae_lstm_gates_fp16(256, 128, 1) == 0   # wide kernels are built for H = 512
+    B, T = 32, 4
+    N = B * T
+    G = torch.zeros(N, 8 * H, device="cuda", dtype=torch.float16)
+    Cs = torch.empty(N, 2 * H, device="cuda")
+    Y = torch.empty(N, 2 * H, device="cuda")
+    xb = ctypes.c_size_t()
+    check(l.mlvae_lstm_workspace_size(256, H, 1, ctypes.byref(xb)))
+    xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    W = torch.zeros(4 * H, H, device="cuda")
+    assert l.mlvae_lstm_fwd_ex2(1, B, T, H, P(W), P(W), P(G), 1, P(Cs), P(Y), None, None, 0, 0, 0.0,
+                                P(xbuf), xb.value, P(err), stream()) != 0
+    assert b"fp16 gates" in l.mlvae_last_error()
+    B, N = 256, 256 * 4
+    G = torch.zeros(N, 8 * H, device="cuda", dtype=torch.float16)
+    Cs = torch.empty(N, 2 * H, device="cuda")
+    assert l.mlvae_lstm_bwd_ex2(1, B, T, H, P(W), P(W), P(G), 1, P(Cs), P(Cs), None,
+                                P(xbuf), xb.value, P(err), stream()) != 0
+    # the batch-group fallback skips neither output: Y = NULL is refused there
+    assert l.mlvae_lstm_fwd_ex2(1, 32, T, H, P(W), P(W), P(G), 0, P(Cs), None, None, None, 0, 0, 0.0,
+                                P(xbuf), xb.value, P(err), stream()) != 0
+    torch.cuda.synchronize()

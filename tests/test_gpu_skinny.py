@@ -74,8 +74,13 @@ def test_skinny_proj_matches_fp32_reference(M, N, K, lda):
     b1d, b2d = b1.cuda(), b2.cuda()  # held: a freed temporary's block would be reused
     check(l.mlvae_skinny_proj(M, N, K, Ad.data_ptr(), lda, Bd.data_ptr(), K, P(b1d), P(b2d), P(C),
                               N, stream()))
+    # fp16 output (the wide recurrence's gate buffer): the fp32 result rounded once
+    C16 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    check(l.mlvae_skinny_proj_ex(M, N, K, Ad.data_ptr(), lda, Bd.data_ptr(), K, P(b1d), P(b2d),
+                                 C16.data_ptr(), N, 1, stream()))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < 1e-5
+    assert torch.equal(C16, C.to(torch.float16))
     # bad shapes are refused, not launched
     assert l.mlvae_skinny_proj(M, N, 40, Ad.data_ptr(), lda, Bd.data_ptr(), 40, None, None, P(C),
                                N, stream()) != 0

@@ -1,4 +1,4 @@
-"""Time the train step's big GEMM shapes (c2, bf16 operands): mlvae_gemm_ex (128² register-staged)
+"""Time the train step's big GEMM shapes (c2 or, GEMM_FRAMES=128000, c3; bf16 operands): mlvae_gemm_ex (128² register-staged)
 against mlvae_gemm_bf16 (256² LDS-DMA), with torch.matmul (hipBLASLt, bf16 out) as the
 library reference point.  usage: python tools/gemm_bench.py"""
 import os
@@ -9,7 +9,8 @@ sys.path.insert(0, os.path.join(ROOT, "ml-vae_amd"))
 import torch  # noqa: E402
 from mlvae_hip._lib import check, lib  # noqa: E402
 
-N, H, D = 16000, 512, 1024
+N = int(os.environ.get("GEMM_FRAMES", "16000"))   # B*T rows: 16,000 at c2, 128,000 at c3
+H, D = 512, 1024
 SHAPES = [  # name, ta, tb, M, Ncols, K
     ("fwd proj  Y=X W^T  ", 0, 1, N, 8 * H, D),
     ("proj l0   Y=Z W^T  ", 0, 1, N, 8 * H, 32),
@@ -60,12 +61,18 @@ def _time(call, iters, M, Nc, K):
 
 
 def main():
+    only = os.environ.get("GEMM_ONLY")        # substring of a shape name: run just that one
+    modes = [int(m) for m in os.environ.get("GEMM_MODES", "0,1,2").split(",")]
     for name, ta, tb, M, Nc, K in SHAPES:
+        if only and only not in name:
+            continue
         r = []
-        for fast in (0, 1, 2):
+        for fast in modes:
             ms, tf = run(ta, tb, M, Nc, K, fast)
             r.append(f"{ms * 1e3:7.1f} us {tf:6.1f} TF")
-        print(f"{name} M={M:5d} N={Nc:5d} K={K:5d} | gemm_ex: {r[0]} | gemm_bf16 256²: {r[1]} | hipBLASLt: {r[2]}", flush=True)
+        names = {0: "gemm_ex", 1: "gemm_bf16 256²", 2: "hipBLASLt"}
+        print(f"{name} M={M:6d} N={Nc:5d} K={K:6d} | " +
+              " | ".join(f"{names[m]}: {x}" for m, x in zip(modes, r)), flush=True)
 
 
 if __name__ == "__main__":

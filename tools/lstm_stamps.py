@@ -26,13 +26,19 @@ def main():
     ap.add_argument("--prec", type=int, default=1)
     ap.add_argument("--bwd", action="store_true")
     ap.add_argument("--mode", type=int, default=0, help="lstm debug mode bits")
+    ap.add_argument("--noy", action="store_true", help="forward without the fp32 h output")
+    ap.add_argument("--drop", type=float, default=0.0, help="forward with the fused bf16 dropout(h)")
     a = ap.parse_args()
     B, T, H, prec = a.B, a.T, a.H, a.prec
     P = lambda t: t.data_ptr()
-    G = torch.randn(B * T, 8 * H, device="cuda") * 0.1
+    lib().mlvae_lstm_set_debug_mode(a.mode)
+    g16 = lib().mlvae_lstm_gates_fp16(B, H, prec)  # wide-batch kernels: fp16 gate buffer
+    G = (torch.randn(B * T, 8 * H, device="cuda") * 0.1).to(torch.float16 if g16 else torch.float32)
     Cs = torch.empty(B * T, 2 * H, device="cuda")
     Y = torch.empty(B * T, 2 * H, device="cuda")
     dGb = torch.empty(B * T, 8 * H, device="cuda", dtype=torch.bfloat16)
+    Yb = torch.empty(B * T, 2 * H, device="cuda", dtype=torch.bfloat16)
+    Ydb = torch.empty(B * T, 2 * H, device="cuda", dtype=torch.bfloat16)
     W0 = torch.randn(4 * H, H, device="cuda") * 0.04
     W1 = torch.randn(4 * H, H, device="cuda") * 0.04
     xb = ctypes.c_size_t()
@@ -41,7 +47,6 @@ def main():
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
     dbg = torch.zeros(T * 16, device="cuda", dtype=torch.int64)
     s = torch.cuda.current_stream().cuda_stream
-    lib().mlvae_lstm_set_debug_mode(a.mode)
     for it in range(4):
         if it == 3:
             lib().mlvae_lstm_set_debug(P(dbg))
@@ -51,11 +56,12 @@ def main():
             Cs.normal_()
         ev0.record()
         if a.bwd:
-            check(lib().mlvae_lstm_bwd_ex(prec, B, T, H, P(W0), P(W1), P(G), P(Cs), P(Y), P(dGb),
-                                          P(xbuf), xb.value, P(err), s))
+            check(lib().mlvae_lstm_bwd_ex2(prec, B, T, H, P(W0), P(W1), P(G), g16, P(Cs), P(Y), P(dGb),
+                                           P(xbuf), xb.value, P(err), s))
         else:
-            check(lib().mlvae_lstm_fwd(prec, B, T, H, P(W0), P(W1), P(G), P(Cs), P(Y), P(xbuf),
-                                       xb.value, P(err), s))
+            check(lib().mlvae_lstm_fwd_ex2(prec, B, T, H, P(W0), P(W1), P(G), g16, P(Cs),
+                                           None if a.noy else P(Y), P(Yb), P(Ydb) if a.drop else None,
+                                           7, 0, a.drop, P(xbuf), xb.value, P(err), s))
         ev1.record()
         torch.cuda.synchronize()
         ms = ev0.elapsed_time(ev1)
