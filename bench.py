@@ -63,12 +63,11 @@ def macs_per_frame(F, E, Z, H, L, C):
     return enc + lstm + heads
 
 
-def lstm_launch_bytes(B, T, H):
-    """Algorithmic HBM bytes of one recurrence launch (both directions), fp32 tensors:
-    fwd: read G [N,8H] + write gates [N,8H] + write c [N,2H] + write h [N,2H]
-    bwd: read gates [N,8H] + read c [N,2H] + read dY [N,2H] + write dG [N,8H]
-    (= 20H*4 bytes per frame either way)."""
-    return B * T * (8 * H + 8 * H + 2 * H + 2 * H) * 4
+def lstm_launch_bytes(B, T, H, gate_bytes=4, dg_bytes=4):
+    """Algorithmic HBM bytes of one BPTT launch (both directions) per frame: read the saved gates
+    [8H] (gate_bytes: 2 = the wide path's fp16 gate buffer, 4 = fp32), read c_{t-1} [2H] and dY
+    [2H] (fp32), write dG [8H] (dg_bytes: 2 = bf16 in bf16 mode)."""
+    return B * T * (8 * H * gate_bytes + 2 * H * 4 + 2 * H * 4 + 8 * H * dg_bytes)
 
 
 def lstm_launch_flops(B, T, H):
@@ -137,12 +136,15 @@ def cpu_baseline(cfg_name, budget_s=12.0):
 
 
 def pmc_traffic(key):
+    """HBM bytes per launch of kernel "<config>/<kernel>" from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/gpu_pmc.sh + tools/pmc_summary.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    cfg, _, kern = key.partition("/")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(key, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        return d.get(cfg, {}).get(kern, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError, AttributeError):
         return None
 
 
@@ -340,7 +342,9 @@ def main():
     if rank == 0:
         dom = "lstm_bwd"
         dur_s = kern[dom] * 1e-3
-        nbytes = lstm_launch_bytes(B, T, H)
+        from mlvae_hip._lib import lib
+        g16 = bool(lib().mlvae_lstm_gates_fp16(B, H, 1 if args.prec == "bf16" else 0))
+        nbytes = lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if args.prec == "bf16" else 4)
         achieved = nbytes / dur_s / 1e9
         step_us = kern[dom] * 1e3 / T
         out = {

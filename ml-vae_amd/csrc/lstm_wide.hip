@@ -31,6 +31,9 @@
 namespace {
 
 constexpr int WW = 8;  // waves per workgroup
+#ifndef NT_AUX
+#define NT_AUX 2  // cache policy of the read-once activation streams (2 = nt)
+#endif
 
 // Publish one 8-byte granule: a plain store when the whole group was verified to run on one
 // XCD (the line stays in that XCD's L2, where the members' sc1 loads read it), else a
@@ -137,7 +140,8 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
       const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
       const unsigned off = (unsigned)(((size_t)t_ * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
       unsigned short* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
-      if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, 0);
+      // nt: read-once stream, kept from displacing the hand-off lines in L2
+      if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
     }
   };
   // Philox keep bits (bit e = element e) of h chunk c8 (8 units) at step s_: one call per 4
@@ -406,7 +410,8 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
   // ahead; staged to LDS one step ahead (cst slot s_ & 1).  Chunks: 16 x 4 x HJ/8 gate chunks
   // (8 fp16 units), 16 x HJ/4 c chunks, 16 x HJ/4 dy chunks (4 fp32 units).
   constexpr int NGC = 16 * 4 * HJ / 8, NFC = 16 * HJ / 4, NCH = NGC + 2 * NFC;
-  constexpr int CPT = (NCH + 511) / 512;      // chunks per thread
+  constexpr int CPT = NCH / 512;              // chunks per thread
+  static_assert(NCH % 512 == 0, "whole chunks per thread");
   const size_t gbase = (size_t)grp * BG * T;  // first row (utterance grp*16, t = 0) of the group
   const auto rG = make_rsrc(reinterpret_cast<const unsigned short*>(a.G) + gbase * 8 * H, 0xffffffffu);
   const auto rC = make_rsrc(a.Cs + gbase * 2 * H, 0xffffffffu);
@@ -421,36 +426,36 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
     const int u = r / (HJ / 4), k = r % (HJ / 4);
     return u * CUTT + CG_B + which * CF_B + k * 16;
   };
+  // Unconditional loads (steps past the end and padded utterances read a clamped valid row and
+  // are never consumed): a conditional load would make the compiler merge the register values
+  // and wait for the loads right here, an HBM round trip on the hand-off's path.  The chunk
+  // kind changes at multiples of 64 chunks, so it -- and the buffer resource -- is wave-uniform.
+  const int ulast = a.B - 1 - grp * BG;  // last valid utterance of the group (>= 0)
   auto load_cell = [&](int s_) {
-    if (s_ >= T || (s_ > 1 && (a.dbg_mode & 2048))) return;  // bit 11: timing without the loads
-    const int t_ = dir ? s_ : T - 1 - s_;
+    const int sc = s_ < T ? s_ : T - 1;
+    const int t_ = dir ? sc : T - 1 - sc;
     const int tp_ = dir ? t_ + 1 : t_ - 1;
     const int tpc = tp_ < 0 ? 0 : (tp_ >= T ? T - 1 : tp_);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + 512 * i;
-      if (c >= NCH) continue;
-      if (c < NGC) {
-        const int u = c / (4 * HJ / 8), k = c % (4 * HJ / 8), g = k / (HJ / 8), uu = (k % (HJ / 8)) * 8;
-        if (grp * BG + u >= a.B) continue;
-        const unsigned o = ((unsigned)(u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2u;
-        creg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rG, o, 0, 0));
-      } else {
-        const int f = c - NGC, which = f / NFC, r = f % NFC;
-        const int u = r / (HJ / 4), uu = (r % (HJ / 4)) * 4;
-        if (grp * BG + u >= a.B) continue;
-        const unsigned o = ((unsigned)(u * T + (which ? t_ : tpc)) * 2 * H + dir * H + j0 + uu) * 4u;
-        creg[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(which ? rY : rC, o, 0, 0));
-      }
+      const int cw = wave * 64 + 512 * i;  // first chunk of this wave (uniform)
+      const int c = cw + lane;
+      const bool isg = cw < NGC, ydy = cw - NGC >= NFC;  // uniform: gates, c, dy chunks
+      const int r = c - NGC - (ydy ? NFC : 0);
+      const int ug = c / (4 * HJ / 8), k = c % (4 * HJ / 8), g = k / (HJ / 8), ugu = (k % (HJ / 8)) * 8;
+      const int uf = r / (HJ / 4), ufu = (r % (HJ / 4)) * 4;
+      const int u = min(isg ? ug : uf, ulast);
+      const unsigned og = ((unsigned)(u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + ugu) * 2u;
+      const unsigned of = ((unsigned)(u * T + (ydy ? t_ : tpc)) * 2 * H + dir * H + j0 + ufu) * 4u;
+      creg[i] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(isg ? rG : (ydy ? rY : rC), isg ? og : of, 0, NT_AUX));
     }
   };
   auto stage_cell = [&](int s_) {  // registers -> LDS slot s_ & 1 (visible after the next barrier)
-    if (s_ >= T) return;
     char* dst = cst + (s_ & 1) * 16 * CUTT;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int c = tid + 512 * i;
-      if (c < NCH) *reinterpret_cast<u32x4*>(dst + chunk_lds(c)) = creg[i];
+      *reinterpret_cast<u32x4*>(dst + chunk_lds(wave * 64 + 512 * i + lane)) = creg[i];
     }
   };
   float dc[CPG], cc[CPG];
@@ -486,14 +491,10 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
     float dh[CPG];
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) dh[ci] = 0.f;
-    if (s == 0) {  // step 1's inputs to LDS, step 2's loads issued
-      stage_cell(1);
-      load_cell(2);
-    }
+    u32x4 pv[CPG][NPL];
     if (s > 0) {
       const unsigned tag = step_tag(s - 1);
       const size_t sb = (size_t)((s - 1) & (NSLOT - 1)) * xslot + (size_t)js * NJ * HJ * 16;
-      u32x4 pv[CPG][NPL];
       unsigned spins = 0;
       while (true) {
 #pragma unroll
@@ -516,11 +517,14 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      STAMP(1);
-      // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
-      // s+2's loads issued right behind this step's hand-off
-      stage_cell(s + 1);
-      load_cell(s + 2);
+    }
+    STAMP(1);
+    // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
+    // s+2's loads issued right behind this step's hand-off -- one program point per step, so
+    // the loaded registers need no merge (and no wait for the loads)
+    stage_cell(s + 1);
+    load_cell(s + 2);
+    if (s > 0) {
       const bool b2 = pg & 4, b1 = pg & 2, b0 = pg & 1;
 #pragma unroll
       for (int ci = 0; ci < CPG; ++ci) {

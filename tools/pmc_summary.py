@@ -1,6 +1,9 @@
 """Per-kernel HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
-usage: python tools/pmc_summary.py <fetch counter_collection.csv> <write counter_collection.csv> <out.json>
+usage: python tools/pmc_summary.py <fetch counter_collection.csv> <write counter_collection.csv> <out.json> <config>
+
+The result is merged into out.json under the bench config's name (c2, c3, ...): bench.py reads
+profiles/pmc_traffic.json[config][kernel] for its roofline "traffic" fields.
 
 Both counters are reported in KB.  MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE
 counts exactly half of the bytes of wide coalesced streaming reads, so the read bytes are
@@ -21,14 +24,14 @@ def per_kernel(path):
 
 def short(name):
     n = name.replace("(anonymous namespace)::", "")
-    if "lstm_bwd_rs_kernel" in n or "lstm_bwd_kernel" in n:
-        return "lstm_bwd"
-    if "lstm_fwd_kernel" in n:
-        return "lstm_fwd"
+    for frag, key in (("lstm_bwd", "lstm_bwd"), ("lstm_fwd", "lstm_fwd"), ("heads_kernel", "heads"),
+                      ("encoder_fwd_kernel", "encoder_fwd"), ("encoder_bwd_kernel", "encoder_bwd")):
+        if frag in n:
+            return key
     return n.split("(")[0]
 
 
-def main(fetch_csv, write_csv, out):
+def main(fetch_csv, write_csv, out, config):
     f, w = per_kernel(fetch_csv), per_kernel(write_csv)
     res = {}
     for name in set(f) | set(w):
@@ -42,11 +45,17 @@ def main(fetch_csv, write_csv, out):
                     "write_size_bytes": write, "read_bytes_corrected": 2 * fetch,
                     "hbm_bytes_per_launch": 2 * fetch + write}
     res = dict(sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]))
-    json.dump(res, open(out, "w"), indent=1)
+    try:
+        with open(out) as fh:
+            allres = json.load(fh)
+    except (OSError, ValueError):
+        allres = {}
+    allres[config] = res
+    json.dump(allres, open(out, "w"), indent=1)
     for k, v in list(res.items())[:10]:
         print(f"{k:40s} launches {v['launches']:3d}  read {v['read_bytes_corrected'] / 1e6:9.1f} MB  "
               f"write {v['write_size_bytes'] / 1e6:9.1f} MB")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
