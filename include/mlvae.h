@@ -124,7 +124,9 @@ int mlvae_lstm_bwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, cons
  *   from Philox(drop_seed) with keep 1 - drop_p -- the same mask mlvae_dropout_ex and the
  *   dropout epilogues (epi 3) draw, so the dgrad GEMM's epilogue recomputes it.
  * bwd_ex2: gates are the forward's (fp16 when gates_fp16); the wide backward writes dG only as
- *   bf16 into dg_bf16 (required). */
+ *   bf16 into dg_bf16 (required) and, when dbias_rows != NULL (wide path only), the fp32 sums of
+ *   dG over each batch group's 16 utterances and all T steps: dbias_rows [ceil(B/16)][8H], whose
+ *   column sums are the layer's b_ih / b_hh gradients (ref:src/modules/decoder.py:14-15). */
 int mlvae_lstm_gates_fp16(int B, int H, int prec);
 int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                        void* gates, int gates_fp16, float* cells, float* y, void* y_bf16,
@@ -133,7 +135,8 @@ int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, con
                        int* err, void* stream);
 int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                        void* gates, int gates_fp16, const float* cells, const float* dy,
-                       void* dg_bf16, void* xbuf, size_t xbytes, int* err, void* stream);
+                       void* dg_bf16, float* dbias_rows, void* xbuf, size_t xbytes, int* err,
+                       void* stream);
 /* Workgroups (one per CU, co-resident) of the recurrence launch for this shape as the engine
  * runs it (fp16 gates where mlvae_lstm_gates_fp16): the wide kernels fill the chip. */
 int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd);

@@ -89,6 +89,32 @@ __device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, int
   }
 }
 
+// One of the 4 pieces of stage(): the interleaved main loop spreads them between MFMAs.
+template <bool KC>
+__device__ __forceinline__ void stage_piece(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
+                                            int k0, int kend, int shT, int sh, int wave, int lane, int j) {
+  const int piece = wave * 4 + j;
+  const int p = piece * 64 + lane;
+  unsigned off;
+  if constexpr (KC) {
+    const int row = p >> 3, c = (p & 7) ^ (row & 7);
+    const int gr = r0 + row, gk = k0 + 8 * c;
+    off = (gr < R && gk < kend) ? (unsigned)(((size_t)gr * ld + gk) * 2) : OOB;
+  } else {
+    const int kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr);
+    int gk = k0 + kr;
+    const int gr = r0 + 8 * c;
+    bool ok = gk < kend && gr < R;
+    if (sh != 0 && ok) {
+      const int t = gk % shT + sh;
+      ok = t >= 0 && t < shT;
+      gk += sh;
+    }
+    off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
+  }
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+}
+
 // MFMA 16x16x32 operand fragment: lane l gets rows/cols (base + (l & 15)), k = kk + 8 (l >> 4) + j.
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag(const short* img, int base, int kk, int lane) {
@@ -171,8 +197,11 @@ __device__ __forceinline__ float epi_apply(const GFArgs& g, float val, int row, 
   return val;
 }
 
-template <bool AKC, bool BKC, bool DEEP>
+// VAR 0: stage the next K-tile's 8 pieces per wave at the top of the K-step; 1: DEEP (BK 32,
+// 3 K-steps in flight); 2/3: the 8 pieces spread one per 8 MFMAs (3: + scheduling hints)
+template <bool AKC, bool BKC, int VAR>
 __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
+  constexpr bool DEEP = VAR == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   short* lds = reinterpret_cast<short*>(smem);   // [buf][A image, B image]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -238,6 +267,48 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
+  } else if constexpr (VAR >= 2) {
+    auto piece = [&](int buf, int k0, int pc) {
+      if (pc < 4)
+        stage_piece<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane, pc);
+      else
+        stage_piece<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane,
+                         pc - 4);
+    };
+    if (nk > 0) {
+#pragma unroll
+      for (int pc = 0; pc < 8; ++pc) piece(0, kbeg, pc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      const bool more = it + 1 < nk;
+      const int k1 = kbeg + (it + 1) * TBK;
+      const short* As = lds + (cur * 2 + 0) * IMG;
+      const short* Bs = lds + (cur * 2 + 1) * IMG;
+#pragma unroll
+      for (int kk = 0; kk < TBK; kk += 32) {
+        bf16x8 af[8], bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = frag<AKC>(As, wm * 128 + i * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (more && (i & 1) == 0) piece(cur ^ 1, k1, (kk / 32) * 4 + i / 2);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          if constexpr (VAR == 3) {
+            if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                     // four MFMAs
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile it+1 has landed (this wave's pieces)
+      __syncthreads();                                 // ... everyone's; buffer cur is free
+    }
   } else {
   auto stage_both = [&](int buf, int k0) {
     stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
@@ -392,9 +463,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
   }
 }
 
-template <bool AKC, bool BKC, bool DEEP>
-int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s) {
-  auto k = gemm256_kernel<AKC, BKC, DEEP>;
+template <bool AKC, bool BKC, int VAR>
+int launch_fast_v(const GFArgs& g, dim3 grid, hipStream_t s) {
+  auto k = gemm256_kernel<AKC, BKC, VAR>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -406,6 +477,16 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s) {
   }
   k<<<grid, 512, FAST_LDS, s>>>(g);
   return 0;
+}
+
+template <bool AKC, bool BKC>
+int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
+  switch (var) {
+    case 1: return launch_fast_v<AKC, BKC, 1>(g, grid, s);
+    case 2: return launch_fast_v<AKC, BKC, 2>(g, grid, s);
+    case 3: return launch_fast_v<AKC, BKC, 3>(g, grid, s);
+    default: return launch_fast_v<AKC, BKC, 0>(g, grid, s);
+  }
 }
 
 // split-K: long-K products (weight gradients over B*T frames) with fewer tiles than half the
@@ -521,23 +602,17 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), batch, s);
   int rc;
-  // deep-pipelined main loop (BK 32, 3 K-steps in flight) only with MLVAE_GEMM_DEEP=1: measured
-  // slower inside the c3 step (16.0 vs 15.3 ms), kept for A/B
-  static const bool deep = [] {
-    const char* e = getenv("MLVAE_GEMM_DEEP");
-    return e && atoi(e) != 0;
+  // main-loop variant (gemm256_kernel VAR): MLVAE_GEMM_VAR overrides (A/B timing).  The deep
+  // BK-32 pipeline (1) measured slower at every c3 shape (proj 1359 vs 1324 us, wgrad 1469 vs
+  // 1236 us)
+  static const int var = [] {
+    const char* e = getenv("MLVAE_GEMM_VAR");
+    return e ? atoi(e) : 0;
   }();
-  if (deep) {
-    if (akc && bkc) rc = launch_fast<true, true, true>(g, grid, st);
-    else if (akc) rc = launch_fast<true, false, true>(g, grid, st);
-    else if (bkc) rc = launch_fast<false, true, true>(g, grid, st);
-    else rc = launch_fast<false, false, true>(g, grid, st);
-  } else {
-    if (akc && bkc) rc = launch_fast<true, true, false>(g, grid, st);
-    else if (akc) rc = launch_fast<true, false, false>(g, grid, st);
-    else if (bkc) rc = launch_fast<false, true, false>(g, grid, st);
-    else rc = launch_fast<false, false, false>(g, grid, st);
-  }
+  if (akc && bkc) rc = launch_fast<true, true>(g, grid, st, var);
+  else if (akc) rc = launch_fast<true, false>(g, grid, st, var);
+  else if (bkc) rc = launch_fast<false, true>(g, grid, st, var);
+  else rc = launch_fast<false, false>(g, grid, st, var);
   if (rc) return rc;
   MLVAE_CHECK_LAUNCH();
   if (s > 1) {

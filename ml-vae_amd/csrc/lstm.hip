@@ -940,8 +940,9 @@ bool use_wide(int B, int H, int prec) {
   return lstm_wide_workgroups(B, H, true) > 0 && lstm_wide_workgroups(B, H, false) > 0;
 }
 
-struct WideExtra {  // forward-only outputs of the wide kernels
-  unsigned short* ydb = nullptr;
+struct WideExtra {  // outputs only the wide kernels write
+  unsigned short* ydb = nullptr;  // forward: bf16 dropout(h)
+  float* dbias = nullptr;         // backward: per batch group bias-gradient rows
   unsigned long long seed = 0, off = 0;
   float p = 0.f;
 };
@@ -962,11 +963,11 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
   if (wide) {
     if (!fwd && !dgb) { mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 (NULL)"); return 1; }
     if (ex.ydb && !(ex.p >= 0.f && ex.p < 1.f)) { mlvae_set_error("lstm: dropout p=%g", ex.p); return 1; }
-    return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.ydb,
+    return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.dbias, ex.ydb,
                          ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode);
   }
-  if (ex.ydb || !Y) {
-    mlvae_set_error("lstm: fused dropout output / Y = NULL only on the wide-batch path");
+  if (ex.ydb || ex.dbias || !Y) {
+    mlvae_set_error("lstm: fused dropout / bias-gradient outputs, Y = NULL only on the wide-batch path");
     return 1;
   }
   const int bmax = max_batch_per_launch(H, fwd, prec);
@@ -1065,11 +1066,14 @@ extern "C" int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_
 
 extern "C" int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd,
                                   const float* w_hh_rev, void* gates, int gates_fp16,
-                                  const float* cells, const float* dy, void* dg_bf16, void* xbuf,
-                                  size_t xbytes, int* err, void* stream) {
+                                  const float* cells, const float* dy, void* dg_bf16,
+                                  float* dbias_rows, void* xbuf, size_t xbytes, int* err,
+                                  void* stream) {
+  WideExtra ex;
+  ex.dbias = dbias_rows;
   return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
              const_cast<float*>(cells), const_cast<float*>(dy), xbuf, xbytes, err,
-             (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), gates_fp16);
+             (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), gates_fp16, ex);
 }
 
 extern "C" int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd,

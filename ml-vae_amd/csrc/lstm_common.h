@@ -31,6 +31,8 @@ struct LstmArgs {
   unsigned* xtab;           // [ngroups][NJ] XCC id + 1 of every member (zeroed per launch)
   unsigned short* Yb;       // optional bf16 copy of h [B*T, 2H] (fwd; GEMM operand)
   unsigned short* dGb;      // optional: bwd writes dG as bf16 [B*T, 8H] here instead of into G
+  float* dbias;             // wide bwd, optional: per batch group sums of dG over (utterance, t),
+                            // [ceil(B/16)][8H] fp32 -- the bias gradients before the group sum
   // wide-batch forward only: bf16 dropout(h) [B*T, 2H] for the next layer (Philox mask of
   // element doff + row*2H + col, keep prob dkeep, scale dscale; NULL = none)
   unsigned short* Ydb;
@@ -111,7 +113,7 @@ __device__ __forceinline__ bool tags_ok(u32x4 v, unsigned tag, bool g0, bool g1)
 // supported (the caller then falls back to chunked batch-group launches), else a status.
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
-                  unsigned short* yb, unsigned short* dgb, unsigned short* ydb,
+                  unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
                   unsigned long long* dbg, int dbg_mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply

@@ -458,11 +458,12 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
       *reinterpret_cast<u32x4*>(dst + chunk_lds(wave * 64 + 512 * i + lane)) = creg[i];
     }
   };
-  float dc[CPG], cc[CPG];
+  float dc[CPG], cc[CPG], bsum[CPG][4];
 #pragma unroll
   for (int ci = 0; ci < CPG; ++ci) {
     dc[ci] = 0.f;
     cc[ci] = 0.f;
+    bsum[ci][0] = bsum[ci][1] = bsum[ci][2] = bsum[ci][3] = 0.f;
     if (bv[ci]) {
       const int t0 = dir ? 0 : T - 1;
       cc[ci] = a.Cs[((size_t)(grp * BG + cu[ci]) * T + t0) * 2 * H + dir * H + j0 + uc[ci]];
@@ -575,6 +576,7 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
         d3 = d_o * xo[ci] * (1.f - xo[ci]);
       }
       cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
+      bsum[ci][0] += d0; bsum[ci][1] += d1; bsum[ci][2] += d2; bsum[ci][3] += d3;
       const int u = uc[ci], r = cu[ci];
       const float dg[4] = {d0, d1, d2, d3};
 #pragma unroll
@@ -631,6 +633,27 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
   };
   for (int s = 0; s < T; ++s)
     if (!step(s)) break;
+  // bias gradients of this workgroup's units: the lane sums over its steps, then over the
+  // group's 16 utterances (8 lanes x CPG halves; fixed order), one row per batch group
+  if (a.dbias) {
+    float bs[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float v = bsum[0][g];
+#pragma unroll
+      for (int ci = 1; ci < CPG; ++ci) v += bsum[ci][g];  // CPG 2: both halves share the unit
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (CPG == 1) v += __shfl_xor(v, 8, 64);  // CPG 1: the two halves are adjacent groups
+      bs[g] = v;
+    }
+    if (pg == 0 && (CPG == 2 || (gq & 1) == 0)) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        a.dbias[(size_t)grp * 8 * H + dir * 4 * H + g * H + j0 + uc[0]] = bs[g];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -711,7 +734,7 @@ size_t lstm_wide_xbytes(int B, int H, bool fwd) {
 
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
-                  unsigned short* yb, unsigned short* dgb, unsigned short* ydb,
+                  unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
                   unsigned long long* dbg, int dbg_mode) {
   WidePlan p = wide_plan(B, H, fwd);
@@ -724,7 +747,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.B = B; a.T = T; a.H = H; a.NB = p.NB; a.NJ = p.NJ; a.HJ = p.HJ; a.Kp = H; a.K4p = 4 * H;
   a.W0 = W0; a.W1 = W1; a.G = G; a.Cs = Cs; a.Y = Y; a.xbuf = xbuf; a.err = err;
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;
-  a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
+  a.dbias = dbias; a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
   a.dscale = dp < 1.f ? 1.f / (1.f - dp) : 0.f;
   a.xtab = reinterpret_cast<unsigned*>(static_cast<char*>(xbuf) + p.xtab_off);
   // zero fill = a stale tag in every granule (and an empty placement table)

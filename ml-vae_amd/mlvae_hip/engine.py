@@ -188,6 +188,9 @@ class _Work:
         # (halves the projection's write and the recurrences' reads; include/mlvae.h)
         self.g16 = bool(lib().mlvae_lstm_gates_fp16(B, H, PREC[cfg.prec]))
         self.G = [empty(N, 8 * H, dtype=torch.float16 if self.g16 else torch.float32) for _ in range(L)]
+        # wide BPTT: per batch group rows of the bias gradients (summed over groups by colsum)
+        self.NBG = (B + 15) // 16
+        self.dbias_rows = [empty(self.NBG, 8 * H, **f) if self.g16 else None for _ in range(L)]
         self.Cs = [empty(N, 2 * H, **f) for _ in range(L)]
         self.Y = [empty(N, 2 * H, **f) for _ in range(L)]
         self.Yd = [empty(N, 2 * H, **f) if cfg.dropout > 0 else None for _ in range(L - 1)]
@@ -814,10 +817,13 @@ class VAEEngine:
             Gl = w.G[li]
             dGb = w.dGb[li] if w.bf else None
             with self._timed("lstm_bwd"):
+                # the layer-0 biases come with dW_ih_l0 from skinny_tn when the encoder is fused
+                rows = w.dbias_rows[li] if (w.g16 and not (li == 0 and w.enc_fused)) else None
                 check(l.mlvae_lstm_bwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                            self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
                                            int(w.g16), _p(w.Cs[li]), _p(w.dY[li]),
                                            _pb(dGb) if dGb is not None else None,
+                                           _p(rows) if rows is not None else None,
                                            _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
             self._flush_side(pending)
             # dG: fp32 in G (fp32 mode) or bf16 in dGb (bf16 mode)
@@ -863,7 +869,10 @@ class VAEEngine:
                     self._mm(w, 1, 0, 4 * H, H, N, pg(dG, 4 * H), 8 * H, _p(w.Y[li], H), 2 * H,
                              gp(f"decoder.rnn.weight_hh_l{li}_reverse"), H, A_bf=pgb(dG_bf, 4 * H),
                              B_bf=pgb(Ybl, H), kshift_T=T, kshift=1)
-                if dG_bf is not None:
+                if w.g16:  # the BPTT summed dG per batch group: sum the groups' rows
+                    self._colsum(w, w.NBG, 8 * H, _p(w.dbias_rows[li]), 8 * H,
+                                 gp(f"decoder.rnn.bias_ih_l{li}"), gp(f"decoder.rnn.bias_hh_l{li}"))
+                elif dG_bf is not None:
                     ws = w.gws_side if self._on_side else w.gws
                     check(lib().mlvae_colsum_ex(N, 8 * H, _pb(dG_bf), 1, 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
                                                 gp(f"decoder.rnn.bias_hh_l{li}"), 0.0, _p(ws), w.gws_bytes,

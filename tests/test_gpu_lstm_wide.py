@@ -88,12 +88,16 @@ def test_wide_recurrence_matches_fp64_loop(B, T, force):
         assert err.item() == 0 and torch.equal(Yb1, Yb) and torch.equal(G1, G)
         dGb = torch.empty(N, 8 * H, device="cuda", dtype=torch.bfloat16)
         dY = dy.float().reshape(N, 2 * H).cuda().contiguous()
+        rows = torch.full(((B + 15) // 16, 8 * H), float("nan"), device="cuda")
         check(lib().mlvae_lstm_bwd_ex2(1, B, T, H, P(W0), P(W1), P(G), 1, P(Cs), P(dY), dGb.data_ptr(),
-                                       P(xbuf), xb.value, P(err), stream()))
+                                       P(rows), P(xbuf), xb.value, P(err), stream()))
         torch.cuda.synchronize()
         assert err.item() == 0
         e1 = rel_err(dGb.float().view(B, T, 8 * H), dG)
         e2 = norm_rel(dGb.float().view(B, T, 8 * H), dG)
+        # bias-gradient rows: per batch group sums of dG over utterances and steps
+        ref_rows = torch.nn.functional.pad(dG, (0, 0, 0, 0, 0, (-B) % 16)).view(-1, 16, T, 8 * H).sum((1, 2))
+        assert norm_rel(rows, ref_rows) < 2e-2 and torch.isfinite(rows).all()
         print(f"\nB={B} T={T} force={force}: Y {rel_err(Y.view(B, T, 2 * H), y):.2e}  dG max-rel {e1:.2e} "
               f"norm-rel {e2:.2e}")
         assert e1 < TOL_DG and e2 < 2e-2
@@ -125,7 +129,7 @@ def test_gate_buffer_format_is_checked():
     B, N = 256, 256 * 4
     G = torch.zeros(N, 8 * H, device="cuda", dtype=torch.float16)
     Cs = torch.empty(N, 2 * H, device="cuda")
-    assert l.mlvae_lstm_bwd_ex2(1, B, T, H, P(W), P(W), P(G), 1, P(Cs), P(Cs), None,
+    assert l.mlvae_lstm_bwd_ex2(1, B, T, H, P(W), P(W), P(G), 1, P(Cs), P(Cs), None, None,
                                 P(xbuf), xb.value, P(err), stream()) != 0
     # the batch-group fallback skips neither output: Y = NULL is refused there
     assert l.mlvae_lstm_fwd_ex2(1, 32, T, H, P(W), P(W), P(G), 0, P(Cs), None, None, None, 0, 0, 0.0,

@@ -56,7 +56,7 @@ def main():
             Cs.normal_()
         ev0.record()
         if a.bwd:
-            check(lib().mlvae_lstm_bwd_ex2(prec, B, T, H, P(W0), P(W1), P(G), g16, P(Cs), P(Y), P(dGb),
+            check(lib().mlvae_lstm_bwd_ex2(prec, B, T, H, P(W0), P(W1), P(G), g16, P(Cs), P(Y), P(dGb), None,
                                            P(xbuf), xb.value, P(err), s))
         else:
             check(lib().mlvae_lstm_fwd_ex2(prec, B, T, H, P(W0), P(W1), P(G), g16, P(Cs),
