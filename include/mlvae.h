@@ -113,6 +113,17 @@ int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, cons
 int mlvae_lstm_bwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                       float* gates, const float* cells, const float* dy, void* dg_bf16,
                       void* xbuf, size_t xbytes, int* err, void* stream);
+/* Unidirectional layer, nn.LSTM(bidirectional=False, batch_first=True): the phoneme
+ * recogniser's and boundary detector's LSTMs (ref:src/modules/phoneme_recognizer.py:13,
+ * ref:src/modules/boundary_detector.py:19) and the MD-VAE's 512-unit RNN (ref:src/models/MD_VAE/
+ * model.yaml:78-83).  gates [B*T, 4H] fp32 (in: x W_ih^T + b_ih + b_hh; out: activated i,f,g,o;
+ * the backward overwrites them with dG unless dg_bf16 != NULL), cells / y / dy [B*T, H].  Same
+ * workspace, err word and batch chunking as mlvae_lstm_fwd. */
+int mlvae_lstm1_fwd(int prec, int B, int T, int H, const float* w_hh, float* gates, float* cells,
+                    float* y, void* y_bf16, void* xbuf, size_t xbytes, int* err, void* stream);
+int mlvae_lstm1_bwd(int prec, int B, int T, int H, const float* w_hh, float* gates,
+                    const float* cells, const float* dy, void* dg_bf16, void* xbuf, size_t xbytes,
+                    int* err, void* stream);
 /* Wide-batch recurrence (csrc/lstm_wide.hip): one launch per layer for the whole batch when B is
  * past one batch-group launch (bf16, H = 512).  mlvae_lstm_gates_fp16(B, H, prec) = 1 for such
  * shapes; their gate buffer is IEEE fp16 [B*T, 8H] (half the projection's write and the
@@ -142,6 +153,29 @@ int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, con
 int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd);
 /* Diagnostics: record per-step phase stamps of workgroup 0 into buf (NULL disables). */
 int mlvae_lstm_set_debug(void* buf);
+
+/* MD-VAE upstream-LSTM losses (csrc/md.hip).
+ * mlvae_phn_bce: PhonemeRecognizer.compute_losses (ref:src/modules/phoneme_recognizer.py:35-81).
+ *   logits [B,T,C] (row stride ldl), feat_lens / phn_lens [B] relative, phn [B,L] int64 ids,
+ *   boundary [B,T] 0/1 (float).  Frame t < T_i = round(T feat_len) gets target one-hot(phn[b, k])
+ *   with k = (boundaries in [0, t]) - 1; loss [B,T,C] = BCE-with-logits, 0 past T_i (may be NULL);
+ *   with dloss given, dlogits = dloss (sigmoid(x) - y).  The reference's asserts set *err bits:
+ *   2 = boundaries do not give L_i = round(L phn_len) segments from frame 0, 4 = phoneme id
+ *   outside [0, C).
+ * mlvae_boundary_fwd / _bwd: BoundaryDetector after its FC heads (ref:src/modules/boundary_detector.py:
+ *   42-97).  za, zb [n] = pre-Softplus head outputs, y [n] boundary targets, u [10][n] U(0,1) draws
+ *   (NULL: Philox(seed) at element offset + s*n + i).  Forward: v = mean of the ten clamped
+ *   Kumaraswamy draws, bce = their mean BCE, kld = KL(Beta(alpha, beta) || Beta(1, 9)) (any output
+ *   may be NULL).  Backward: dza, dzb from the cotangents dv, dbce, dkld (NULL = 0). */
+int mlvae_phn_bce(int B, int T, int C, const float* logits, int ldl, const float* feat_lens,
+                  const long long* phn, int L, const float* phn_lens, const float* boundary,
+                  float* loss, const float* dloss, float* dlogits, int* err, void* stream);
+int mlvae_boundary_fwd(size_t n, const float* za, const float* zb, const float* y, const float* u,
+                       unsigned long long seed, unsigned long long offset, float* v, float* bce,
+                       float* kld, void* stream);
+int mlvae_boundary_bwd(size_t n, const float* za, const float* zb, const float* y, const float* u,
+                       unsigned long long seed, unsigned long long offset, const float* dv,
+                       const float* dbce, const float* dkld, float* dza, float* dzb, void* stream);
 
 /* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
  * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   __shared__ int abort_flag;
   __shared__ volatile int poll_seq;  // last step whose hand-off wave 0 has received
 
-  const int ngroups = 2 * a.NB;
+  const int ngroups = a.ndir * a.NB;
   int gid, js;
   if (a.xcd_local) {
     gid = blockIdx.x & 7; js = blockIdx.x >> 3;
@@ -72,6 +72,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
     gid = blockIdx.x % ngroups; js = blockIdx.x / ngroups;
   }
   const int dir = gid / a.NB, grp = gid % a.NB;
+  const int GLD = 4 * a.H * a.ndir, YLD = a.H * a.ndir;  // row strides of G and of c / h
   const int H = a.H, T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* W = dir ? a.W1 : a.W0;
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   auto io_gload = [&](int s_, f32x4 (&v)[4]) {
     if (iobv && s_ < T) {
       const int t_ = dir ? T - 1 - s_ : s_;
-      const float* p = a.G + ((size_t)iobg * T + t_) * 8 * H + dir * 4 * H + iog * H + j0;
+      const float* p = a.G + ((size_t)iobg * T + t_) * GLD + dir * 4 * H + iog * H + j0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const f32x4*>(p + 4 * i);
     }
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
       float v[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = src[iob * OUS + u * 8 + iog];
-      float* gp = a.G + ((size_t)iobg * T + t_) * 8 * H + dir * 4 * H + iog * H + j0;
+      float* gp = a.G + ((size_t)iobg * T + t_) * GLD + dir * 4 * H + iog * H + j0;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         *reinterpret_cast<f32x4*>(gp + 4 * i) = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
       float v[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = src[b2 * OUS + u * 8 + (kind == 0 ? 4 : 5)];
-      const size_t o = ((size_t)bg2 * T + t_) * 2 * H + dir * H + j0;
+      const size_t o = ((size_t)bg2 * T + t_) * YLD + dir * H + j0;
       if (kind < 2) {
         float* dp = (kind == 0 ? a.Cs : a.Y) + o;
 #pragma unroll
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   auto load_gx = [&](int s_) {
     if (valid && s_ < T && !(s_ > 0 && (a.dbg_mode & 2048))) {  // bit 11: timing without prefetch
       const int t_ = dir ? T - 1 - s_ : s_;
-      const float* gp = a.G + ((size_t)bglob * T + t_) * 8 * H + dir * 4 * H + j0 + jj;
+      const float* gp = a.G + ((size_t)bglob * T + t_) * GLD + dir * 4 * H + j0 + jj;
 #pragma unroll
       for (int g = 0; g < 4; ++g) gx[g] = gp[g * H];
     }
@@ -317,11 +318,11 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
     } else {
       load_gx(s + 1);
       if (valid && !(a.dbg_mode & 1)) {  // saved activations: plain stores, off the critical path
-        float* gp = a.G + n * 8 * H + dir * 4 * H + j0 + jj;
+        float* gp = a.G + n * GLD + dir * 4 * H + j0 + jj;
         gp[0] = ig; gp[H] = fg; gp[2 * H] = gg; gp[3 * H] = og;
-        a.Cs[n * 2 * H + dir * H + j0 + jj] = c;
-        a.Y[n * 2 * H + dir * H + j0 + jj] = hv;
-        if (a.Yb) a.Yb[n * 2 * H + dir * H + j0 + jj] = (unsigned short)f2bf(hv);
+        a.Cs[n * YLD + dir * H + j0 + jj] = c;
+        a.Y[n * YLD + dir * H + j0 + jj] = hv;
+        if (a.Yb) a.Yb[n * YLD + dir * H + j0 + jj] = (unsigned short)f2bf(hv);
       }
     }
   }
@@ -373,9 +374,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
   float* red = reinterpret_cast<float*>(smem);  // [2][4 waves][16 utterances][RW] partials
   __shared__ int abort_flag;
 
-  const int ngroups = 2 * a.NB;
+  const int ngroups = a.ndir * a.NB;
   const int gid = blockIdx.x % ngroups, js = blockIdx.x / ngroups;
   const int dir = gid / a.NB, grp = gid % a.NB;
+  const int GLD = 4 * a.H * a.ndir, YLD = a.H * a.ndir;  // row strides of G and of c / h
   const int H = a.H, T = a.T, j0 = js * HJ, G4 = 4 * H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* W = dir ? a.W1 : a.W0;
@@ -429,12 +431,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
         const int uu = cj + 16 * u;
         if (uu < HJ) {
           const int j = j0 + uu;
-          const float* gp = a.G + n_ * 8 * H + dir * 4 * H + j;
+          const float* gp = a.G + n_ * GLD + dir * 4 * H + j;
           gi[u] = gp[0]; gf[u] = gp[H]; gg[u] = gp[2 * H]; go[u] = gp[3 * H];
-          cc[u] = a.Cs[n_ * 2 * H + dir * H + j];
-          const float cpl = a.Cs[np_ * 2 * H + dir * H + j];
+          cc[u] = a.Cs[n_ * YLD + dir * H + j];
+          const float cpl = a.Cs[np_ * YLD + dir * H + j];
           cp[u] = has_prev ? cpl : 0.f;
-          dy[u] = a.Y[n_ * 2 * H + dir * H + j];
+          dy[u] = a.Y[n_ * YLD + dir * H + j];
         }
       }
     }
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
       for (int u = 0; u < UPT; ++u) {
         const int uu = cj + 16 * u;
         if (uu < HJ) {
-          const size_t o = n * 8 * H + dir * 4 * H + j0 + uu;
+          const size_t o = n * GLD + dir * 4 * H + j0 + uu;
           if (a.dGb) {
             unsigned short* gb = a.dGb + o;
             gb[0] = (unsigned short)f2bf(dG[u][0]); gb[H] = (unsigned short)f2bf(dG[u][1]);
@@ -607,7 +609,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
   short* abuf = reinterpret_cast<short*>(smem);  // [2][16 utterances][AST]
   __shared__ int abort_flag, placement;
 
-  const int ngroups = 2 * a.NB;
+  const int ngroups = a.ndir * a.NB;
   int gid, js;
   if (a.xcd_local) {
     gid = blockIdx.x & 7; js = blockIdx.x >> 3;
@@ -616,6 +618,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
     gid = blockIdx.x % ngroups; js = blockIdx.x / ngroups;
   }
   const int dir = gid / a.NB, grp = gid % a.NB;
+  const int GLD = 4 * a.H * a.ndir, YLD = a.H * a.ndir;  // row strides of G and of c / h
   const int H = a.H, T = a.T, j0 = js * 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* W = dir ? a.W1 : a.W0;
@@ -667,11 +670,11 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
       const int tp_ = dir ? t_ + 1 : t_ - 1;
       const size_t n_ = (size_t)bglob * T + t_;
       const size_t np_ = (size_t)bglob * T + min(max(tp_, 0), T - 1);
-      const float* gp = a.G + n_ * 8 * H + dir * 4 * H + j;
+      const float* gp = a.G + n_ * GLD + dir * 4 * H + j;
       c.gi = gp[0]; c.gf = gp[H]; c.gg = gp[2 * H]; c.go = gp[3 * H];
-      c.cc = a.Cs[n_ * 2 * H + dir * H + j];
-      c.cp = a.Cs[np_ * 2 * H + dir * H + j];
-      c.dy = a.Y[n_ * 2 * H + dir * H + j];
+      c.cc = a.Cs[n_ * YLD + dir * H + j];
+      c.cp = a.Cs[np_ * YLD + dir * H + j];
+      c.dy = a.Y[n_ * YLD + dir * H + j];
     }
   };
   float dc = 0.f;
@@ -795,7 +798,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
     }
     STAMP(4);
     if (bvalid && !(a.dbg_mode & 1)) {  // dG for the weight-gradient GEMMs: plain stores
-      const size_t o = n * 8 * H + dir * 4 * H + j;
+      const size_t o = n * GLD + dir * 4 * H + j;
       if (a.dGb) {
         unsigned short* gb = a.dGb + o;
         gb[0] = (unsigned short)f2bf(dG0); gb[H] = (unsigned short)f2bf(dG1);
@@ -886,7 +889,7 @@ int max_batch_per_launch(int H, bool fwd, int prec) {
 
 template <int PREC, int HJ, int NL>
 int launch_nl(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
-  dim3 grid(a.xcd_local ? 8 * a.NJ : 2 * a.NB * a.NJ);
+  dim3 grid(a.xcd_local ? 8 * a.NJ : a.ndir * a.NB * a.NJ);
   auto k = fwd ? lstm_fwd_kernel<PREC, HJ, NL> : lstm_bwd_kernel<PREC, HJ, NL>;
   const size_t lds = p.lds;
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
@@ -919,7 +922,7 @@ int launch(bool fwd, const LstmArgs& a, const Plan& p, hipStream_t s) {
 
 template <int NTW>
 int launch_rs(const LstmArgs& a, const Plan& p, hipStream_t s) {
-  dim3 grid(a.xcd_local ? 8 * a.NJ : 2 * a.NB * a.NJ);
+  dim3 grid(a.xcd_local ? 8 * a.NJ : a.ndir * a.NB * a.NJ);
   auto k = lstm_bwd_rs_kernel<NTW>;
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
     mlvae_set_error("lstm: cannot reserve %zu B LDS", p.lds);
@@ -950,12 +953,14 @@ struct WideExtra {  // outputs only the wide kernels write
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
         float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
         unsigned short* yb = nullptr, unsigned short* dgb = nullptr, int gates_fp16 = 0,
-        const WideExtra& ex = WideExtra()) {
+        const WideExtra& ex = WideExtra(), int ndir = 2) {
   if (B <= 0 || T <= 0) return 0;
   if (H <= 0 || H % 4 != 0) { mlvae_set_error("lstm: H=%d must be a positive multiple of 4", H); return 1; }
   if (prec != PREC_F32 && prec != PREC_BF16) { mlvae_set_error("lstm: bad prec %d", prec); return 1; }
   // fp16 gates select the wide-batch kernels; fp32 gates the batch-group kernels (chunked)
   const bool wide = gates_fp16 != 0;
+  if (ndir != 1 && ndir != 2) { mlvae_set_error("lstm: %d directions", ndir); return 1; }
+  if (wide && ndir != 2) { mlvae_set_error("lstm: fp16 gates are bidirectional only"); return 1; }
   if (wide && !use_wide(B, H, prec)) {
     mlvae_set_error("lstm: B=%d H=%d prec=%d: fp16 gates only where mlvae_lstm_gates_fp16() = 1", B, H, prec);
     return 1;
@@ -985,12 +990,14 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     LstmArgs a;
     a.B = bc; a.T = T; a.H = H; a.NB = p.NB; a.NJ = p.NJ; a.HJ = p.HJ; a.Kp = p.Kp; a.K4p = p.K4p;
     a.W0 = W0; a.W1 = W1;
-    a.G = G + (size_t)b0 * T * 8 * H;
-    a.Cs = Cs + (size_t)b0 * T * 2 * H;
-    a.Y = Y + (size_t)b0 * T * 2 * H;
+    const size_t gld = (size_t)4 * H * ndir, yld = (size_t)H * ndir;  // row strides
+    a.ndir = ndir;
+    a.G = G + (size_t)b0 * T * gld;
+    a.Cs = Cs + (size_t)b0 * T * yld;
+    a.Y = Y + (size_t)b0 * T * yld;
     a.xbuf = xbuf; a.err = err; a.dbg = g_dbg; a.dbg_mode = g_dbg_mode;
-    a.Yb = yb ? yb + (size_t)b0 * T * 2 * H : nullptr;
-    a.dGb = dgb ? dgb + (size_t)b0 * T * 8 * H : nullptr;
+    a.Yb = yb ? yb + (size_t)b0 * T * yld : nullptr;
+    a.dGb = dgb ? dgb + (size_t)b0 * T * gld : nullptr;
     // XCD-local groups: on by default for the forward (measured 2.67 vs 2.73 us/step at c2;
     // bit 2 turns it off), opt-in for the backward (bit 1: no gain inside a training step,
     // where the side-stream weight-gradient GEMMs want those XCDs)
@@ -1074,6 +1081,23 @@ extern "C" int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_
   return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
              const_cast<float*>(cells), const_cast<float*>(dy), xbuf, xbytes, err,
              (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), gates_fp16, ex);
+}
+
+// Unidirectional layer (nn.LSTM(bidirectional=False)): gates [B*T, 4H] fp32 (in: x W_ih^T + b;
+// out: activated i,f,g,o), cells / y [B*T, H]; batch-group kernels with one direction's groups.
+extern "C" int mlvae_lstm1_fwd(int prec, int B, int T, int H, const float* w_hh, float* gates,
+                               float* cells, float* y, void* y_bf16, void* xbuf, size_t xbytes,
+                               int* err, void* stream) {
+  return run(true, prec, B, T, H, w_hh, w_hh, gates, cells, y, xbuf, xbytes, err,
+             (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 0, WideExtra(), 1);
+}
+
+extern "C" int mlvae_lstm1_bwd(int prec, int B, int T, int H, const float* w_hh, float* gates,
+                               const float* cells, const float* dy, void* dg_bf16, void* xbuf,
+                               size_t xbytes, int* err, void* stream) {
+  return run(false, prec, B, T, H, w_hh, w_hh, gates, const_cast<float*>(cells),
+             const_cast<float*>(dy), xbuf, xbytes, err, (hipStream_t)stream, nullptr,
+             static_cast<unsigned short*>(dg_bf16), 0, WideExtra(), 1);
 }
 
 extern "C" int mlvae_lstm_fwd_ex(int prec, int B, int T, int H, const float* w_hh_fwd,

@@ -15,6 +15,7 @@ constexpr int MIN_LDS = 82 * 1024; // > half of 160 KiB: one workgroup per CU (r
 struct LstmArgs {
   int B, T, H;        // B = utterances handled by this launch (<= NB*16)
   int NB, NJ, HJ;     // batch groups, hidden slices per group, hidden units per slice
+  int ndir;           // directions: 2 (bidirectional, gates [N,8H], h [N,2H]) or 1 ([N,4H], [N,H])
   int Kp;             // H padded (pow2 >= 128): fwd exchange row stride / MFMA K
   int K4p;            // 4H padded (pow2 >= 128): bwd exchange row stride / MFMA K
   const float* W0;    // W_hh forward dir  [4H, H]

@@ -744,6 +744,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
     return 1;
   }
   LstmArgs a{};
+  a.ndir = 2;
   a.B = B; a.T = T; a.H = H; a.NB = p.NB; a.NJ = p.NJ; a.HJ = p.HJ; a.Kp = H; a.K4p = 4 * H;
   a.W0 = W0; a.W1 = W1; a.G = G; a.Cs = Cs; a.Y = Y; a.xbuf = xbuf; a.err = err;
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;

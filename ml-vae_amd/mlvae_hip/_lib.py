@@ -38,6 +38,11 @@ _SIGS = {
     "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_fwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_phn_bce": [I, I, I, P, I, P, P, I, P, P, P, P, P, P, P],
+    "mlvae_boundary_fwd": [SZ, P, P, P, P, U64, U64, P, P, P, P],
+    "mlvae_boundary_bwd": [SZ, P, P, P, P, U64, U64, P, P, P, P, P, P],
+    "mlvae_lstm1_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_lstm1_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_gates_fp16": [I, I, I],
     "mlvae_lstm_fwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_bwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, P, SZ, P, P],

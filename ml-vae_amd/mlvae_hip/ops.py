@@ -267,33 +267,39 @@ def _dropout(src, dst, seed, p):
     check(lib().mlvae_dropout(src.numel(), _p(src), _p(dst), None, seed, p, _stream()), "dropout")
 
 
-class BiLSTMFn(torch.autograd.Function):
-    """nn.LSTM(bidirectional=True, batch_first=True) on libmlvae (ref:src/modules/decoder.py:14-15,22):
-    per layer an input-projection GEMM per direction + the persistent recurrence; inter-layer
-    dropout (Philox, recomputed in backward) in train mode.  weights = the layer-major list
-    [w_ih, w_hh, b_ih, b_hh, w_ih_r, w_hh_r, b_ih_r, b_hh_r] * L."""
+class LSTMFn(torch.autograd.Function):
+    """nn.LSTM(batch_first=True) on libmlvae, bidirectional (ndir 2: ref:src/modules/decoder.py:14-15,22)
+    or not (ndir 1: ref:src/modules/phoneme_recognizer.py:13, boundary_detector.py:19): per layer
+    an input-projection GEMM per direction + the persistent recurrence; inter-layer dropout
+    (Philox, recomputed in backward) in train mode.  weights = the layer-major list
+    [w_ih, w_hh, b_ih, b_hh] (+ [w_ih_r, w_hh_r, b_ih_r, b_hh_r] when bidirectional) * L."""
 
     @staticmethod
-    def forward(ctx, x, H, L, dropout, seed, *weights):
+    def forward(ctx, x, H, L, ndir, dropout, seed, *weights):
         x = _need(x, "lstm input")
         B, T, _ = x.shape
         N = B * T
         l = lib()
         xbuf, err = _lstm_ws(B, H)
+        nw = 4 * ndir
         saved, inputs, seeds = [], [], []
         h = x
         for li in range(L):
-            w = [_need(t, "lstm weight") for t in weights[8 * li:8 * li + 8]]
+            w = [_need(t, "lstm weight") for t in weights[nw * li:nw * li + nw]]
             din = h.shape[-1]
-            G = torch.empty(N, 8 * H, device=x.device, dtype=torch.float32)
-            for d in range(2):
+            G = torch.empty(N, 4 * H * ndir, device=x.device, dtype=torch.float32)
+            for d in range(ndir):
                 wi, _, bi, bh = w[4 * d:4 * d + 4]
-                gemm(0, 1, N, 4 * H, din, _p(h), din, _p(wi), din, _p(G, 4 * H * d), 8 * H,
+                gemm(0, 1, N, 4 * H, din, _p(h), din, _p(wi), din, _p(G, 4 * H * d), 4 * H * ndir,
                      bias1=_p(bi), bias2=_p(bh))
-            Cs = torch.empty(N, 2 * H, device=x.device, dtype=torch.float32)
-            Y = torch.empty(B, T, 2 * H, device=x.device, dtype=torch.float32)
-            check(l.mlvae_lstm_fwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(Y),
-                                   _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_fwd")
+            Cs = torch.empty(N, H * ndir, device=x.device, dtype=torch.float32)
+            Y = torch.empty(B, T, H * ndir, device=x.device, dtype=torch.float32)
+            if ndir == 2:
+                check(l.mlvae_lstm_fwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(Y),
+                                       _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_fwd")
+            else:
+                check(l.mlvae_lstm1_fwd(_prec(), B, T, H, _p(w[1]), _p(G), _p(Cs), _p(Y), None,
+                                        _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm1_fwd")
             inputs.append(h)
             saved += [G, Cs, Y]
             h = Y
@@ -306,12 +312,13 @@ class BiLSTMFn(torch.autograd.Function):
             else:
                 seeds.append(None)
         ctx.save_for_backward(*inputs, *saved, *weights)
-        ctx.H, ctx.L, ctx.dropout, ctx.seeds = H, L, dropout, seeds
+        ctx.H, ctx.L, ctx.ndir, ctx.dropout, ctx.seeds = H, L, ndir, dropout, seeds
         return h
 
     @staticmethod
     def backward(ctx, dy):
-        H, L = ctx.H, ctx.L
+        H, L, ndir = ctx.H, ctx.L, ctx.ndir
+        nw, GL = 4 * ndir, 4 * H * ndir
         t = ctx.saved_tensors
         inputs, saved, weights = t[:L], t[L:4 * L], t[4 * L:]
         dy = _need(dy, "lstm grad").clone()
@@ -323,45 +330,151 @@ class BiLSTMFn(torch.autograd.Function):
         dx = None
         for li in range(L - 1, -1, -1):
             G, Cs, Y = saved[3 * li:3 * li + 3]
-            w = weights[8 * li:8 * li + 8]
+            w = weights[nw * li:nw * li + nw]
             xin = inputs[li]
             din = xin.shape[-1]
-            check(l.mlvae_lstm_bwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(dy),
-                                   _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_bwd")
+            if ndir == 2:
+                check(l.mlvae_lstm_bwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(dy),
+                                       _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_bwd")
+            else:
+                check(l.mlvae_lstm1_bwd(_prec(), B, T, H, _p(w[1]), _p(G), _p(Cs), _p(dy), None,
+                                        _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm1_bwd")
             dx = torch.empty(B, T, din, device=dy.device, dtype=torch.float32)
-            for d in range(2):
+            for d in range(ndir):
                 wi = w[4 * d]
-                gemm(0, 0, N, din, 4 * H, _p(G, 4 * H * d), 8 * H, _p(wi), din, _p(dx), din,
+                gemm(0, 0, N, din, 4 * H, _p(G, 4 * H * d), GL, _p(wi), din, _p(dx), din,
                      beta=1.0 if d else 0.0)
                 gwi = torch.empty_like(wi)
-                gemm(1, 0, 4 * H, din, N, _p(G, 4 * H * d), 8 * H, _p(xin), din, _p(gwi), din)
+                gemm(1, 0, 4 * H, din, N, _p(G, 4 * H * d), GL, _p(xin), din, _p(gwi), din)
                 gwh = torch.empty_like(w[4 * d + 1])
-                gemm(1, 0, 4 * H, H, N, _p(G, 4 * H * d), 8 * H, _p(Y, H * d), 2 * H, _p(gwh), H,
+                # dW_hh = sum_t dG_t^T h_{t-1} (forward) / h_{t+1} (reverse): time-shifted B rows
+                gemm(1, 0, 4 * H, H, N, _p(G, 4 * H * d), GL, _p(Y, H * d), H * ndir, _p(gwh), H,
                      kshift_T=T, kshift=1 if d else -1)
                 gbi = torch.empty_like(w[4 * d + 2])
                 gbh = torch.empty_like(w[4 * d + 3])
-                colsum(N, 4 * H, _p(G, 4 * H * d), 8 * H, _p(gbi), _p(gbh))
-                base = 8 * li + 4 * d
+                colsum(N, 4 * H, _p(G, 4 * H * d), GL, _p(gbi), _p(gbh))
+                base = nw * li + 4 * d
                 dW[base:base + 4] = [gwi, gwh, gbi, gbh]
             if li > 0 and ctx.seeds[li - 1] is not None:
                 _dropout(dx, dx, ctx.seeds[li - 1], ctx.dropout)
             dy = dx
         if int(err.item()) != 0:
             raise RuntimeError("LSTM recurrence hand-off timed out")
-        return (dx, None, None, None, None, *dW)
+        return (dx, None, None, None, None, None, *dW)
 
 
-def bilstm(x, lstm_module, train):
-    """Run an nn.LSTM's parameters through the HIP recurrence (its own forward is not used)."""
+def lstm(x, lstm_module, train):
+    """Run an nn.LSTM's parameters (batch_first, uni- or bidirectional) through the HIP
+    recurrence; its own forward is not used."""
+    if not lstm_module.batch_first:
+        raise ValueError("the HIP LSTM path is batch_first only (as every reference LSTM)")
     H, L = lstm_module.hidden_size, lstm_module.num_layers
+    ndir = 2 if lstm_module.bidirectional else 1
     weights = []
     for li in range(L):
-        for sfx in ("", "_reverse"):
+        for sfx in ("", "_reverse")[:ndir]:
             for kind in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
                 weights.append(getattr(lstm_module, f"{kind}_l{li}{sfx}"))
     p = float(lstm_module.dropout) if train else 0.0
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-    return BiLSTMFn.apply(x, H, L, p, seed, *weights)
+    return LSTMFn.apply(x, H, L, ndir, p, seed, *weights)
+
+
+def bilstm(x, lstm_module, train):
+    """The decoder's bidirectional nn.LSTM (ref:src/modules/decoder.py:22)."""
+    return lstm(x, lstm_module, train)
+
+
+# --------------------------------------------------------------------------- MD-VAE upstream losses
+def _md_err():
+    dev = torch.cuda.current_device()
+    e = _ws.get((dev, "md_err"))
+    if e is None:
+        e = torch.zeros(1, device="cuda", dtype=torch.int32)
+        _ws[(dev, "md_err")] = e
+    return e
+
+
+def _raise_md(err):
+    code = int(err.item())
+    if code:
+        err.zero_()
+        raise AssertionError(
+            "phoneme-recogniser targets: " +
+            ("boundaries do not give one segment per phoneme from frame 0 " if code & 2 else "") +
+            ("phoneme id outside [0, n_phonemes + 2)" if code & 4 else "") +
+            " (ref:src/modules/phoneme_recognizer.py:65-67)")
+
+
+class PhnBceFn(torch.autograd.Function):
+    """PhonemeRecognizer.compute_losses on libmlvae (ref:src/modules/phoneme_recognizer.py:35-81):
+    [B,T,C] BCE-with-logits against the boundary-expanded canonical phoneme sequence."""
+
+    @staticmethod
+    def forward(ctx, out, feat_lens, phn, phn_lens, boundary):
+        out = _need(out, "recogniser output")
+        B, T, C = out.shape
+        fl = _need(feat_lens.to(out.device, torch.float32), "feat_lens")
+        pl = _need(phn_lens.to(out.device, torch.float32), "phn_lens")
+        bnd = _need(boundary.to(out.device, torch.float32), "boundary_seqs")
+        ids = phn.to(out.device, torch.int64).contiguous()
+        loss = torch.empty_like(out)
+        err = _md_err()
+        check(lib().mlvae_phn_bce(B, T, C, _p(out), C, _p(fl), ids.data_ptr(), ids.shape[1], _p(pl),
+                                  _p(bnd), _p(loss), None, None, _p(err), _stream()), "phn_bce")
+        _raise_md(err)  # the reference asserts on the host too (one sync per batch, not per utterance)
+        ctx.save_for_backward(out, fl, ids, pl, bnd)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        out, fl, ids, pl, bnd = ctx.saved_tensors
+        B, T, C = out.shape
+        dloss = _need(dloss, "grad")
+        dout = torch.empty_like(out)
+        err = _md_err()
+        check(lib().mlvae_phn_bce(B, T, C, _p(out), C, _p(fl), ids.data_ptr(), ids.shape[1], _p(pl),
+                                  _p(bnd), None, _p(dloss), _p(dout), _p(err), _stream()), "phn_bce_bwd")
+        return dout, None, None, None, None
+
+
+def phn_bce(out, feat_lens, phn, phn_lens, boundary):
+    return PhnBceFn.apply(out, feat_lens, phn, phn_lens, boundary)
+
+
+class BoundaryHeadsFn(torch.autograd.Function):
+    """BoundaryDetector after its FC heads (ref:src/modules/boundary_detector.py:42-97): Softplus
+    + 1e-5, Beta(1, 9) KL, ten Kumaraswamy draws; returns (boundary_v, bce, kld).  u = the ten
+    U(0,1) draws [10, B, T] (None: Philox keyed by seed and element index)."""
+
+    @staticmethod
+    def forward(ctx, za, zb, y, u, seed):
+        za, zb = _need(za, "alpha head"), _need(zb, "beta head")
+        y = _need(y.to(za.device, torch.float32), "boundary_seqs")
+        u = _need(u, "uniforms") if u is not None else None
+        v, bce, kld = torch.empty_like(za), torch.empty_like(za), torch.empty_like(za)
+        check(lib().mlvae_boundary_fwd(za.numel(), _p(za), _p(zb), _p(y), _p(u) if u is not None else None,
+                                       seed, 0, _p(v), _p(bce), _p(kld), _stream()), "boundary_fwd")
+        ctx.save_for_backward(za, zb, y, *([u] if u is not None else []))
+        ctx.seed, ctx.has_u = seed, u is not None
+        return v, bce, kld
+
+    @staticmethod
+    def backward(ctx, dv, dbce, dkld):
+        t = ctx.saved_tensors
+        za, zb, y = t[:3]
+        u = t[3] if ctx.has_u else None
+        grads = [None if g is None else _need(g, "grad") for g in (dv, dbce, dkld)]
+        dza, dzb = torch.empty_like(za), torch.empty_like(zb)
+        check(lib().mlvae_boundary_bwd(za.numel(), _p(za), _p(zb), _p(y), _p(u) if u is not None else None,
+                                       ctx.seed, 0, *[(_p(g) if g is not None else None) for g in grads],
+                                       _p(dza), _p(dzb), _stream()), "boundary_bwd")
+        return dza, dzb, None, None, None
+
+
+def boundary_heads(za, zb, boundary, u=None):
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if u is None else 0
+    return BoundaryHeadsFn.apply(za, zb, boundary, u, seed)
 
 
 # --------------------------------------------------------------------------- GMM-VAE / H-VAE

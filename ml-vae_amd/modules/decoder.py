@@ -2,7 +2,7 @@
 
 rnn: a bidirectional L-layer LSTM.  An nn.LSTM instance is kept as the parameter holder so
 initialisation and state_dict keys (rnn.weight_ih_l0, ...) match the reference; its forward is
-not used -- the recurrence runs in the persistent HIP kernels (mlvae_hip.ops.BiLSTMFn).
+not used -- the recurrence runs in the persistent HIP kernels (mlvae_hip.ops.LSTMFn).
 mean_fc / log_var_fc: FCBlock heads.  compute_recon_loss: Gaussian NLL ('likelihood', the
 default) or MSE, per element; anything else raises ValueError('Invalid loss type: ...').
 """
