@@ -177,6 +177,22 @@ int mlvae_boundary_bwd(size_t n, const float* za, const float* zb, const float* 
                        unsigned long long seed, unsigned long long offset, const float* dv,
                        const float* dbce, const float* dkld, float* dza, float* dzb, void* stream);
 
+/* MD-VAE Viterbi decode (csrc/decode.hip): decode_plvl_md_lbl_seqs_full
+ * (ref:src/utils/decode_utils.py:374-565, run in the MD-VAE forward at ref:src/models/MD_VAE/
+ * model.py:133-141).  logits [B,T,N] (phoneme recogniser output, row stride ldl), boundary_v
+ * [B,T], pi_logits [B,T,2], prior [N], seqs [B,L] int64 canonical ids, feat_lens / seq_lens [B]
+ * relative, weight = dec_weight.  Outputs (int32): boundary_out [B,T] decoded boundaries (0/1),
+ * flvl_out [B,T] frame-level and plvl_out [B,L] phoneme-level mispronunciation labels (-1 past
+ * T_i / L_i), lens_out [B,2] = (T_i, L_i).  ws: mlvae_viterbi_workspace_size(B,T,L) bytes (the
+ * argmax path map).  *err bits: 8 = the backtrack did not end at (l, t) = (0, 0) (the reference's
+ * assert), 16 = T_i or L_i empty / L_i > 1024.  L <= 1024. */
+size_t mlvae_viterbi_workspace_size(int B, int T, int L);
+int mlvae_viterbi_md(int B, int T, int N, int L, const float* logits, int ldl, const float* boundary_v,
+                     const float* pi_logits, const float* prior, const long long* seqs,
+                     const float* feat_lens, const float* seq_lens, float weight, void* ws,
+                     size_t ws_bytes, int* boundary_out, int* flvl_out, int* plvl_out, int* lens_out,
+                     int* err, void* stream);
+
 /* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
  * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */
 int mlvae_elbo_partials_count(int B, int T, int C);

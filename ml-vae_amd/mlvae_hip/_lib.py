@@ -38,6 +38,8 @@ _SIGS = {
     "mlvae_lstm_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_fwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_ex": [I, I, I, I, P, P, P, P, P, P, P, SZ, P, P],
+    "mlvae_viterbi_workspace_size": [I, I, I],
+    "mlvae_viterbi_md": [I, I, I, I, P, I, P, P, P, P, P, P, F, P, SZ, P, P, P, P, P, P],
     "mlvae_phn_bce": [I, I, I, P, I, P, P, I, P, P, P, P, P, P, P],
     "mlvae_boundary_fwd": [SZ, P, P, P, P, U64, U64, P, P, P, P],
     "mlvae_boundary_bwd": [SZ, P, P, P, P, U64, U64, P, P, P, P, P, P],
@@ -95,6 +97,7 @@ _RESTYPE = {
     "mlvae_gemm_bf16_workspace_size": SZ,
     "mlvae_skinny_tn_workspace_size": SZ,
     "mlvae_encoder_workspace_size": SZ,
+    "mlvae_viterbi_workspace_size": SZ,
 }
 
 _lib = None
