@@ -24,6 +24,10 @@ DEFAULT_RUN_OPTS = {
     "nonfinite_patience": 3,
     "noprogressbar": True,
     "ckpt_interval_minutes": 0,
+    "distributed_launch": False,   # brain.distributed.init_from_env fills rank / world_size
+    "distributed_backend": None,
+    "rank": 0,
+    "world_size": 1,
 }
 
 
@@ -190,5 +194,7 @@ class Brain:
 
     def make_dataloader(self, dataset, stage, **loader_kwargs):
         if hasattr(dataset, "batches"):
+            if self.world_size > 1:  # this rank's slice of every global batch
+                loader_kwargs = dict(loader_kwargs, rank=self.rank, world=self.world_size)
             return dataset.batches(stage=stage, **loader_kwargs)
         return dataset

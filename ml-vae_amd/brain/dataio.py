@@ -12,17 +12,25 @@ def length_to_mask(length, max_len=None, dtype=None, device=None):
 
 
 class PaddedBatch(dict):
-    """dict of fields; tensor fields are (padded [B, Tmax, ...], relative lengths [B])."""
+    """dict of fields; tensor fields (sequences: feat, phoneme / boundary sequences, ...) are
+    (padded [B, Lmax, ...], relative lengths [B]); other fields are lists."""
 
     def __init__(self, examples, key="feat"):
-        feats = [e[key] for e in examples]
-        tmax = max(f.shape[0] for f in feats)
-        out = torch.zeros(len(feats), tmax, *feats[0].shape[1:], dtype=feats[0].dtype)
-        for i, f in enumerate(feats):
-            out[i, :f.shape[0]] = f
-        lens = torch.tensor([f.shape[0] / tmax for f in feats], dtype=torch.float32)
         super().__init__()
-        self[key] = (out, lens)
+        keys = [k for k in examples[0] if k != "id"]
+        if key not in keys:
+            keys.insert(0, key)
+        for k in keys:
+            vals = [e[k] for e in examples]
+            if all(torch.is_tensor(v) and v.dim() >= 1 for v in vals):
+                tmax = max(v.shape[0] for v in vals)
+                out = torch.zeros(len(vals), tmax, *vals[0].shape[1:], dtype=vals[0].dtype)
+                for i, v in enumerate(vals):
+                    out[i, :v.shape[0]] = v
+                lens = torch.tensor([v.shape[0] / tmax for v in vals], dtype=torch.float32)
+                self[k] = (out, lens)
+            else:
+                self[k] = vals
         self["id"] = [e.get("id", str(i)) for i, e in enumerate(examples)]
 
     def to(self, device):

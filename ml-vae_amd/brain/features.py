@@ -38,6 +38,14 @@ class InputNormalization(torch.nn.Module):
         stds = torch.clamp(var.sqrt(), min=self.eps)
         cur_mean = means.mean(0)
         cur_std = stds.mean(0)
+        from brain.distributed import all_reduce_sum_, world_size
+        if self.training and world_size() > 1:  # data parallel: the statistics of the global batch
+            acc = torch.cat([means.sum(0).reshape(-1), stds.sum(0).reshape(-1),
+                             torch.tensor([float(B)], device=x.device, dtype=means.dtype)])
+            all_reduce_sum_(acc)
+            k = cur_mean.numel()
+            cur_mean = (acc[:k] / acc[-1]).reshape(cur_mean.shape)
+            cur_std = (acc[k:2 * k] / acc[-1]).reshape(cur_std.shape)
         if self.training:
             if self.count == 0:
                 self.glob_mean, self.glob_std = cur_mean, cur_std

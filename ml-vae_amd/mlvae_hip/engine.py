@@ -1029,7 +1029,13 @@ class VAEEngine:
         return w.loss
 
     def eval_step(self, x, lens, eps=None):
-        w = self.forward(x, lens, eps=eps, train=False)
+        """Forward only; under data parallelism the returned [kld, recon, loss] is the global
+        batch's (each rank's share uses the all-reduced frame count; the shares are summed)."""
+        with self._main():
+            w = self.forward(x, lens, eps=eps, train=False)
+            if self.world > 1:
+                from . import dist as mdist
+                mdist.allreduce_loss(w.loss, self.process_group)
         self.rng_step += 1
         return w.loss
 

@@ -80,6 +80,10 @@ class MDModel(Brain):
                 max_grad_norm=self.max_grad_norm,
                 seed=int(torch.randint(0, 2 ** 62, (1,)).item()))
             self.optimizers = {"optimizer": EngineOptimizer(self.engine)}
+            if self.world_size > 1:  # data parallel: global offsets, broadcast weights, grad all-reduce
+                from mlvae_hip import dist as mdist
+                mdist.attach(self.engine, self.rank, self.world_size,
+                             int(getattr(self.hparams, "batch_size", 8)))
         else:
             from mlvae_hip import optim as hip_optim
             self.optimizers = {}
@@ -112,6 +116,12 @@ class MDModel(Brain):
         outputs = self.compute_forward(batch, Stage.TRAIN)
         loss = self.compute_objectives(outputs, batch, Stage.TRAIN)
         loss.backward()
+        if self.world_size > 1:  # module mode under DP: DDP's mean of the ranks' gradients
+            import torch.distributed as tdist
+            for p_ in self.modules.parameters():
+                if p_.grad is not None:
+                    tdist.all_reduce(p_.grad)
+                    p_.grad /= self.world_size
         opts = list(self.optimizers.values())
         if self.check_gradients(loss):
             for opt in opts:
@@ -210,17 +220,20 @@ class MDModel(Brain):
             epoch = self.hparams.epoch_counter.current
         log = self._collect_metrics(stage_loss)
         if stage in (Stage.TRAIN, Stage.VALID):
-            self.train_logger.log_stats(stats_meta={"stage": name, "epoch": epoch},
-                                        **{f"{name}_stats": log})
+            if self.rank == 0:
+                self.train_logger.log_stats(stats_meta={"stage": name, "epoch": epoch},
+                                            **{f"{name}_stats": log})
             if stage == Stage.VALID:
                 max_keys = [self.hparams.max_key] if getattr(self.hparams, "max_key", None) else []
                 min_keys = [self.hparams.min_key] if getattr(self.hparams, "min_key", None) else []
                 if not max_keys and not min_keys:
                     raise ValueError("no max_key or min_key provided")
-                if self.checkpointer is not None:
+                if self.checkpointer is not None and self.rank == 0:  # rank 0 writes
                     self.checkpointer.save_and_keep_only(meta=log, max_keys=max_keys,
                                                          min_keys=min_keys)
-        if stage == Stage.TEST:
+                from brain.distributed import barrier
+                barrier()
+        if stage == Stage.TEST and self.rank == 0:
             out = Path(self.hparams.output_dir) / "test_output"
             out.mkdir(parents=True, exist_ok=True)
             with open(out / "test_metrics.txt", "w") as f:

@@ -13,6 +13,9 @@ from utils.data_io import prepare_datasets
 
 def prepare_experiment(args, prepare_exp_dir):
     hparams_file, run_opts, overrides = brain.parse_arguments(args)
+    # data-parallel launch (torch.distributed.run): process group, rank's device (brain.distributed)
+    from brain.distributed import init_from_env, is_main
+    init_from_env(run_opts)
     parsed = yaml.safe_load(_strip_tags(overrides)) if overrides else None
     extra_overrides = {}
     if parsed and "extra_overrides" in parsed:
@@ -25,12 +28,17 @@ def prepare_experiment(args, prepare_exp_dir):
         hparams = load_hyperpyyaml(fin, [extra_overrides, overrides])
     recursive_update(hparams, extra_overrides)
 
-    if prepare_exp_dir:
+    if prepare_exp_dir and is_main():
         brain.create_experiment_directory(experiment_directory=hparams["output_dir"],
                                           hyperparams_to_save=hparams_file,
                                           overrides=[extra_overrides, overrides])
     prepared = {"hparams": hparams}
-    importlib.import_module(f"datasets.{hparams['dataset']}.prepare").prepare(**hparams["prepare"])
+    try:
+        prep = importlib.import_module(f"datasets.{hparams['dataset']}.prepare")
+    except ModuleNotFoundError:
+        prep = None  # a corpus the reference computed already: utils.data_io reads its pickles
+    if prep is not None:
+        prep.prepare(**hparams["prepare"])
     datasets, label_encoder = prepare_datasets(hparams)
     prepared["datasets"] = datasets
     if "model_class" in hparams:
