@@ -193,6 +193,26 @@ int mlvae_viterbi_md(int B, int T, int N, int L, const float* logits, int ldl, c
                      size_t ws_bytes, int* boundary_out, int* flvl_out, int* plvl_out, int* lens_out,
                      int* err, void* stream);
 
+/* Conv1d encoder layers (csrc/conv.hip), BASELINE.json configs[3]'s "Conv1d encoder variant":
+ * the reference has none (SURVEY.md Appendix A); semantics = torch.nn.Conv1d(Cin, Cout, K,
+ * padding=(K-1)/2) over each utterance of the batch-first frames [B, T, C] (row b*T + t), zero
+ * outside [0, T).  This replaces the encoder's Linear layers (ref:src/modules/vanilla_vae.py:13-16,
+ * FCBlock ref:src/modules/fc_block.py:4-21) in modules/conv_vae.py.  w: torch layout
+ * [Cout][Cin][K] fp32; activations fp32, bf16 MFMA operands, fp32 accumulate.
+ *   fwd:   y = act(conv(x) + bias)                      act: 1 = LeakyReLU(0.01)
+ *   dgrad: dx = conv^T(dy) [* lrelu'(aux)]              (aux = the layer input's LReLU output)
+ *   wgrad: dw = sum over frames, db = column sums of dy  (overwritten; deterministic)
+ * Limits: K odd <= 9, Cin % 4 == 0 and <= 128, Cout % 16 == 0 and <= 128, 16-byte aligned
+ * rows; wgrad: Cout in {16, 32, 64}, K * roundup(Cin, 16) <= 512 (mlvae_conv1d_supported). */
+int mlvae_conv1d_supported(int Cin, int Cout, int K);
+int mlvae_conv1d_fwd(int B, int T, int Cin, int Cout, int K, const float* x, int ldx, const float* w,
+                     const float* bias, int act, float* y, int ldy, void* stream);
+int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const float* dy, int lddy, const float* w,
+                       const float* aux, int ldaux, float* dx, int lddx, void* stream);
+size_t mlvae_conv1d_wgrad_workspace_size(int B, int T, int Cin, int Cout, int K);
+int mlvae_conv1d_wgrad(int B, int T, int Cin, int Cout, int K, const float* dy, int lddy, const float* x,
+                       int ldx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
+
 /* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
  * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */
 int mlvae_elbo_partials_count(int B, int T, int C);

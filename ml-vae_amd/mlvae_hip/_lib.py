@@ -41,6 +41,11 @@ _SIGS = {
     "mlvae_viterbi_workspace_size": [I, I, I],
     "mlvae_viterbi_md": [I, I, I, I, P, I, P, P, P, P, P, P, F, P, SZ, P, P, P, P, P, P],
     "mlvae_phn_bce": [I, I, I, P, I, P, P, I, P, P, P, P, P, P, P],
+    "mlvae_conv1d_supported": [I, I, I],
+    "mlvae_conv1d_fwd": [I, I, I, I, I, P, I, P, P, I, P, I, P],
+    "mlvae_conv1d_dgrad": [I, I, I, I, I, P, I, P, P, I, P, I, P],
+    "mlvae_conv1d_wgrad_workspace_size": [I, I, I, I, I],
+    "mlvae_conv1d_wgrad": [I, I, I, I, I, P, I, P, I, P, P, P, SZ, P],
     "mlvae_boundary_fwd": [SZ, P, P, P, P, U64, U64, P, P, P, P],
     "mlvae_boundary_bwd": [SZ, P, P, P, P, U64, U64, P, P, P, P, P, P],
     "mlvae_lstm1_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
@@ -91,6 +96,7 @@ _SIGS = {
 }
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
+    "mlvae_conv1d_wgrad_workspace_size": SZ,
     "mlvae_gemm_workspace_size": SZ,
     "mlvae_gemm_ex_workspace_size": SZ,
     "mlvae_colsum_workspace_size": SZ,

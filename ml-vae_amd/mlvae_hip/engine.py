@@ -51,6 +51,11 @@ class VAEConfig:
     adam_eps: float = 1e-8
     max_grad_norm: float = 5.0
     prec: str = "fp32"      # "fp32" (exact parity mode) or "bf16" (bf16 MFMA operands)
+    enc_conv: int = 0       # Conv1d encoder kernel size (modules/conv_vae.py, configs[3]); 0 = Linear
+
+    @property
+    def enc_prefix(self):
+        return "encoder.conv.0.blocks" if self.enc_conv else "encoder.fc.0.blocks"
 
     def check(self):
         for k in ("F", "E", "Z", "H", "C"):
@@ -61,6 +66,15 @@ class VAEConfig:
             raise ValueError(f"Invalid loss type: {self.loss_type}")
         if self.prec not in PREC:
             raise ValueError(f"prec must be one of {list(PREC)}")
+        if self.enc_conv:
+            if self.enc_conv % 2 != 1:
+                raise ValueError("enc_conv: the Conv1d kernel size must be odd")
+            if self.prec != "bf16":
+                raise ValueError("the Conv1d encoder kernels use bf16 operands: prec must be 'bf16'")
+            if not (lib().mlvae_conv1d_supported(self.F, self.E, self.enc_conv) and
+                    lib().mlvae_conv1d_supported(self.E, self.E, self.enc_conv)):
+                raise ValueError(f"Conv1d encoder F={self.F} E={self.E} K={self.enc_conv} not supported "
+                                 "(include/mlvae.h mlvae_conv1d_supported)")
         return self
 
 
@@ -69,10 +83,11 @@ def reference_shapes(cfg):
     (encoder: ref:src/modules/vanilla_vae.py:13-19; decoder: ref:src/modules/decoder.py:14-17)."""
     F, E, Z, H, L, C = cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C
     s = OrderedDict()
-    s["encoder.fc.0.blocks.0.weight"] = (E, F)
-    s["encoder.fc.0.blocks.0.bias"] = (E,)
-    s["encoder.fc.0.blocks.2.weight"] = (E, E)
-    s["encoder.fc.0.blocks.2.bias"] = (E,)
+    k, ep = (cfg.enc_conv,), cfg.enc_prefix
+    s[f"{ep}.0.weight"] = (E, F) + (k if cfg.enc_conv else ())
+    s[f"{ep}.0.bias"] = (E,)
+    s[f"{ep}.2.weight"] = (E, E) + (k if cfg.enc_conv else ())
+    s[f"{ep}.2.bias"] = (E,)
     s["encoder.mean_fc.weight"] = (Z, E)
     s["encoder.mean_fc.bias"] = (Z,)
     s["encoder.log_var_fc.weight"] = (Z, E)
@@ -95,8 +110,8 @@ def reference_shapes(cfg):
 def _engine_order(cfg):
     """Flat-buffer order: groups listed together are laid out back to back (no padding),
     so one launch can read them as a single stacked matrix/vector."""
-    g = [["encoder.fc.0.blocks.0.weight"], ["encoder.fc.0.blocks.0.bias"],
-         ["encoder.fc.0.blocks.2.weight"], ["encoder.fc.0.blocks.2.bias"],
+    ep = cfg.enc_prefix
+    g = [[f"{ep}.0.weight"], [f"{ep}.0.bias"], [f"{ep}.2.weight"], [f"{ep}.2.bias"],
          ["encoder.mean_fc.weight", "encoder.log_var_fc.weight"],
          ["encoder.mean_fc.bias", "encoder.log_var_fc.bias"]]
     for l in range(cfg.L):
@@ -237,6 +252,9 @@ class _Work:
         self.pke = empty(max(self.nke, 1), **f)  # fused encoder's KL partials
         ewb = l.mlvae_encoder_workspace_size(B, T, F, E, Z) if self.enc_fused else 0
         self.enc_ws = empty(ewb // 4 + 1, **f)
+        # Conv1d encoder: weight-gradient slabs of the two layers (main and side stream)
+        self.conv_ws = ([empty(l.mlvae_conv1d_wgrad_workspace_size(B, T, cin, E, cfg.enc_conv) // 4 + 1, **f)
+                         for cin in (F, E)] if cfg.enc_conv else None)
         self.loss = torch.zeros(3, device=device, dtype=torch.float32)  # own tensor: returned to the caller   # [kld_loss, recon_loss, total]
         self.count = torch.zeros(1, device=device, dtype=torch.int32)
         # GEMM split-K workspace: the largest any call of the step asks for
@@ -308,7 +326,7 @@ class VAEEngine:
                      if self.fused_heads else None)
         # bf16 mode: the encoder (+ reparameterisation + KL) runs as two fused kernels
         # (encoder.hip) and the bottom layer's products on skinny kernels (skinny.hip)
-        self.fused_encoder = (cfg.prec == "bf16" and
+        self.fused_encoder = (cfg.prec == "bf16" and not cfg.enc_conv and
                               bool(lib().mlvae_encoder_supported(cfg.F, cfg.E, cfg.Z)))
         if cfg.prec == "bf16":
             for li in range(1, cfg.L):
@@ -373,9 +391,14 @@ class VAEEngine:
         """Build an engine whose flat buffer becomes the storage of the given modules'
         parameters (VanillaVAE + Decoder, as the recipe yaml builds them): after this call
         module.parameters() are views of engine.flat and their .grad views of engine.grad."""
-        lin0 = encoder.fc[0].linear_plan()[0][0]
         heads = decoder.mean_fc.linear_plan()
-        cfg = VAEConfig(F=lin0.in_features, E=lin0.out_features,
+        if hasattr(encoder, "conv"):  # modules/conv_vae.py ConvVAE
+            c0 = encoder.conv[0].conv_plan()[0][0]
+            F, E, kconv = c0.in_channels, c0.out_channels, c0.kernel_size[0]
+        else:
+            lin0 = encoder.fc[0].linear_plan()[0][0]
+            F, E, kconv = lin0.in_features, lin0.out_features, 0
+        cfg = VAEConfig(F=F, E=E, enc_conv=kconv,
                         Z=encoder.mean_fc.out_features, H=decoder.rnn.hidden_size,
                         L=decoder.rnn.num_layers, C=heads[0][0].out_features,
                         dropout=float(decoder.rnn.dropout), loss_type=decoder.loss_type,
@@ -404,7 +427,7 @@ class VAEEngine:
                     bound = 1.0 / math.sqrt(self.cfg.H)
                 else:
                     wshape = self.layout.shapes[name[:-4] + "weight"] if name.endswith("bias") else shp
-                    bound = 1.0 / math.sqrt(wshape[1])
+                    bound = 1.0 / math.sqrt(math.prod(wshape[1:]))  # fan_in (Conv1d: Cin * K)
                 v = self.view(name)
                 v.uniform_(-bound, bound, generator=g)
         return self
@@ -601,12 +624,21 @@ class VAEEngine:
             if eps_t is None:
                 check(l.mlvae_randn(N * Z, self.seed, eps_off, _p(w.eps), s), "mlvae_randn")
             # ---- encoder (ref:src/modules/vanilla_vae.py:21-28)
-            self._mm(w, 0, 1, N, E, Fd, X, Fd, self._ptr("encoder.fc.0.blocks.0.weight"), Fd,
-                     _p(w.E1), E, B_bf=wb("encoder.fc.0.blocks.0.weight"),
-                     bias1=self._ptr("encoder.fc.0.blocks.0.bias"), epi=EPI_LRELU)
-            self._mm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
-                     _p(w.E2), E, B_bf=wb("encoder.fc.0.blocks.2.weight"),
-                     bias1=self._ptr("encoder.fc.0.blocks.2.bias"), epi=EPI_LRELU)
+            ep = cfg.enc_prefix
+            if cfg.enc_conv:  # Conv1d variant (modules/conv_vae.py, csrc/conv.hip)
+                K = cfg.enc_conv
+                with self._timed("conv_fwd"):
+                    check(l.mlvae_conv1d_fwd(B, T, Fd, E, K, X, Fd, self._ptr(f"{ep}.0.weight"),
+                                             self._ptr(f"{ep}.0.bias"), 1, _p(w.E1), E, s), "conv1d_fwd")
+                    check(l.mlvae_conv1d_fwd(B, T, E, E, K, _p(w.E1), E, self._ptr(f"{ep}.2.weight"),
+                                             self._ptr(f"{ep}.2.bias"), 1, _p(w.E2), E, s), "conv1d_fwd")
+            else:
+                self._mm(w, 0, 1, N, E, Fd, X, Fd, self._ptr(f"{ep}.0.weight"), Fd,
+                         _p(w.E1), E, B_bf=wb(f"{ep}.0.weight"),
+                         bias1=self._ptr(f"{ep}.0.bias"), epi=EPI_LRELU)
+                self._mm(w, 0, 1, N, E, E, _p(w.E1), E, self._ptr(f"{ep}.2.weight"), E,
+                         _p(w.E2), E, B_bf=wb(f"{ep}.2.weight"),
+                         bias1=self._ptr(f"{ep}.2.bias"), epi=EPI_LRELU)
             self._mm(w, 0, 1, N, 2 * Z, E, _p(w.E2), E, self._ptr("encoder.mean_fc.weight"), E,
                      _p(w.ML), 2 * Z, B_bf=wb("encoder.mean_fc.weight"), bias1=self._ptr("encoder.mean_fc.bias"))
             check(l.mlvae_reparam_kl_fwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(lens), _p(w.Zs),
@@ -948,15 +980,31 @@ class VAEEngine:
         self._mm(w, 0, 0, N, E, 2 * Z, _p(w.dML), 2 * Z, self._ptr("encoder.mean_fc.weight"), E,
                  _p(w.dE2), E, B_bf=wb("encoder.mean_fc.weight"), epi=EPI_DLRELU, aux=_p(w.E2), ldaux=E)
 
+        ep = cfg.enc_prefix
+        if cfg.enc_conv:  # Conv1d variant: weight gradients + the input gradient (csrc/conv.hip)
+            K = cfg.enc_conv
+
+            def wgc(cin, dy, xin, name, ws):
+                check(l.mlvae_conv1d_wgrad(B, T, cin, E, K, _p(dy), E, xin, cin, gp(f"{ep}.{name}.weight"),
+                                           gp(f"{ep}.{name}.bias"), _p(ws), ws.numel() * 4, self._stream()),
+                      "conv1d_wgrad")
+            self._side(lambda: wgc(E, w.dE2, _p(w.E1), 2, w.conv_ws[1]))
+            with self._timed("conv_bwd"):
+                check(l.mlvae_conv1d_dgrad(B, T, E, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1), E,
+                                           _p(w.dE1), E, s), "conv1d_dgrad")
+                wgc(Fd, w.dE1, _p(w.x), 0, w.conv_ws[0])
+            self._join_side()
+            return
+
         def wge1():
-            self._mm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp("encoder.fc.0.blocks.2.weight"), E)
-            self._colsum(w, N, E, _p(w.dE2), E, gp("encoder.fc.0.blocks.2.bias"))
+            self._mm(w, 1, 0, E, E, N, _p(w.dE2), E, _p(w.E1), E, gp(f"{ep}.2.weight"), E)
+            self._colsum(w, N, E, _p(w.dE2), E, gp(f"{ep}.2.bias"))
         self._side(wge1)
-        self._mm(w, 0, 0, N, E, E, _p(w.dE2), E, self._ptr("encoder.fc.0.blocks.2.weight"), E,
-                 _p(w.dE1), E, B_bf=wb("encoder.fc.0.blocks.2.weight"), epi=EPI_DLRELU,
+        self._mm(w, 0, 0, N, E, E, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), E,
+                 _p(w.dE1), E, B_bf=wb(f"{ep}.2.weight"), epi=EPI_DLRELU,
                  aux=_p(w.E1), ldaux=E)
-        self._mm(w, 1, 0, E, Fd, N, _p(w.dE1), E, _p(w.x), Fd, gp("encoder.fc.0.blocks.0.weight"), Fd)
-        self._colsum(w, N, E, _p(w.dE1), E, gp("encoder.fc.0.blocks.0.bias"))
+        self._mm(w, 1, 0, E, Fd, N, _p(w.dE1), E, _p(w.x), Fd, gp(f"{ep}.0.weight"), Fd)
+        self._colsum(w, N, E, _p(w.dE1), E, gp(f"{ep}.0.bias"))
         self._join_side()
 
     # ------------------------------------------------------------------ optimizer

@@ -120,6 +120,65 @@ def linear(x, w, b=None, act=False):
     return LinearFn.apply(x, w, b, act)
 
 
+# --------------------------------------------------------------------------- Conv1d encoder
+def _conv_ws(nbytes):
+    return _workspace(max(int(nbytes), 16), key="conv_wgrad")
+
+
+class Conv1dFn(torch.autograd.Function):
+    """y = act(conv1d(x) + b) over the time axis of batch-first frames x [B, T, Cin]; w
+    [Cout, Cin, K] (torch.nn.Conv1d layout, padding (K-1)/2 at each utterance's ends).
+    BASELINE.json configs[3]'s Conv1d encoder (csrc/conv.hip); bf16 operands, fp32 accumulate."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        x, w = _need(x, "conv1d x"), _need(w, "conv1d weight")
+        b = _need(b, "conv1d bias") if b is not None else None
+        if x.dim() != 3:
+            raise ValueError("conv1d: x must be [B, T, C]")
+        if _prec() != 1:
+            raise RuntimeError("the Conv1d encoder kernels use bf16 operands: set precision bf16")
+        B, T, Cin = x.shape
+        Cout, _, K = w.shape
+        y = torch.empty(B, T, Cout, device=x.device, dtype=torch.float32)
+        check(lib().mlvae_conv1d_fwd(B, T, Cin, Cout, K, _p(x), Cin, _p(w), _p(b) if b is not None else None,
+                                     1 if act else 0, _p(y), Cout, _stream()), "conv1d_fwd")
+        ctx.save_for_backward(x, w, y)
+        ctx.act, ctx.has_b = act, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = _need(dy, "conv1d grad")
+        B, T, Cin = x.shape
+        Cout, _, K = w.shape
+        if ctx.act:  # dpre = dy * lrelu'(y)
+            dpre = torch.empty_like(dy)
+            check(lib().mlvae_lrelu_bwd(dy.numel(), _p(dy), _p(y), _p(dpre), _stream()), "lrelu_bwd")
+        else:
+            dpre = dy
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            check(lib().mlvae_conv1d_dgrad(B, T, Cin, Cout, K, _p(dpre), Cout, _p(w), None, 0, _p(dx), Cin,
+                                           _stream()), "conv1d_dgrad")
+        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+            dw = torch.empty_like(w)
+            db = torch.empty(Cout, device=dy.device, dtype=torch.float32)
+            nb = lib().mlvae_conv1d_wgrad_workspace_size(B, T, Cin, Cout, K)
+            ws = _conv_ws(nb)
+            check(lib().mlvae_conv1d_wgrad(B, T, Cin, Cout, K, _p(dpre), Cout, _p(x), Cin, _p(dw), _p(db),
+                                           _p(ws), ws.numel() * ws.element_size(), _stream()), "conv1d_wgrad")
+            if not ctx.has_b:
+                db = None
+        return dx, dw, db, None
+
+
+def conv1d(x, w, b=None, act=False):
+    return Conv1dFn.apply(x, w, b, act)
+
+
 # --------------------------------------------------------------------------- ELBO part 1
 class ReparamKLFn(torch.autograd.Function):
     """z = eps*exp(lv/2) + mu and per-element KL (ref:src/modules/vanilla_vae.py:37-45);

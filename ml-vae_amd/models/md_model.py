@@ -49,11 +49,12 @@ class MDModel(Brain):
 
     def _fused_candidate(self, infos):
         from modules.decoder import Decoder
+        from modules.conv_vae import ConvVAE
         from modules.vanilla_vae import VanillaVAE
         from mlvae_hip import optim as hip_optim
         if set(self.modules.keys()) != {"encoder", "decoder"} or len(infos) != 1:
             return None
-        if not (isinstance(self.modules["encoder"], VanillaVAE) and
+        if not (isinstance(self.modules["encoder"], (VanillaVAE, ConvVAE)) and
                 isinstance(self.modules["decoder"], Decoder)):
             return None
         info = next(iter(infos.values()))

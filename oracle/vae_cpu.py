@@ -40,13 +40,16 @@ NEG_SLOPE = 0.01  # nn.LeakyReLU default, ref:src/modules/fc_block.py:11
 # --------------------------------------------------------------------------
 # configuration / parameter naming
 # --------------------------------------------------------------------------
-def param_shapes(F, enc, z, H, L, dec_fc):
-    """Reference parameter names and shapes, in Brain.modules.parameters() order."""
+def param_shapes(F, enc, z, H, L, dec_fc, enc_conv=0):
+    """Reference parameter names and shapes, in Brain.modules.parameters() order.
+    enc_conv = K > 0: the Conv1d encoder variant (configs[3]; no reference counterpart --
+    ml-vae_amd/modules/conv_vae.py), Conv1d weights [Cout, Cin, K] under ``encoder.conv.0``."""
     s = OrderedDict()
-    s["encoder.fc.0.blocks.0.weight"] = (enc, F)
-    s["encoder.fc.0.blocks.0.bias"] = (enc,)
-    s["encoder.fc.0.blocks.2.weight"] = (enc, enc)
-    s["encoder.fc.0.blocks.2.bias"] = (enc,)
+    pre, k = ("encoder.conv.0.blocks", (enc_conv,)) if enc_conv else ("encoder.fc.0.blocks", ())
+    s[f"{pre}.0.weight"] = (enc, F) + k
+    s[f"{pre}.0.bias"] = (enc,)
+    s[f"{pre}.2.weight"] = (enc, enc) + k
+    s[f"{pre}.2.bias"] = (enc,)
     s["encoder.mean_fc.weight"] = (z, enc)
     s["encoder.mean_fc.bias"] = (z,)
     s["encoder.log_var_fc.weight"] = (z, enc)
@@ -66,7 +69,7 @@ def param_shapes(F, enc, z, H, L, dec_fc):
     return s
 
 
-def init_params(F, enc, z, H, L, dec_fc, seed=123456, dtype=torch.float32):
+def init_params(F, enc, z, H, L, dec_fc, seed=123456, dtype=torch.float32, enc_conv=0):
     """PyTorch-default init (kaiming-uniform Linear, U(-1/sqrt(H),1/sqrt(H)) LSTM).
 
     Same distributions the reference gets from nn.Linear/nn.LSTM constructors
@@ -75,14 +78,14 @@ def init_params(F, enc, z, H, L, dec_fc, seed=123456, dtype=torch.float32):
     """
     g = torch.Generator().manual_seed(seed)
     out = OrderedDict()
-    for name, shp in param_shapes(F, enc, z, H, L, dec_fc).items():
+    for name, shp in param_shapes(F, enc, z, H, L, dec_fc, enc_conv).items():
         if ".rnn." in name:
             bound = 1.0 / math.sqrt(H)
         else:
-            fan_in = shp[1] if len(shp) == 2 else None
+            fan_in = math.prod(shp[1:]) if len(shp) >= 2 else None  # Conv1d: Cin * K
             if fan_in is None:  # bias: use the weight's fan_in
                 wname = name[:-4] + "weight"
-                fan_in = out[wname].shape[1]
+                fan_in = math.prod(out[wname].shape[1:])
             bound = 1.0 / math.sqrt(fan_in)
         out[name] = (torch.rand(shp, generator=g, dtype=torch.float64) * 2 - 1).mul(bound).to(dtype)
     return out
@@ -123,15 +126,40 @@ def lrelu(x):
 
 def encoder_forward(p, x, eps):
     """VanillaVAE.forward with injected eps (ref:src/modules/vanilla_vae.py:21-45).
-    fc = Seq(FCBlock([F,enc,enc]), LeakyReLU): Linear-LReLU-Linear, then LReLU."""
-    h = lrelu(Fn.linear(x, p["encoder.fc.0.blocks.0.weight"], p["encoder.fc.0.blocks.0.bias"]))
-    h = lrelu(Fn.linear(h, p["encoder.fc.0.blocks.2.weight"], p["encoder.fc.0.blocks.2.bias"]))
+    fc = Seq(FCBlock([F,enc,enc]), LeakyReLU): Linear-LReLU-Linear, then LReLU.
+    Conv1d variant (``encoder.conv.0.*`` present): the same with Conv1d(K, padding (K-1)/2)
+    over time on the [B, C, T] transpose (torch's own conv1d, cross-checked by conv1d_numpy)."""
+    if "encoder.conv.0.blocks.0.weight" in p:
+        h = x.transpose(1, 2)
+        for i in (0, 2):
+            wt = p[f"encoder.conv.0.blocks.{i}.weight"]
+            h = lrelu(Fn.conv1d(h, wt, p[f"encoder.conv.0.blocks.{i}.bias"], padding=wt.shape[2] // 2))
+        h = h.transpose(1, 2)
+    else:
+        h = lrelu(Fn.linear(x, p["encoder.fc.0.blocks.0.weight"], p["encoder.fc.0.blocks.0.bias"]))
+        h = lrelu(Fn.linear(h, p["encoder.fc.0.blocks.2.weight"], p["encoder.fc.0.blocks.2.bias"]))
     mean = Fn.linear(h, p["encoder.mean_fc.weight"], p["encoder.mean_fc.bias"])
     log_var = Fn.linear(h, p["encoder.log_var_fc.weight"], p["encoder.log_var_fc.bias"])
     std = torch.exp(0.5 * log_var)
     z = eps * std + mean
     kld = -0.5 * (1 + log_var - mean.pow(2) - log_var.exp())
     return {"mean": mean, "log_var": log_var, "sampled_h": z, "loss": kld}
+
+
+def conv1d_numpy(x, w, b):
+    """Explicit restatement of Conv1d over time for batch-first frames: x [B, T, Cin] (numpy),
+    w [Cout, Cin, K], b [Cout]; y[b, t] = b + sum_j W[:, :, j] x[b, t + j - (K-1)/2] with zeros
+    outside [0, T) (the semantics torch.nn.Conv1d(padding=(K-1)/2) has on [B, C, T])."""
+    import numpy as np
+    B, T, _ = x.shape
+    K = w.shape[2]
+    p = (K - 1) // 2
+    xp = np.zeros((B, T + 2 * p, x.shape[2]), dtype=np.float64)
+    xp[:, p:p + T] = x
+    y = np.broadcast_to(np.asarray(b, dtype=np.float64), (B, T, w.shape[0])).copy()
+    for j in range(K):
+        y += xp[:, j:j + T] @ np.asarray(w[:, :, j], dtype=np.float64).T
+    return y
 
 
 def lstm_direction_loop(x, w_ih, w_hh, b_ih, b_hh, reverse):
