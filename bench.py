@@ -50,6 +50,7 @@ CONFIGS = {
     "c3": (80, 64, 32, 512, 2, 64, GLOBAL_BATCH, 500, True),
     "c4": (80, 64, 32, 512, 2, 64, 64, 2000, False),
 }
+ENC_CONV = {"c4": 5}     # configs[3]: Conv1d encoder variant (kernel size 5), modules/conv_vae.py
 TIMER_EVERY = 4          # time kernels with HIP events on every 4th timed step
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
@@ -94,6 +95,16 @@ def heads_bytes(N, F, C, H):
     return N * (2 * 2 * H + 4 * F + 4 * (2 * C + 2 * C + 2 * F + 2 * F + 2 * C + 2 * C) + 4 * 2 * H)
 
 
+def conv_fwd_bytes(N, F, E):
+    """Both Conv1d encoder layers forward (conv.hip): read x (F fp32), write E1; read E1, write E2."""
+    return N * 4 * (F + 3 * E)
+
+
+def conv_bwd_bytes(N, F, E):
+    """Layer-2 input gradient (read dE2, E1; write dE1) + layer-1 weight gradient (read dE1, x)."""
+    return N * 4 * (5 * E + F)
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -115,7 +126,7 @@ def cpu_baseline(cfg_name, budget_s=12.0):
     cap = int(os.environ.get("OMP_NUM_THREADS", threads))
     torch.set_num_threads(max(1, min(threads, cap)))
     g = torch.Generator().manual_seed(1)
-    params = O.init_params(F, E, Z, H, L, C, seed=123456)
+    params = O.init_params(F, E, Z, H, L, C, seed=123456, enc_conv=ENC_CONV.get(cfg_name, 0))
     x = torch.randn(B, T, F, generator=g)
     lens = torch.ones(B)
     cfg = dict(L=L, loss_type="likelihood", kld_weight=1e-3)
@@ -204,7 +215,7 @@ def dry_run(rank, world):
 def make_engine(cfg_name, prec, device, world, rank, B):
     from mlvae_hip.engine import VAEConfig, VAEEngine
     F, E, Z, H, L, C, _, T, _ = CONFIGS[cfg_name]
-    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=prec)
+    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=prec, enc_conv=ENC_CONV.get(cfg_name, 0))
     eng = VAEEngine(cfg, device=device)
     eng.init_default(seed=123456)
     if world > 1:
@@ -263,6 +274,8 @@ def secondary(kern, B, T, cfg_name):
                          "frac": tf / MFMA_PEAK_TFLOPS["bf16"]}
     for name, nbytes, key in (("encoder_fwd", encoder_fwd_bytes(N, F, E, Z), "encoder_fwd"),
                               ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), "encoder_bwd"),
+                              ("conv_fwd", conv_fwd_bytes(N, F, E), "conv_fwd"),
+                              ("conv_bwd", conv_bwd_bytes(N, F, E), "conv_bwd"),
                               ("heads", heads_bytes(N, F, C, H), "heads")):
         if name in kern:
             gbs = nbytes / (kern[name] * 1e-3) / 1e9
@@ -274,9 +287,10 @@ def secondary(kern, B, T, cfg_name):
 
 
 def extra_runs(args, device):
-    """N=1 extras: configs[1] (c2, B=32 bf16) and the fp32 parity mode on the headline batch."""
+    """N=1 extras: configs[1] (c2, B=32 bf16), configs[3] (c4: Conv1d encoder, T=2000, B=64,
+    bf16) and the fp32 parity mode on the headline batch."""
     out = {}
-    runs = [("c2_bf16", "c2", "bf16", 10, 2)]
+    runs = [("c2_bf16", "c2", "bf16", 10, 2), ("c4_conv_bf16", "c4", "bf16", 4, 2)]
     if args.prec != "fp32":
         runs.append((f"{args.config}_fp32", args.config, "fp32", 3, 1))
     for key, cname, prec, steps, warm in runs:
@@ -284,11 +298,18 @@ def extra_runs(args, device):
         eng = make_engine(cname, prec, device, 1, 0, B)
         x = global_batch_shard(B, T, F, 0, device)
         lens = torch.ones(B, device=device)
-        dt, loss = timed_run(eng, x, lens, steps, warm, 1)
+        timers = {}
+        dt, loss = timed_run(eng, x, lens, steps, warm, 1, timers if cname == "c4" else None)
         lv = loss.tolist()
         out[key] = {"global_batch": B, "seq_len": T, "dtype": prec, "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
                     "loss": lv[2]}
+        if timers:
+            kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
+            out[key]["encoder"] = f"Conv1d K={ENC_CONV[cname]} [{F},{E},{E}]"
+            out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname).items()
+                                   if k.startswith("conv")}
+            out[key]["kernel_ms"] = kern
         del eng, x
         torch.cuda.empty_cache()
     return out
@@ -347,6 +368,7 @@ def main():
         nbytes = lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if args.prec == "bf16" else 4)
         achieved = nbytes / dur_s / 1e9
         step_us = kern[dom] * 1e3 / T
+        enc_desc = f"Conv1d(K={ENC_CONV[args.config]})" if args.config in ENC_CONV else "VanillaVAE"
         out = {
             "metric": METRIC,
             "value": value,
@@ -361,7 +383,7 @@ def main():
             "dtype": args.prec,
             "data": "synthetic N(0,1) 80-d frames (normalised log-mel stand-in), lens=1, "
                     "random-init weights (PyTorch default init, seed 123456)",
-            "config": {"workload": f"{args.config}: VanillaVAE enc [{F},{E},{E}] z={Z}, BiLSTM "
+            "config": {"workload": f"{args.config}: {enc_desc} enc [{F},{E},{E}] z={Z}, BiLSTM "
                                    f"{L}x{H} (dropout 0.15), dec-FC [{2 * H},{C},{C},{F}], T={T}, "
                                    f"global batch {B * world} = {B}/GPU x {world}, Gaussian-NLL ELBO, "
                                    f"clip 5.0 + Adam 1e-3",
