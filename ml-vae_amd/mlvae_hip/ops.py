@@ -27,6 +27,23 @@ def get_precision():
     return _state["prec"]
 
 
+class precision:
+    """Context: matrix-product operand precision inside the block (the mixed-precision region of
+    MDModel.fit_batch's auto_mix_prec branch; backward runs inside it too, since the HIP ops read
+    the precision when they launch)."""
+
+    def __init__(self, prec):
+        self.prec = prec
+
+    def __enter__(self):
+        self.prev = get_precision()
+        set_precision(self.prec)
+        return self
+
+    def __exit__(self, *exc):
+        set_precision(self.prev)
+
+
 def _prec():
     return PREC[_state["prec"]]
 

@@ -73,9 +73,17 @@ class MDModel(Brain):
             from mlvae_hip.engine import VAEEngine
             from mlvae_hip.optim import EngineOptimizer
             kw = fused.keywords
+            prec = getattr(self.hparams, "precision", "fp32")
+            if self.auto_mix_prec and prec != "bf16":
+                # --auto_mix_prec (the reference's fp16 autocast + GradScaler, ref:src/models/
+                # md_model.py:60-76): the fused step's mixed-precision mode is bf16 operands with
+                # fp32 accumulation / master weights; bf16 keeps fp32's exponent range, so the
+                # loss needs no scaling
+                logger.info("auto_mix_prec: fused step in bf16 operand mode")
+                prec = "bf16"
             self.engine = VAEEngine.from_modules(
                 self.modules["encoder"], self.modules["decoder"], device=self.device,
-                prec=getattr(self.hparams, "precision", "fp32"),
+                prec=prec,
                 kld_weight=self._weight_for("kld_loss"), recon_weight=self._weight_for("recon_loss"),
                 lr=kw.get("lr", 1e-3), betas=kw.get("betas", (0.9, 0.999)), eps=kw.get("eps", 1e-8),
                 max_grad_norm=self.max_grad_norm,
@@ -112,18 +120,32 @@ class MDModel(Brain):
             self._log_losses(loss)
             self.optimizer_step += 1
             return loss[2].detach()
+        opts = list(self.optimizers.values())
         if self.auto_mix_prec:
-            raise NotImplementedError("fp16 AMP: use precision: bf16 in the model yaml instead")
+            # ref:src/models/md_model.py:60-76: zero_grad, autocast forward, scaled backward,
+            # unscale, check_gradients, scaler.step, scaler.update.  The autocast region is the
+            # HIP ops' bf16-operand mode (fp32 accumulation); the dynamic loss scale is kept.
+            from mlvae_hip import ops
+            scaler = self._amp_scaler()
+            for opt in opts:
+                opt.zero_grad()
+            with ops.precision("bf16"):
+                outputs = self.compute_forward(batch, Stage.TRAIN)
+                loss = self.compute_objectives(outputs, batch, Stage.TRAIN)
+                scaler.scale(loss).backward()
+            self._dp_mean_grads()
+            for opt in opts:
+                scaler.unscale_(opt)
+            if self.check_gradients(loss):
+                for opt in opts:
+                    scaler.step(opt)
+            scaler.update()
+            self.optimizer_step += 1
+            return loss.detach()
         outputs = self.compute_forward(batch, Stage.TRAIN)
         loss = self.compute_objectives(outputs, batch, Stage.TRAIN)
         loss.backward()
-        if self.world_size > 1:  # module mode under DP: DDP's mean of the ranks' gradients
-            import torch.distributed as tdist
-            for p_ in self.modules.parameters():
-                if p_.grad is not None:
-                    tdist.all_reduce(p_.grad)
-                    p_.grad /= self.world_size
-        opts = list(self.optimizers.values())
+        self._dp_mean_grads()
         if self.check_gradients(loss):
             for opt in opts:
                 opt.step()
@@ -131,6 +153,22 @@ class MDModel(Brain):
             opt.zero_grad()
         self.optimizer_step += 1
         return loss.detach()
+
+    def _dp_mean_grads(self):
+        if self.world_size > 1:  # module mode under DP: DDP's mean of the ranks' gradients
+            import torch.distributed as tdist
+            for p_ in self.modules.parameters():
+                if p_.grad is not None:
+                    tdist.all_reduce(p_.grad)
+                    p_.grad /= self.world_size
+
+    def _amp_scaler(self):
+        """SpeechBrain's GradScaler for auto_mix_prec (a checkpoint recoverable, 'scaler')."""
+        if getattr(self, "scaler", None) is None:
+            self.scaler = torch.amp.GradScaler("cuda")
+            if self.checkpointer is not None:
+                self.checkpointer.add_recoverable("scaler", self.scaler)
+        return self.scaler
 
     def evaluate_batch(self, batch, stage):
         if self.engine is not None:
