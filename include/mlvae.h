@@ -193,6 +193,21 @@ int mlvae_viterbi_md(int B, int T, int N, int L, const float* logits, int ldl, c
                      size_t ws_bytes, int* boundary_out, int* flvl_out, int* plvl_out, int* lens_out,
                      int* err, void* stream);
 
+/* fp8 GEMM mode (BASELINE.json configs[4], csrc/gemm_fast.hip VAR 8 + csrc/fp8.hip): the decoder's
+ * layer-1 input projection (ref:src/modules/decoder.py:14-15,22, nn.LSTM's x W_ih^T) on fp8 e4m3
+ * (OCP) operands with per-tensor scales, v_mfma_scale_f32_16x16x128_f8f6f4, fp32 accumulate.
+ *   gemm_fp8:  C = (*alpha) * A . B^T + bias1 + bias2, A [M][K], B [N][K] fp8 (k-contiguous,
+ *              K, lda, ldb % 16, 16-byte aligned); C fp32, or fp16 with epi = 16 (EPI_OUT_F16).
+ *   fp8_scale: out[0] = q = 448 / max|x| (1 if 0 / non-finite), out[1] = 1 / (q * other_scale).
+ *   cast_fp8:  dst = e4m3(clamp(src * scale, +-448)), RNE; scale = *scale_p if non-null. */
+int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                   const float* alpha, const float* bias1, const float* bias2, int epi, void* stream);
+size_t mlvae_fp8_scale_workspace_size(void);
+int mlvae_fp8_scale(size_t n, const float* x, float other_scale, float* out, float* ws, size_t ws_bytes,
+                    void* stream);
+int mlvae_cast_fp8(size_t n, const void* src, int src_bf16, const float* scale_p, float scale, void* dst,
+                   void* stream);
+
 /* Conv1d encoder layers (csrc/conv.hip), BASELINE.json configs[3]'s "Conv1d encoder variant":
  * the reference has none (SURVEY.md Appendix A); semantics = torch.nn.Conv1d(Cin, Cout, K,
  * padding=(K-1)/2) over each utterance of the batch-first frames [B, T, C] (row b*T + t), zero

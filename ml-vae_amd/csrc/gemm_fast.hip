@@ -47,6 +47,7 @@ struct GFArgs {
   int splits, kchunk;
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
   int c16;            // C stored as fp16 (epi bit EPI_OUT_F16)
+  const float* alpha; // device scalar multiplying A.B (fp8 operand scales), or null
   float* ws;
 };
 
@@ -197,8 +198,22 @@ __device__ __forceinline__ float epi_apply(const GFArgs& g, float val, int row, 
   return val;
 }
 
+// fp8 e4m3 operand fragment of v_mfma_scale_f32_16x16x128_f8f6f4 from a k-contiguous image of
+// 128-byte rows (128 fp8 = the K-tile; the same bytes as a 64-deep bf16 image, same swizzle):
+// lane l holds row base + (l & 15), k = 32 (l >> 4) + j, j < 32 (two 16-byte chunks).  Any
+// k-slot assignment is exact as long as A and B use the same one.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ i32x8 frag8(const short* img, int base, int lane) {
+  const int row = base + (lane & 15), c = 2 * (lane >> 4);
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(img + row * TBK + ((c ^ (row & 7)) << 3));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(img + row * TBK + (((c + 1) ^ (row & 7)) << 3));
+  return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
 // VAR 0: stage the next K-tile's 8 pieces per wave at the top of the K-step; 1: DEEP (BK 32,
-// 3 K-steps in flight); 2/3: the 8 pieces spread one per 8 MFMAs (3: + scheduling hints)
+// 3 K-steps in flight); 2/3: the 8 pieces spread one per 8 MFMAs (3: + scheduling hints);
+// 8: fp8 e4m3 operands (both k-contiguous), one 16x16x128 block-scaled MFMA (unit scales) per
+// tile pair and K-tile of 128 -- twice the bf16 MFMA rate, the same staging bytes per K-tile
 template <bool AKC, bool BKC, int VAR>
 __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   constexpr bool DEEP = VAR == 1;
@@ -267,7 +282,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
-  } else if constexpr (VAR >= 2) {
+  } else if constexpr (VAR == 2 || VAR == 3) {
     auto piece = [&](int buf, int k0, int pc) {
       if (pc < 4)
         stage_piece<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane, pc);
@@ -309,6 +324,38 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile it+1 has landed (this wave's pieces)
       __syncthreads();                                 // ... everyone's; buffer cur is free
     }
+  } else if constexpr (VAR == 8) {
+    static_assert(AKC && BKC, "fp8 operands are k-contiguous");
+    auto stage_both = [&](int buf, int k0) {
+      stage<true>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+      stage<true>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, 0, 0, wave, lane);
+    };
+    if (nk > 0) {
+      stage_both(0, kbeg);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < nk) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
+      const short* As = lds + (cur * 2 + 0) * IMG;
+      const short* Bs = lds + (cur * 2 + 1) * IMG;
+      i32x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag8(Bs, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = frag8(As, wm * 128 + i * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, 127,
+                                                                       0, 127);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   } else {
   auto stage_both = [&](int buf, int k0) {
     stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
@@ -344,6 +391,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   }
   }
 
+  if (g.alpha) {  // fp8 operand scales
+    const float al = *g.alpha;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] *= al;
+  }
   // epilogue: lane holds C[m0 + wm*128 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
   const bool split = g.splits > 1;
   float* Cb = g.c16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(g.C) + bz * g.c_bs)
@@ -485,6 +539,9 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
     case 1: return launch_fast_v<AKC, BKC, 1>(g, grid, s);
     case 2: return launch_fast_v<AKC, BKC, 2>(g, grid, s);
     case 3: return launch_fast_v<AKC, BKC, 3>(g, grid, s);
+    case 8:
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 8>(g, grid, s);
+      return 1;
     default: return launch_fast_v<AKC, BKC, 0>(g, grid, s);
   }
 }
@@ -583,6 +640,7 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   g.kshiftT = kshift_T; g.kshift = kshift; g.kshift_bstep = kshift_bstep;
   g.dseed = drop_seed; g.doff = drop_offset; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
   g.ws = ws;
+  g.alpha = nullptr;
   int s, kc;
   fast_plan(M, N, K, batch, &s, &kc);
   if (s > 1 && (N % 4 != 0 || !ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
@@ -622,5 +680,54 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     splitk_reduce_fast<<<dim3(blocks, batch), 256, 0, st>>>(g);
     MLVAE_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+// C[M,N] (fp32, or fp16 with EPI_OUT_F16) = (*alpha) * A . B^T + bias1 + bias2 over fp8 e4m3 (OCP)
+// operands A [M][K], B [N][K] (k-contiguous, leading dims in elements).  gemm256_kernel VAR 8.
+extern "C" int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                              const float* alpha, const float* bias1, const float* bias2, int epi, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || !C || (K > 0 && (!A || !B))) {
+    mlvae_set_error("mlvae_gemm_fp8: bad shape/ptr");
+    return 1;
+  }
+  if (M == 0 || N == 0) return 0;
+  const int c16 = (epi & EPI_OUT_F16) ? 1 : 0;
+  epi &= ~EPI_OUT_F16;
+  if (epi != EPI_NONE || N % 4 || ldc % 4 || ((uintptr_t)C % 16) || ((uintptr_t)bias1 % 16) ||
+      ((uintptr_t)bias2 % 16)) {
+    mlvae_set_error("mlvae_gemm_fp8: epilogue none (+ fp16 C), N and ldc %% 4, aligned C / bias");
+    return 1;
+  }
+  if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || (lda % 16) || (ldb % 16) || (K % 16)) {
+    mlvae_set_error("mlvae_gemm_fp8: operands need 16-byte chunks (K, lda, ldb %% 16, aligned)");
+    return 1;
+  }
+  if ((size_t)M * lda >= OOB || (size_t)N * ldb >= OOB) {
+    mlvae_set_error("mlvae_gemm_fp8: operand larger than 2 GB");
+    return 1;
+  }
+  // the staging works in 2-byte units: an fp8 row of K elements is K / 2 "shorts"
+  GFArgs g;
+  g.M = M; g.N = N; g.K = K / 2;
+  g.A = static_cast<const short*>(A); g.lda = lda / 2; g.a_bs = 0;
+  g.B = static_cast<const short*>(B); g.ldb = ldb / 2; g.b_bs = 0;
+  g.C = static_cast<float*>(C); g.ldc = ldc; g.c_bs = 0; g.beta = 0.f;
+  g.bias1 = bias1; g.bias2 = bias2; g.epi = EPI_NONE; g.aux = nullptr; g.ldaux = 0;
+  g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
+  g.dseed = 0; g.doff = 0; g.dkeep = 1.f; g.dscale = 1.f;
+  g.ws = nullptr; g.alpha = alpha;
+  g.splits = 1; g.kchunk = ((g.K + TBK - 1) / TBK) * TBK;
+  if (g.K == 0) g.kchunk = TBK;
+  static const int group_m = [] {
+    const char* e = getenv("MLVAE_GEMM_GROUP_M");
+    return e ? atoi(e) : 4;
+  }();
+  g.group_m = group_m;
+  g.c16 = c16;
+  dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), 1, 1);
+  const int rc = launch_fast<true, true>(g, grid, (hipStream_t)stream, 8);
+  if (rc) return rc;
+  MLVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -41,6 +41,10 @@ _SIGS = {
     "mlvae_viterbi_workspace_size": [I, I, I],
     "mlvae_viterbi_md": [I, I, I, I, P, I, P, P, P, P, P, P, F, P, SZ, P, P, P, P, P, P],
     "mlvae_phn_bce": [I, I, I, P, I, P, P, I, P, P, P, P, P, P, P],
+    "mlvae_gemm_fp8": [I, I, I, P, I, P, I, P, I, P, P, P, I, P],
+    "mlvae_fp8_scale_workspace_size": [],
+    "mlvae_fp8_scale": [SZ, P, F, P, P, SZ, P],
+    "mlvae_cast_fp8": [SZ, P, I, P, F, P, P],
     "mlvae_conv1d_supported": [I, I, I],
     "mlvae_conv1d_fwd": [I, I, I, I, I, P, I, P, P, I, P, I, P],
     "mlvae_conv1d_dgrad": [I, I, I, I, I, P, I, P, P, I, P, I, P],
@@ -97,6 +101,7 @@ _SIGS = {
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
     "mlvae_conv1d_wgrad_workspace_size": SZ,
+    "mlvae_fp8_scale_workspace_size": SZ,
     "mlvae_gemm_workspace_size": SZ,
     "mlvae_gemm_ex_workspace_size": SZ,
     "mlvae_colsum_workspace_size": SZ,
