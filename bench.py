@@ -49,11 +49,14 @@ CONFIGS = {
     "c2": (80, 64, 32, 512, 2, 64, 32, 500, False),
     "c3": (80, 64, 32, 512, 2, 64, GLOBAL_BATCH, 500, True),
     "c4": (80, 64, 32, 512, 2, 64, 64, 2000, False),
+    "c5": (80, 64, 32, 512, 2, 64, 64, 500, False),   # configs[4]: B=512 over 8 GPUs = 64 per GPU
 }
+CONFIGS["c5bf16"] = CONFIGS["c5"]   # the same per-GPU shard in bf16 (the fp8 comparison)
+FP8 = {"c5"}             # configs[4]: fp8 e4m3 layer-1 input projection (VAEConfig.fp8)
 ENC_CONV = {"c4": 5}     # configs[3]: Conv1d encoder variant (kernel size 5), modules/conv_vae.py
 TIMER_EVERY = 4          # time kernels with HIP events on every 4th timed step
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s spec
-MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}
 HANDOFF_FLOOR_US = 0.8   # MI355X_MICROARCH.md handoff-1to1, idle, 8 B
 
 
@@ -215,7 +218,8 @@ def dry_run(rank, world):
 def make_engine(cfg_name, prec, device, world, rank, B):
     from mlvae_hip.engine import VAEConfig, VAEEngine
     F, E, Z, H, L, C, _, T, _ = CONFIGS[cfg_name]
-    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=prec, enc_conv=ENC_CONV.get(cfg_name, 0))
+    cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=prec, enc_conv=ENC_CONV.get(cfg_name, 0),
+                    fp8=cfg_name in FP8 and prec != "fp32")
     eng = VAEEngine(cfg, device=device)
     eng.init_default(seed=123456)
     if world > 1:
@@ -290,7 +294,8 @@ def extra_runs(args, device):
     """N=1 extras: configs[1] (c2, B=32 bf16), configs[3] (c4: Conv1d encoder, T=2000, B=64,
     bf16) and the fp32 parity mode on the headline batch."""
     out = {}
-    runs = [("c2_bf16", "c2", "bf16", 10, 2), ("c4_conv_bf16", "c4", "bf16", 4, 2)]
+    runs = [("c2_bf16", "c2", "bf16", 10, 2), ("c4_conv_bf16", "c4", "bf16", 4, 2),
+            ("c5_fp8_per_gpu", "c5", "bf16", 10, 2), ("c5_bf16_per_gpu", "c5bf16", "bf16", 10, 2)]
     if args.prec != "fp32":
         runs.append((f"{args.config}_fp32", args.config, "fp32", 3, 1))
     for key, cname, prec, steps, warm in runs:
@@ -299,16 +304,25 @@ def extra_runs(args, device):
         x = global_batch_shard(B, T, F, 0, device)
         lens = torch.ones(B, device=device)
         timers = {}
-        dt, loss = timed_run(eng, x, lens, steps, warm, 1, timers if cname == "c4" else None)
+        dt, loss = timed_run(eng, x, lens, steps, warm, 1, timers if cname in ("c4", "c5", "c5bf16") else None)
         lv = loss.tolist()
         out[key] = {"global_batch": B, "seq_len": T, "dtype": prec, "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
                     "loss": lv[2]}
         if timers:
             kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
-            out[key]["encoder"] = f"Conv1d K={ENC_CONV[cname]} [{F},{E},{E}]"
-            out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname).items()
-                                   if k.startswith("conv")}
+            if cname in ENC_CONV:
+                out[key]["encoder"] = f"Conv1d K={ENC_CONV[cname]} [{F},{E},{E}]"
+                out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname).items()
+                                       if k.startswith("conv")}
+            else:
+                sec = secondary(kern, B, T, cname)
+                if cname in FP8 and "proj_l1" in sec:  # against the fp8 (block-scaled) MFMA peak
+                    sec["proj_l1"].update(what="layer-1 input projection on fp8 e4m3 operands (incl. the "
+                                               "x / W_ih casts)", peak=MFMA_PEAK_TFLOPS["fp8"])
+                    sec["proj_l1"]["frac"] = sec["proj_l1"]["achieved"] / MFMA_PEAK_TFLOPS["fp8"]
+                out[key]["kernels"] = {k: v for k, v in sec.items() if k == "proj_l1"}
+                out[key]["fp8"] = cname in FP8
             out[key]["kernel_ms"] = kern
         del eng, x
         torch.cuda.empty_cache()

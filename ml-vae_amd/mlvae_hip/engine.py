@@ -31,6 +31,7 @@ PREC = {"fp32": 0, "bf16": 1}
 LOSS = {"likelihood": 0, "mse": 1}
 EPI_NONE, EPI_LRELU, EPI_DLRELU, EPI_DROPOUT = 0, 1, 2, 3
 EPI_OUT_F16 = 16  # flag: mlvae_gemm_bf16 stores C as fp16
+X8_SCALE = 256.0  # fp8 mode: scale of the layer inputs (|dropout(h)| <= 1/(1-p) -> <= 302 < 448)
 
 
 @dataclass
@@ -52,6 +53,7 @@ class VAEConfig:
     max_grad_norm: float = 5.0
     prec: str = "fp32"      # "fp32" (exact parity mode) or "bf16" (bf16 MFMA operands)
     enc_conv: int = 0       # Conv1d encoder kernel size (modules/conv_vae.py, configs[3]); 0 = Linear
+    fp8: bool = False       # configs[4]: the layer >= 1 input projections on fp8 e4m3 operands (bf16 mode)
 
     @property
     def enc_prefix(self):
@@ -66,6 +68,8 @@ class VAEConfig:
             raise ValueError(f"Invalid loss type: {self.loss_type}")
         if self.prec not in PREC:
             raise ValueError(f"prec must be one of {list(PREC)}")
+        if self.fp8 and self.prec != "bf16":
+            raise ValueError("fp8 projections run inside the bf16 mode: prec must be 'bf16'")
         if self.enc_conv:
             if self.enc_conv % 2 != 1:
                 raise ValueError("enc_conv: the Conv1d kernel size must be odd")
@@ -221,6 +225,7 @@ class _Work:
         self.enc_fused = self.bf and enc_fused
         self.ZA = Z + 16 if self.enc_fused else Z
         self.Zb = empty(N, self.ZA, **b16) if self.bf else None  # first layer's GEMM operand
+        self.X8 = empty(N, 2 * H, dtype=torch.uint8) if (self.bf and cfg.fp8) else None  # fp8 layer input
         self.E1b = empty(N, E, **b16) if self.enc_fused else None
         self.E2b = empty(N, E, **b16) if self.enc_fused else None
         if self.bf:
@@ -331,6 +336,11 @@ class VAEEngine:
         if cfg.prec == "bf16":
             for li in range(1, cfg.L):
                 self.wih_t[li] = torch.empty(2 * cfg.H * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
+            if cfg.fp8:  # fp8 e4m3 copies of W_ih_l{>=1} (both directions) and their scales
+                self.w8 = {li: torch.empty(8 * cfg.H * 2 * cfg.H, device=self.device, dtype=torch.uint8)
+                           for li in range(1, cfg.L)}
+                self.w8s = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
+                self.f8ws = torch.empty(lib().mlvae_fp8_scale_workspace_size() // 4 + 1, device=self.device)
             if self.fused_encoder:  # dZ = dG W_ih_l0 over its k-contiguous transpose
                 self.wih_t[0] = torch.empty(cfg.Z * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
         self.nparts = lib().mlvae_sumsq_partials_count(n)
@@ -659,6 +669,21 @@ class VAEEngine:
                                              self._ptr(f"decoder.rnn.bias_ih_l{li}"),
                                              self._ptr(f"decoder.rnn.bias_hh_l{li}"), _p(w.G[li]), 8 * H,
                                              int(w.g16), s), "skinny_proj")
+            elif w.bf and cfg.fp8 and li > 0 and din % 16 == 0 and ldx == din:
+                # configs[4]: fp8 e4m3 operands, per-tensor scales (x: the fixed 2^8, |x| <= 1/(1-p);
+                # W_ih: 448 / max|W_ih|), block-scaled MFMA, alpha = 1 / (2^8 q_w) (fp8.hip)
+                with self._timed(f"proj_l{li}"):
+                    wih = self._ptr(f"decoder.rnn.weight_ih_l{li}")
+                    check(l.mlvae_fp8_scale(8 * H * din, wih, X8_SCALE, _p(self.w8s[li]), _p(self.f8ws),
+                                            self.f8ws.numel() * 4, s), "fp8_scale")
+                    check(l.mlvae_cast_fp8(8 * H * din, wih, 0, _p(self.w8s[li]), 0.0, self.w8[li].data_ptr(), s),
+                          "cast_fp8")
+                    check(l.mlvae_cast_fp8(N * din, _pb(xin_bf), 1, None, X8_SCALE, w.X8.data_ptr(), s), "cast_fp8")
+                    check(l.mlvae_gemm_fp8(N, 8 * H, din, w.X8.data_ptr(), din, self.w8[li].data_ptr(), din,
+                                           _p(w.G[li]), 8 * H, _p(self.w8s[li], 1),
+                                           self._ptr(f"decoder.rnn.bias_ih_l{li}"),
+                                           self._ptr(f"decoder.rnn.bias_hh_l{li}"),
+                                           EPI_OUT_F16 if w.g16 else EPI_NONE, s), "gemm_fp8")
             elif w.bf and din % 8 == 0:  # input projection on the 256² GEMM
                 with self._timed(f"proj_l{li}"):
                     self._fast(w, 0, 1, N, 8 * H, din, _pb(xin_bf), ldx, wb(f"decoder.rnn.weight_ih_l{li}"),
