@@ -315,6 +315,9 @@ def extra_runs(args, device):
                 out[key]["encoder"] = f"Conv1d K={ENC_CONV[cname]} [{F},{E},{E}]"
                 out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname).items()
                                        if k.startswith("conv")}
+                # PMC HBM bytes per launch of each conv kernel (profiles/pmc_traffic.json[c4])
+                out[key]["pmc_bytes_per_launch"] = {k: pmc_traffic(f"{cname}/{k}") for k in
+                                                    ("conv_fwd_layer", "conv_dgrad", "conv_wgrad")}
             else:
                 sec = secondary(kern, B, T, cname)
                 if cname in FP8 and "proj_l1" in sec:  # against the fp8 (block-scaled) MFMA peak

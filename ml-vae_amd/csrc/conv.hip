@@ -72,10 +72,10 @@ struct ConvArgs {
   const float* bias;
   const float* aux; int ldaux; // dgrad: LeakyReLU output whose derivative multiplies dx
   float* y; int ldy;
-  int dgrad, act, tpu, ntiles;
+  int act, tpu, ntiles;
 };
 
-template <int NT>
+template <int NT, bool DG>  // DG: input gradient (transposed, time-flipped weights)
 __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) short smem[];
   const int K = a.K, CinP = a.CinP, KC = K * CinP;
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
     const int o = e / KC, rem = e - o * KC, j = rem / CinP, c = rem - j * CinP;
     float v = 0.f;
     if (c < a.Cin)
-      v = a.dgrad ? a.w[((size_t)c * a.Lc + o) * K + (K - 1 - j)] : a.w[((size_t)o * a.Lc + c) * K + j];
+      v = DG ? a.w[((size_t)c * a.Lc + o) * K + (K - 1 - j)] : a.w[((size_t)o * a.Lc + c) * K + j];
     Wl[o * ldw + rem] = f2bf(v);
   }
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
@@ -252,6 +252,7 @@ int launch_lds(Kern k, int grid, size_t lds, hipStream_t s, const Args& a) {
   return 0;
 }
 
+template <bool DG>
 int launch_conv(ConvArgs& a, int B, hipStream_t s) {
   a.tpu = (a.T + BM - 1) / BM;
   a.ntiles = B * a.tpu;
@@ -262,7 +263,7 @@ int launch_conv(ConvArgs& a, int B, hipStream_t s) {
   }
   int g = a.ntiles < 2 * device_cus() ? a.ntiles : 2 * device_cus();
   switch (a.Cout / 16) {
-#define CASE(n) case n: return launch_lds(conv_kernel<n>, g, lds, s, a);
+#define CASE(n) case n: return launch_lds(conv_kernel<n, DG>, g, lds, s, a);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE
     default: mlvae_set_error("conv1d: output channels %d", a.Cout); return 1;
@@ -292,8 +293,8 @@ extern "C" int mlvae_conv1d_fwd(int B, int T, int Cin, int Cout, int K, const fl
   ConvArgs a{};
   a.T = T; a.Cin = Cin; a.Cout = Cout; a.K = K; a.CinP = round_up(Cin, 32); a.Lc = Cin;
   a.x = x; a.ldx = ldx; a.w = w; a.bias = bias; a.aux = nullptr; a.ldaux = 0; a.y = y; a.ldy = ldy;
-  a.dgrad = 0; a.act = act ? 1 : 0;
-  return launch_conv(a, B, (hipStream_t)stream);
+  a.act = act ? 1 : 0;
+  return launch_conv<false>(a, B, (hipStream_t)stream);
 }
 
 extern "C" int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const float* dy, int lddy,
@@ -308,8 +309,8 @@ extern "C" int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const 
   ConvArgs a{};
   a.T = T; a.Cin = Cout; a.Cout = Cin; a.K = K; a.CinP = round_up(Cout, 32); a.Lc = Cin;
   a.x = dy; a.ldx = lddy; a.w = w; a.bias = nullptr; a.aux = aux; a.ldaux = ldaux; a.y = dx; a.ldy = lddx;
-  a.dgrad = 1; a.act = 0;
-  return launch_conv(a, B, (hipStream_t)stream);
+  a.act = 0;
+  return launch_conv<true>(a, B, (hipStream_t)stream);
 }
 
 static int wgrad_grid(int B, int T) {

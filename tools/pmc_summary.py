@@ -25,9 +25,12 @@ def per_kernel(path):
 def short(name):
     n = name.replace("(anonymous namespace)::", "")
     for frag, key in (("lstm_bwd", "lstm_bwd"), ("lstm_fwd", "lstm_fwd"), ("heads_kernel", "heads"),
-                      ("encoder_fwd_kernel", "encoder_fwd"), ("encoder_bwd_kernel", "encoder_bwd")):
+                      ("encoder_fwd_kernel", "encoder_fwd"), ("encoder_bwd_kernel", "encoder_bwd"),
+                      ("conv_wgrad_kernel", "conv_wgrad"), ("gemm256_kernel<true, true, 8>", "gemm_fp8")):
         if frag in n:
             return key
+    if "conv_kernel" in n:  # forward layers / input gradient (csrc/conv.hip)
+        return "conv_dgrad" if "true>" in n else "conv_fwd_layer"
     return n.split("(")[0]
 
 
