@@ -251,7 +251,10 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
               if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
               break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            // a longer back-off thins the L2 poll traffic (3.27 -> 3.20 us/step at B = 256);
+            // bit 18: the previous s_sleep(2)
+            if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
+            else __builtin_amdgcn_s_sleep(6);
           }
           STAMP(1);
 #pragma unroll
@@ -516,7 +519,9 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
           if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        // BPTT: a shorter back-off (3.03 -> 2.97 us/step at B = 256); bit 18: s_sleep(2)
+        if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(1);
       }
     }
     STAMP(1);
