@@ -78,8 +78,11 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
   unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);  // [2][NC8] keep bits
   __shared__ int abort_flag;
 
-  const int ngroups = 2 * a.NB;
-  const int gid = blockIdx.x % ngroups, js = blockIdx.x / ngroups;
+  // group slots padded to a multiple of 8 (idle slots exit at once): members gid + k * gstride
+  // then share one XCD under round-robin dispatch at every batch size (B = 32: 4 groups)
+  const int ngroups = 2 * a.NB, gstride = (ngroups + 7) & ~7;
+  const int gid = blockIdx.x % gstride, js = blockIdx.x / gstride;
+  if (gid >= ngroups) return;
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -107,8 +110,8 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
       else wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane] = v;
     }
   }
-  // group members are blocks gid + k * ngroups: one XCD under round-robin dispatch whenever
-  // ngroups % 8 == 0; verified at run time, never assumed (lstm_common.h group_on_one_xcd)
+  // group members are blocks gid + k * gstride: one XCD under round-robin dispatch; verified
+  // at run time, never assumed (lstm_common.h group_on_one_xcd)
   __shared__ int placement;
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement) &&
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
@@ -358,8 +361,11 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
   char* cst = smem + 2 * AIMG + (size_t)8 * NTW * KLB * 64 * 16;  // [2][16][CUTT]
   __shared__ int abort_flag;
 
-  const int ngroups = 2 * a.NB;
-  const int gid = blockIdx.x % ngroups, js = blockIdx.x / ngroups;
+  // group slots padded to a multiple of 8 (idle slots exit at once): members gid + k * gstride
+  // then share one XCD under round-robin dispatch at every batch size (B = 32: 4 groups)
+  const int ngroups = 2 * a.NB, gstride = (ngroups + 7) & ~7;
+  const int gid = blockIdx.x % gstride, js = blockIdx.x / gstride;
+  if (gid >= ngroups) return;
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -720,7 +726,7 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
     mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
     return 2;
   }
-  k<<<dim3(2 * p.NB * p.NJ), 512, p.lds, s>>>(a);
+  k<<<dim3(((2 * p.NB + 7) & ~7) * p.NJ), 512, p.lds, s>>>(a);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

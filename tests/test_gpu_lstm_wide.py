@@ -110,28 +110,32 @@ def test_gate_buffer_format_is_checked():
     need_gpu()
     l = lib()
     assert l.mlvae_lstm_gates_fp16(256, H, 1) == 1
-    assert l.mlvae_lstm_gates_fp16(32, H, 1) == 0      # c2: one batch-group launch
+    assert l.mlvae_lstm_gates_fp16(32, H, 1) == 1      # c2: the wide kernels at every batch size
+    assert l.mlvae_lstm_gates_fp16(8, H, 1) == 1
     assert l.mlvae_lstm_gates_fp16(256, H, 0) == 0     # fp32 parity mode
     assert l.mlvae_lstm_gates_fp16(256, 128, 1) == 0   # wide kernels are built for H = 512
-    B, T = 32, 4
+    B, T, H2 = 8, 4, 128                               # a batch-group shape refuses fp16 gates
     N = B * T
-    G = torch.zeros(N, 8 * H, device="cuda", dtype=torch.float16)
-    Cs = torch.empty(N, 2 * H, device="cuda")
-    Y = torch.empty(N, 2 * H, device="cuda")
+    G = torch.zeros(N, 8 * H2, device="cuda", dtype=torch.float16)
+    Cs = torch.empty(N, 2 * H2, device="cuda")
+    Y = torch.empty(N, 2 * H2, device="cuda")
     xb = ctypes.c_size_t()
     check(l.mlvae_lstm_workspace_size(256, H, 1, ctypes.byref(xb)))
     xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
-    W = torch.zeros(4 * H, H, device="cuda")
-    assert l.mlvae_lstm_fwd_ex2(1, B, T, H, P(W), P(W), P(G), 1, P(Cs), P(Y), None, None, 0, 0, 0.0,
+    W2 = torch.zeros(4 * H2, H2, device="cuda")
+    assert l.mlvae_lstm_fwd_ex2(1, B, T, H2, P(W2), P(W2), P(G), 1, P(Cs), P(Y), None, None, 0, 0, 0.0,
                                 P(xbuf), xb.value, P(err), stream()) != 0
     assert b"fp16 gates" in l.mlvae_last_error()
+    W = torch.zeros(4 * H, H, device="cuda")
     B, N = 256, 256 * 4
     G = torch.zeros(N, 8 * H, device="cuda", dtype=torch.float16)
     Cs = torch.empty(N, 2 * H, device="cuda")
     assert l.mlvae_lstm_bwd_ex2(1, B, T, H, P(W), P(W), P(G), 1, P(Cs), P(Cs), None, None,
                                 P(xbuf), xb.value, P(err), stream()) != 0
-    # the batch-group fallback skips neither output: Y = NULL is refused there
-    assert l.mlvae_lstm_fwd_ex2(1, 32, T, H, P(W), P(W), P(G), 0, P(Cs), None, None, None, 0, 0, 0.0,
+    # the batch-group kernels skip neither output: Y = NULL is refused there
+    G32 = torch.zeros(8 * T, 8 * H2, device="cuda")
+    Cs2 = torch.empty(8 * T, 2 * H2, device="cuda")
+    assert l.mlvae_lstm_fwd_ex2(1, 8, T, H2, P(W2), P(W2), P(G32), 0, P(Cs2), None, None, None, 0, 0, 0.0,
                                 P(xbuf), xb.value, P(err), stream()) != 0
     torch.cuda.synchronize()
