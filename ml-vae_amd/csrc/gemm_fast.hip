@@ -48,6 +48,7 @@ struct GFArgs {
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
   int c16;            // C stored as fp16 (epi bit EPI_OUT_F16)
   const float* alpha; // device scalar multiplying A.B (fp8 operand scales), or null
+  int abl;            // ablation bits (MLVAE_GEMM_ABL, timing only): 1 no MFMA, 2 no staging loads
   float* ws;
 };
 
@@ -324,6 +325,47 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile it+1 has landed (this wave's pieces)
       __syncthreads();                                 // ... everyone's; buffer cur is free
     }
+  } else if constexpr (VAR == 4) {
+    // VAR 4: both k-halves' fragments (24 ds_reads) issued right after the barrier, so the
+    // second half's MFMAs never wait on an LDS round trip in mid-step
+    auto stage_both = [&](int buf, int k0) {
+      stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+      stage<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+    };
+    if (nk > 0) {
+      stage_both(0, kbeg);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < nk) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
+      const short* As = lds + (cur * 2 + 0) * IMG;
+      const short* Bs = lds + (cur * 2 + 1) * IMG;
+      bf16x8 af0[8], bf0[4], af1[8], bf1[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf0[j] = frag<BKC>(Bs, wn * 64 + j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af0[i] = frag<AKC>(As, wm * 128 + i * 16, 0, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf1[j] = frag<BKC>(Bs, wn * 64 + j * 16, 32, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af1[i] = frag<AKC>(As, wm * 128 + i * 16, 32, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf0[j], af0[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   } else if constexpr (VAR == 8) {
     static_assert(AKC && BKC, "fp8 operands are k-contiguous");
     auto stage_both = [&](int buf, int k0) {
@@ -368,7 +410,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   }
   for (int it = 0; it < nk; ++it) {
     const int cur = it & 1;
-    if (it + 1 < nk) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
+    if (it + 1 < nk && !(g.abl & 2)) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
     const short* As = lds + (cur * 2 + 0) * IMG;
     const short* Bs = lds + (cur * 2 + 1) * IMG;
 #pragma unroll
@@ -378,6 +420,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wn * 64 + j * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) af[i] = frag<AKC>(As, wm * 128 + i * 16, kk, lane);
+      if (g.abl & 1) {  // ablation: fragments read, no MFMA
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bfr[j]));
+        continue;
+      }
       // operands swapped (D = B^T A^T): a lane's 4 results are 4 consecutive columns of one
       // row, so the epilogue stores 16 B per lane
 #pragma unroll
@@ -539,10 +588,17 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
     case 1: return launch_fast_v<AKC, BKC, 1>(g, grid, s);
     case 2: return launch_fast_v<AKC, BKC, 2>(g, grid, s);
     case 3: return launch_fast_v<AKC, BKC, 3>(g, grid, s);
+    case 4: return launch_fast_v<AKC, BKC, 4>(g, grid, s);
+    case 5: return launch_fast_v<AKC, BKC, 0>(g, grid, s);  // the previous default (A/B)
     case 8:
       if constexpr (AKC && BKC) return launch_fast_v<true, true, 8>(g, grid, s);
       return 1;
-    default: return launch_fast_v<AKC, BKC, 0>(g, grid, s);
+    default:
+      // k-contiguous x k-contiguous (projection, dgrad): both k-halves' fragments up front
+      // (VAR 4: c3 projection 1.329 -> 1.314 ms, dgrad 1.148 -> 1.132 standalone; 252 VGPRs, the
+      // m/n-contiguous layouts would spill)
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 4>(g, grid, s);
+      return launch_fast_v<AKC, BKC, 0>(g, grid, s);
   }
 }
 
@@ -641,6 +697,11 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   g.dseed = drop_seed; g.doff = drop_offset; g.dkeep = 1.f - drop_p; g.dscale = 1.f / (1.f - drop_p);
   g.ws = ws;
   g.alpha = nullptr;
+  static const int abl = [] {
+    const char* e = getenv("MLVAE_GEMM_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  g.abl = abl;
   int s, kc;
   fast_plan(M, N, K, batch, &s, &kc);
   if (s > 1 && (N % 4 != 0 || !ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
@@ -716,7 +777,7 @@ extern "C" int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const
   g.bias1 = bias1; g.bias2 = bias2; g.epi = EPI_NONE; g.aux = nullptr; g.ldaux = 0;
   g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
   g.dseed = 0; g.doff = 0; g.dkeep = 1.f; g.dscale = 1.f;
-  g.ws = nullptr; g.alpha = alpha;
+  g.ws = nullptr; g.alpha = alpha; g.abl = 0;
   g.splits = 1; g.kchunk = ((g.K + TBK - 1) / TBK) * TBK;
   if (g.K == 0) g.kchunk = TBK;
   static const int group_m = [] {
