@@ -82,13 +82,31 @@ __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
   const int ldw = KC + SKEW, ldxl = CinP + SKEW, p = (K - 1) / 2;
   short* Wl = smem;                          // [Cout][K * CinP]
   short* Xl = smem + a.Cout * ldw;           // [BM + K - 1][CinP]
-  // packed bf16 weights, once per workgroup: Wl[o][j * CinP + c]
-  for (int e = threadIdx.x; e < a.Cout * KC; e += CT) {
-    const int o = e / KC, rem = e - o * KC, j = rem / CinP, c = rem - j * CinP;
-    float v = 0.f;
-    if (c < a.Cin)
-      v = DG ? a.w[((size_t)c * a.Lc + o) * K + (K - 1 - j)] : a.w[((size_t)o * a.Lc + c) * K + j];
-    Wl[o * ldw + rem] = f2bf(v);
+  // packed bf16 weights, once per workgroup: Wl[o][j * CinP + c].  The fp32 weight is read in
+  // its own order (coalesced 16-byte loads) and scattered into the LDS image; the padding
+  // channels c in [Cin, CinP) are zeroed first.
+  if (a.Cin < CinP) {
+    const int padc = CinP - a.Cin;
+    for (int e = threadIdx.x; e < a.Cout * K * padc; e += CT) {
+      const int o = e / (K * padc), rem = e - o * K * padc, j = rem / padc, c = a.Cin + rem - j * padc;
+      Wl[o * ldw + j * CinP + c] = 0;
+    }
+  }
+  {
+    const int total4 = a.Cout * a.Cin * K / 4;  // the layer weight [Lo][Li][K], Lo * Li * K elements
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(a.w);
+    for (int e4 = threadIdx.x; e4 < total4; e4 += CT) {
+      const f32x4 v = w4[e4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int idx = 4 * e4 + r, j = idx % K, rc = idx / K;
+        const int lo = rc / a.Lc, li = rc - lo * a.Lc;  // layer (out, in) channel
+        // forward: product row o = lo, column c = li, tap j; input gradient: o = li, c = lo,
+        // tap K - 1 - j (transposed, time-flipped)
+        const int o = DG ? li : lo, c = DG ? lo : li, jj = DG ? K - 1 - j : j;
+        Wl[o * ldw + jj * CinP + c] = f2bf(v[r]);
+      }
+    }
   }
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -286,7 +304,7 @@ extern "C" int mlvae_conv1d_fwd(int B, int T, int Cin, int Cout, int K, const fl
                                 const float* bias, int act, float* y, int ldy, void* stream) {
   if (B <= 0 || T <= 0) return 0;
   if (!dims_ok(B, T, Cin, Cout, K) || !x || !w || !y || ldx < Cin || ldy < Cout || ldx % 4 || ldy % 4 ||
-      !aligned16(x) || !aligned16(y)) {
+      !aligned16(x) || !aligned16(y) || !aligned16(w)) {
     mlvae_set_error("mlvae_conv1d_fwd: unsupported shape/stride/alignment (Cin %d Cout %d K %d)", Cin, Cout, K);
     return 1;
   }
@@ -302,7 +320,7 @@ extern "C" int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const 
                                   void* stream) {
   if (B <= 0 || T <= 0) return 0;
   if (!dims_ok(B, T, Cout, Cin, K) || !dy || !w || !dx || lddy < Cout || lddx < Cin || lddy % 4 || lddx % 4 ||
-      (aux && (ldaux < Cin || ldaux % 4 || !aligned16(aux))) || !aligned16(dy) || !aligned16(dx)) {
+      (aux && (ldaux < Cin || ldaux % 4 || !aligned16(aux))) || !aligned16(dy) || !aligned16(dx) || !aligned16(w)) {
     mlvae_set_error("mlvae_conv1d_dgrad: unsupported shape/stride/alignment (Cin %d Cout %d K %d)", Cin, Cout, K);
     return 1;
   }
