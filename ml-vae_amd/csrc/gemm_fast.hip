@@ -410,7 +410,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   }
   for (int it = 0; it < nk; ++it) {
     const int cur = it & 1;
-    if (it + 1 < nk && !(g.abl & 2)) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
+    if (it + 1 < nk && !(VAR == 6 && (g.abl & 2))) stage_both(cur ^ 1, kbeg + (it + 1) * TBK);
     const short* As = lds + (cur * 2 + 0) * IMG;
     const short* Bs = lds + (cur * 2 + 1) * IMG;
 #pragma unroll
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wn * 64 + j * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < 8; ++i) af[i] = frag<AKC>(As, wm * 128 + i * 16, kk, lane);
-      if (g.abl & 1) {  // ablation: fragments read, no MFMA
+      if (VAR == 6 && (g.abl & 1)) {  // ablation build (VAR 6): fragments read, no MFMA
 #pragma unroll
         for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i]));
 #pragma unroll
@@ -590,6 +590,7 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
     case 3: return launch_fast_v<AKC, BKC, 3>(g, grid, s);
     case 4: return launch_fast_v<AKC, BKC, 4>(g, grid, s);
     case 5: return launch_fast_v<AKC, BKC, 0>(g, grid, s);  // the previous default (A/B)
+    case 6: return launch_fast_v<AKC, BKC, 6>(g, grid, s);  // VAR 0 with the MLVAE_GEMM_ABL switches
     case 8:
       if constexpr (AKC && BKC) return launch_fast_v<true, true, 8>(g, grid, s);
       return 1;

@@ -1,6 +1,6 @@
 """GEMM ablation timing (diagnostics): the c3 projection / dgrad / wgrad shapes on the 256² kernel
 with MLVAE_GEMM_ABL set by the caller (1: no MFMA, 2: no staging loads, 3: neither).
-usage: MLVAE_GEMM_ABL=N python tools/gemm_abl.py"""
+usage: MLVAE_GEMM_VAR=6 MLVAE_GEMM_ABL=N python tools/gemm_abl.py [proj dgrad wgrad]"""
 import os
 import sys
 
