@@ -397,7 +397,7 @@ class VAEEngine:
     @classmethod
     def from_modules(cls, encoder, decoder, device="cuda", prec="fp32", kld_weight=1e-3,
                      recon_weight=1.0, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                     max_grad_norm=5.0, seed=123456):
+                     max_grad_norm=5.0, seed=123456, fp8=False):
         """Build an engine whose flat buffer becomes the storage of the given modules'
         parameters (VanillaVAE + Decoder, as the recipe yaml builds them): after this call
         module.parameters() are views of engine.flat and their .grad views of engine.grad."""
@@ -413,7 +413,7 @@ class VAEEngine:
                         L=decoder.rnn.num_layers, C=heads[0][0].out_features,
                         dropout=float(decoder.rnn.dropout), loss_type=decoder.loss_type,
                         kld_weight=kld_weight, recon_weight=recon_weight, lr=lr, betas=tuple(betas),
-                        adam_eps=eps, max_grad_norm=max_grad_norm, prec=prec)
+                        adam_eps=eps, max_grad_norm=max_grad_norm, prec=prec, fp8=fp8)
         params = OrderedDict()
         for pre, mod in (("encoder.", encoder), ("decoder.", decoder)):
             for n, p in mod.named_parameters():

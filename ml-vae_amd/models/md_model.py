@@ -74,6 +74,9 @@ class MDModel(Brain):
             from mlvae_hip.optim import EngineOptimizer
             kw = fused.keywords
             prec = getattr(self.hparams, "precision", "fp32")
+            fp8 = prec == "fp8"  # configs[4]: bf16 step with the fp8 layer-1 input projection
+            if fp8:
+                prec = "bf16"
             if self.auto_mix_prec and prec != "bf16":
                 # --auto_mix_prec (the reference's fp16 autocast + GradScaler, ref:src/models/
                 # md_model.py:60-76): the fused step's mixed-precision mode is bf16 operands with
@@ -87,14 +90,20 @@ class MDModel(Brain):
                 kld_weight=self._weight_for("kld_loss"), recon_weight=self._weight_for("recon_loss"),
                 lr=kw.get("lr", 1e-3), betas=kw.get("betas", (0.9, 0.999)), eps=kw.get("eps", 1e-8),
                 max_grad_norm=self.max_grad_norm,
-                seed=int(torch.randint(0, 2 ** 62, (1,)).item()))
+                seed=int(torch.randint(0, 2 ** 62, (1,)).item()), fp8=fp8)
             self.optimizers = {"optimizer": EngineOptimizer(self.engine)}
             if self.world_size > 1:  # data parallel: global offsets, broadcast weights, grad all-reduce
                 from mlvae_hip import dist as mdist
                 mdist.attach(self.engine, self.rank, self.world_size,
                              int(getattr(self.hparams, "batch_size", 8)))
         else:
+            from mlvae_hip import ops
             from mlvae_hip import optim as hip_optim
+            # module mode: the HIP ops' operand precision from the yaml's `precision` (fp8 has
+            # no module-mode kernels: its bf16 step)
+            prec = getattr(self.hparams, "precision", None)
+            if prec is not None:
+                ops.set_precision("bf16" if prec == "fp8" else prec)
             self.optimizers = {}
             for key, info in infos.items():
                 if isinstance(info, dict):

@@ -34,3 +34,20 @@ def test_train_and_test_scripts(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     m = open(tmp_path / "out" / "test_output" / "test_metrics.txt").read()
     assert "kld_loss.loss" in m and "recon_loss.loss" in m
+
+
+@pytest.mark.parametrize("model_class,precision", [("test_conv_vae", "bf16"), ("test_vanilla_vae", "fp8")])
+def test_recipe_variants(tmp_path, model_class, precision):
+    """configs[3]'s Conv1d-encoder recipe (models/test_conv_vae) and configs[4]'s fp8 mode
+    (`precision: fp8`) through train.py on the fused engine."""
+    from gpu_utils import need_gpu
+    need_gpu()
+    args = ["train.py", "config/run.yaml", "--model_class", model_class, "--model_name", f"vae_{precision}",
+            "--model", f"!include:../models/{model_class}/model.yaml", "--output_dir", str(tmp_path / "out"),
+            "--extra_overrides", "{model: {n_epochs: 1, input_size: 80, dec_rnn_hidden_size: 512, "
+                                 "precision: " + precision + "}}"]
+    r = _run(args, PKG)
+    assert r.returncode == 0, r.stderr[-3000:]
+    log = open(tmp_path / "out" / "train_log.txt").read()
+    assert "epoch: 1" in log and "valid loss" in log, log[-2000:]
+    assert ("ConvVAE" in log) == (model_class == "test_conv_vae")
