@@ -75,6 +75,10 @@ size_t mlvae_gemm_bf16_workspace_size(int M, int N, int K, int batch);
  * launching thread right before the launches it should shape (the engine lowers it for weight
  * gradients that overlap a recurrence).  Workspace sizes assume the default or lower. */
 int mlvae_gemm_bf16_set_split_target(int workgroups);
+/* main-loop variant of mlvae_gemm_bf16 (0 = the default per operand layout; others are the
+ * kernel's measured alternatives, for same-process A/B timing); returns the previous value
+ * (values < 0 only query).  Initialised from MLVAE_GEMM_VAR.  Host-side planning state. */
+int mlvae_gemm_bf16_set_variant(int var);
 int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch, const void* A,
                     int lda, long long a_bstride, const void* B, int ldb, long long b_bstride,
                     float* C, int ldc, long long c_bstride, float beta, const float* bias1,

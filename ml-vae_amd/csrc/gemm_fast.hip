@@ -60,6 +60,18 @@ typedef __attribute__((address_space(3))) bf16x4* lds_b4_t;
 
 __device__ __forceinline__ unsigned mc_swz(int r) { return 2u * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
+// Time-shifted K rows (the recurrent dW_hh: row k reads k + sh when 0 <= k % T + sh < T): time
+// index of row k0 + kr, kr < span.  k0 % T is wave-uniform (one scalar division per stage); a
+// lane then needs one conditional subtract when T >= span (wgrad hh: 1.6x faster staging than a
+// per-lane modulo)
+__device__ __forceinline__ bool shift_ok(int k0, int kr, int shT, int sh, int span) {
+  int t = k0 % shT + kr;
+  if (shT >= span) t = t >= shT ? t - shT : t;
+  else t %= shT;
+  t += sh;
+  return t >= 0 && t < shT;
+}
+
 // Issue this wave's 4 LDS-DMA pieces (1 KB each) of one 256 x 64 operand tile.
 //   KC: element (row, k) at p[row * ld + k];   MC: element (row, k) at p[k * ld + row]
 // rows [r0, r0 + 256) bounded by R; k [k0, k0 + 64) bounded by kend (and by the time shift).
@@ -80,41 +92,14 @@ __device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, int
       int gk = k0 + kr;
       const int gr = r0 + 8 * c;
       bool ok = gk < kend && gr < R;
-      if (sh != 0 && ok) {
-        const int t = gk % shT + sh;
-        ok = t >= 0 && t < shT;
+      if (sh != 0) {
+        ok = ok && shift_ok(k0, kr, shT, sh, TBK);
         gk += sh;
       }
       off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
   }
-}
-
-// One of the 4 pieces of stage(): the interleaved main loop spreads them between MFMAs.
-template <bool KC>
-__device__ __forceinline__ void stage_piece(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
-                                            int k0, int kend, int shT, int sh, int wave, int lane, int j) {
-  const int piece = wave * 4 + j;
-  const int p = piece * 64 + lane;
-  unsigned off;
-  if constexpr (KC) {
-    const int row = p >> 3, c = (p & 7) ^ (row & 7);
-    const int gr = r0 + row, gk = k0 + 8 * c;
-    off = (gr < R && gk < kend) ? (unsigned)(((size_t)gr * ld + gk) * 2) : OOB;
-  } else {
-    const int kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr);
-    int gk = k0 + kr;
-    const int gr = r0 + 8 * c;
-    bool ok = gk < kend && gr < R;
-    if (sh != 0 && ok) {
-      const int t = gk % shT + sh;
-      ok = t >= 0 && t < shT;
-      gk += sh;
-    }
-    off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
-  }
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
 }
 
 // MFMA 16x16x32 operand fragment: lane l gets rows/cols (base + (l & 15)), k = kk + 8 (l >> 4) + j.
@@ -135,23 +120,21 @@ __device__ __forceinline__ bf16x8 frag(const short* img, int base, int kk, int l
   }
 }
 
-// ---- deep-pipelined variant: BK = 32, four LDS buffers (4 x 32 KB), three K-steps in flight.
-// The 2-buffer loop above drains vmcnt(0) at every K-step, so each 64-deep step waits for the
-// next step's loads issued only one step earlier; at B*T = 128,000 rows (the metric's batch)
-// that latency, not the MFMA, set the projection's 37 % of peak.  Here K-step it+3 is staged
-// right after the barrier that retires K-step it, and the wait before each step is a counted
-// vmcnt that leaves the two younger steps in flight (raw s_barrier: no implicit drain).
+// ---- BK = 32 ring (VAR 12): four LDS buffers (4 x 32 KB), three K-steps in flight behind a
+// counted vmcnt (raw s_barrier: no implicit drain).  The 2-buffer loop drains vmcnt(0) at every
+// K-step, so each 64-deep step waits for loads issued only one step earlier.
 constexpr int DBK = 32, DNB = 4;
 constexpr int DIMG = TBM * DBK;  // elements per operand image (16 KB)
 
 __device__ __forceinline__ int kc_swz(int row) { return ((row >> 2) & 1) << 1; }  // 32-k rows
 
-template <bool KC>
+// NP pieces (1 KB each) per wave: 2 with all 8 waves staging, 4 with one 4-wave group
+template <bool KC, int NP = 2>
 __device__ __forceinline__ void stage32(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
                                         int k0, int kend, int shT, int sh, int wave, int lane) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int piece = wave * 2 + j;
+  for (int j = 0; j < NP; ++j) {
+    const int piece = wave * NP + j;
     const int p = piece * 64 + lane;
     unsigned off;
     if constexpr (KC) {  // [256 rows][32 k]: 4 chunks per row, chunk c at slot c ^ kc_swz(row)
@@ -163,9 +146,8 @@ __device__ __forceinline__ void stage32(short* img, __amdgpu_buffer_rsrc_t rs, i
       int gk = k0 + kr;
       const int gr = r0 + 8 * c;
       bool ok = gk < kend && gr < R;
-      if (sh != 0 && ok) {
-        const int t = gk % shT + sh;
-        ok = t >= 0 && t < shT;
+      if (sh != 0) {
+        ok = ok && shift_ok(k0, kr, shT, sh, DBK);
         gk += sh;
       }
       off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
@@ -211,22 +193,32 @@ __device__ __forceinline__ i32x8 frag8(const short* img, int base, int lane) {
   return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
 }
 
-// VAR 0: stage the next K-tile's 8 pieces per wave at the top of the K-step; 1: DEEP (BK 32,
-// 3 K-steps in flight); 2/3: the 8 pieces spread one per 8 MFMAs (3: + scheduling hints);
+// VAR 0: stage the next K-tile's 8 pieces per wave at the top of the K-step (two buffers);
+// 4: VAR 0 with both k-halves' fragments read up front; 12: ping-pong over a BK-32 ring;
 // 8: fp8 e4m3 operands (both k-contiguous), one 16x16x128 block-scaled MFMA (unit scales) per
 // tile pair and K-tile of 128 -- twice the bf16 MFMA rate, the same staging bytes per K-tile
 template <bool AKC, bool BKC, int VAR>
 __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
-  constexpr bool DEEP = VAR == 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   short* lds = reinterpret_cast<short*>(smem);   // [buf][A image, B image]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int TM = (g.M + TBM - 1) / TBM, TN = (g.N + TBN - 1) / TBN, ntiles = TM * TN;
-  int tile;
-  {  // XCD-aware bijective order: each XCD works a contiguous run of tiles (shared A panels)
+  int tile, bz = blockIdx.y, kz = blockIdx.z;
+  if (gridDim.y * gridDim.z == 1) {  // XCD-aware bijective order: each XCD works a contiguous run of tiles
     const int b = blockIdx.x, xcd = b % 8, local = b / 8, q = ntiles / 8, r = ntiles % 8;
     tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  } else {
+    // batched / split-K: the same over the flat (split, batch, tile) space, split-major, so an
+    // XCD works whole K-ranges -- every A and B chunk of a K-range comes from HBM once into that
+    // XCD's L2 (wgrad hh at c3: 16 tiles x 16 splits read the h operand 8x before)
+    const int nb = gridDim.x * gridDim.y * gridDim.z;
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = b % 8, local = b / 8, q = nb / 8, r = nb % 8;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+    tile = w % (int)gridDim.x;
+    bz = (w / (int)gridDim.x) % (int)gridDim.y;
+    kz = w / ((int)gridDim.x * (int)gridDim.y);
   }
   int mt = tile / TN, nt = tile % TN;
   if (g.group_m > 1) {  // grouped order: concurrent tiles share group_m A panels and fewer B panels
@@ -236,15 +228,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     nt = in / gsz;
   }
   const int m0 = mt * TBM, n0 = nt * TBN;
-  const int bz = blockIdx.y;
   const short* Ap = g.A + bz * g.a_bs;
   const short* Bp = g.B + bz * g.b_bs;
   const int sh = g.kshift + bz * g.kshift_bstep;
   const auto ra = make_rsrc(Ap, OOB);
   const auto rb = make_rsrc(Bp, OOB);
-  const int kbeg = blockIdx.z * g.kchunk;
+  const int kbeg = kz * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + (DEEP ? DBK : TBK) - 1) / (DEEP ? DBK : TBK) : 0;
+  constexpr int SBK = VAR == 12 ? DBK : TBK;  // K per main-loop step
+  const int nk = kend > kbeg ? (kend - kbeg + SBK - 1) / SBK : 0;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -252,80 +244,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (DEEP) {
-    auto stage4 = [&](int it) {  // K-step it into buffer it & 3
-      const int buf = it & (DNB - 1), k0 = kbeg + it * DBK;
-      stage32<AKC>(lds + (buf * 2 + 0) * DIMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
-      stage32<BKC>(lds + (buf * 2 + 1) * DIMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
-    };
-    for (int it = 0; it < 3 && it < nk; ++it) stage4(it);
-    for (int it = 0; it < nk; ++it) {
-      // K-step it's pieces (4 per wave) have landed once at most the younger steps' remain
-      const int younger = min(2, nk - 1 - it);
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // ... everyone's; and step it-1's buffer is free
-      if (it + 3 < nk) stage4(it + 3);
-      const short* As = lds + ((it & (DNB - 1)) * 2 + 0) * DIMG;
-      const short* Bs = lds + ((it & (DNB - 1)) * 2 + 1) * DIMG;
-      bf16x8 af[8], bfr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag32<BKC>(Bs, wn * 64 + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = frag32<AKC>(As, wm * 128 + i * 16, lane);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
-  } else if constexpr (VAR == 2 || VAR == 3) {
-    auto piece = [&](int buf, int k0, int pc) {
-      if (pc < 4)
-        stage_piece<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane, pc);
-      else
-        stage_piece<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane,
-                         pc - 4);
-    };
-    if (nk > 0) {
-#pragma unroll
-      for (int pc = 0; pc < 8; ++pc) piece(0, kbeg, pc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    for (int it = 0; it < nk; ++it) {
-      const int cur = it & 1;
-      const bool more = it + 1 < nk;
-      const int k1 = kbeg + (it + 1) * TBK;
-      const short* As = lds + (cur * 2 + 0) * IMG;
-      const short* Bs = lds + (cur * 2 + 1) * IMG;
-#pragma unroll
-      for (int kk = 0; kk < TBK; kk += 32) {
-        bf16x8 af[8], bfr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wn * 64 + j * 16, kk, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) af[i] = frag<AKC>(As, wm * 128 + i * 16, kk, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (more && (i & 1) == 0) piece(cur ^ 1, k1, (kk / 32) * 4 + i / 2);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-          if constexpr (VAR == 3) {
-            if ((i & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                     // four MFMAs
-          }
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-tile it+1 has landed (this wave's pieces)
-      __syncthreads();                                 // ... everyone's; buffer cur is free
-    }
-  } else if constexpr (VAR == 4) {
+  if constexpr (VAR == 4) {
     // VAR 4: both k-halves' fragments (24 ds_reads) issued right after the barrier, so the
     // second half's MFMAs never wait on an LDS round trip in mid-step
     auto stage_both = [&](int buf, int k0) {
@@ -366,6 +285,64 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else if constexpr (VAR == 12) {
+    // VAR 12: ping-pong.  Two groups of four waves -- waves 0-3 and 4-7, one of each on every
+    // SIMD -- run one barrier apart over a ring of four BK-32 buffers: while one group's waves
+    // issue their 32 MFMAs, the other group's read their next fragments from LDS and stage a
+    // future K-step, so each SIMD's MFMA pipe is fed by one wave or the other at every moment
+    // (the 8-phase idea of cdna_hip_programming.md §5, two slots per K-step).  Slot sequence of
+    // a wave: M(it) = fragment reads of step it + its group's half of step it+3 (group 0 the A
+    // image, group 1 the B image) + waits, barrier, C(it) = 32 MFMAs, barrier.  Group 1 starts
+    // one barrier late.  RAW: step it+1 is waited for (counted vmcnt: it+2, it+3 stay in
+    // flight) before the barrier that ends each group's M(it), and the other group reads it
+    // only after that barrier.  WAR: step it+3 goes into the buffer of step it-1, whose reads
+    // both groups retired (lgkmcnt(0)) before their barriers of the previous slots.
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int grpw = wv >> 2, w4 = wv & 3;
+    auto share = [&](int it) {
+      const int buf = it & (DNB - 1), k0 = kbeg + it * DBK;
+      if (grpw == 0)
+        stage32<AKC, 4>(lds + (buf * 2 + 0) * DIMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, w4, lane);
+      else
+        stage32<BKC, 4>(lds + (buf * 2 + 1) * DIMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, w4, lane);
+    };
+    auto wait_younger = [&](int n) {  // this wave's shares: all but the n youngest landed
+      if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    const int npre = min(3, nk);
+    for (int it = 0; it < npre; ++it) share(it);
+    if (nk > 0) wait_younger(npre - 1);
+    __builtin_amdgcn_s_barrier();
+    if (grpw == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one slot behind
+    bf16x8 af[8], bfr[4];
+    for (int it = 0; it < nk; ++it) {
+      {
+        const short* As = lds + ((it & (DNB - 1)) * 2 + 0) * DIMG;
+        const short* Bs = lds + ((it & (DNB - 1)) * 2 + 1) * DIMG;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag32<BKC>(Bs, wn * 64 + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = frag32<AKC>(As, wm * 128 + i * 16, lane);
+      }
+      if (it + 3 < nk) share(it + 3);
+      if (it + 1 < nk) wait_younger(min(2, nk - it - 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);  // the MFMAs stay in their slot
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (grpw == 0) __builtin_amdgcn_s_barrier();  // both groups pass the same number of barriers
+    __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
   } else if constexpr (VAR == 8) {
     static_assert(AKC && BKC, "fp8 operands are k-contiguous");
     auto stage_both = [&](int buf, int k0) {
@@ -451,7 +428,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   const bool split = g.splits > 1;
   float* Cb = g.c16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(g.C) + bz * g.c_bs)
                     : g.C + bz * g.c_bs;
-  float* wsz = split ? g.ws + ((size_t)bz * g.splits + blockIdx.z) * (size_t)g.M * g.N : nullptr;
+  float* wsz = split ? g.ws + ((size_t)bz * g.splits + kz) * (size_t)g.M * g.N : nullptr;
   const bool vec = (g.ldc % 4) == 0 && (((uintptr_t)Cb) % 16) == 0;
   // Row-contiguous epilogue through the (now free) LDS: four passes of 64 tile rows; every
   // store instruction then writes one whole 1 KB row segment instead of 16 rows x 64 B
@@ -585,20 +562,20 @@ int launch_fast_v(const GFArgs& g, dim3 grid, hipStream_t s) {
 template <bool AKC, bool BKC>
 int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
   switch (var) {
-    case 1: return launch_fast_v<AKC, BKC, 1>(g, grid, s);
-    case 2: return launch_fast_v<AKC, BKC, 2>(g, grid, s);
-    case 3: return launch_fast_v<AKC, BKC, 3>(g, grid, s);
-    case 4: return launch_fast_v<AKC, BKC, 4>(g, grid, s);
+    case 4:
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 4>(g, grid, s);
+      return launch_fast_v<AKC, BKC, 0>(g, grid, s);
     case 5: return launch_fast_v<AKC, BKC, 0>(g, grid, s);  // the previous default (A/B)
     case 6: return launch_fast_v<AKC, BKC, 6>(g, grid, s);  // VAR 0 with the MLVAE_GEMM_ABL switches
+    case 12: return launch_fast_v<AKC, BKC, 12>(g, grid, s);
     case 8:
       if constexpr (AKC && BKC) return launch_fast_v<true, true, 8>(g, grid, s);
       return 1;
     default:
-      // k-contiguous x k-contiguous (projection, dgrad): both k-halves' fragments up front
-      // (VAR 4: c3 projection 1.329 -> 1.314 ms, dgrad 1.148 -> 1.132 standalone; 252 VGPRs, the
-      // m/n-contiguous layouts would spill)
-      if constexpr (AKC && BKC) return launch_fast_v<true, true, 4>(g, grid, s);
+      // k-contiguous A (projection, dgrad): the ping-pong ring (same-process A/B at c3 against
+      // VAR 4: projection 1.328 -> 1.287 ms, dgrad 1.134 -> 1.098 (W^T) / 1.361 -> 1.252 (W),
+      // 4096^3 1,119 -> 1,217 TF/s); m-contiguous A (weight gradients): VAR 0
+      if constexpr (AKC) return launch_fast_v<true, BKC, 12>(g, grid, s);
       return launch_fast_v<AKC, BKC, 0>(g, grid, s);
   }
 }
@@ -611,6 +588,17 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
 // bandwidth to the latency-bound hand-off chain (c2: 256 -> 128 takes 0.15 ms off the step).
 int g_split_target = 256;
 int split_target() { return g_split_target; }
+
+// main-loop variant (gemm256_kernel VAR; 0 = the default per operand layout): MLVAE_GEMM_VAR or
+// mlvae_gemm_bf16_set_variant() select another for same-process A/B timing
+int g_variant = -1;
+int gemm_variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("MLVAE_GEMM_VAR");
+    g_variant = e ? atoi(e) : 0;
+  }
+  return g_variant;
+}
 
 void fast_plan(int M, int N, int K, int batch, int* splits, int* kchunk) {
   const long tiles = (long)((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN) * batch;
@@ -634,6 +622,12 @@ void fast_plan(int M, int N, int K, int batch, int* splits, int* kchunk) {
 extern "C" int mlvae_gemm_bf16_set_split_target(int workgroups) {
   const int prev = g_split_target;
   if (workgroups >= 1) g_split_target = workgroups;
+  return prev;
+}
+
+extern "C" int mlvae_gemm_bf16_set_variant(int var) {
+  const int prev = gemm_variant();
+  if (var >= 0) g_variant = var;
   return prev;
 }
 
@@ -722,13 +716,11 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), batch, s);
   int rc;
-  // main-loop variant (gemm256_kernel VAR): MLVAE_GEMM_VAR overrides (A/B timing).  The deep
-  // BK-32 pipeline (1) measured slower at every c3 shape (proj 1359 vs 1324 us, wgrad 1469 vs
-  // 1236 us)
-  static const int var = [] {
-    const char* e = getenv("MLVAE_GEMM_VAR");
-    return e ? atoi(e) : 0;
-  }();
+  // main-loop variant (gemm256_kernel VAR): MLVAE_GEMM_VAR / set_variant override (A/B timing).
+  // Measured and dropped: a BK-32 four-buffer loop without ping-pong (proj 1359 vs 1324 us, wgrad
+  // 1469 vs 1236), the same with register-double-buffered fragments (proj 1.38 vs 1.31 ms), the
+  // staging pieces spread one per 8 MFMAs (+-1 %)
+  const int var = gemm_variant();
   if (akc && bkc) rc = launch_fast<true, true>(g, grid, st, var);
   else if (akc) rc = launch_fast<true, false>(g, grid, st, var);
   else if (bkc) rc = launch_fast<false, true>(g, grid, st, var);

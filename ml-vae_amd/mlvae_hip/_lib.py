@@ -31,6 +31,7 @@ _SIGS = {
     "mlvae_cast_bf16_t": [I, I, P, P, P],
     "mlvae_gemm_bf16_workspace_size": [I, I, I, I],
     "mlvae_gemm_bf16_set_split_target": [I],
+    "mlvae_gemm_bf16_set_variant": [I],
     "mlvae_gemm_bf16": [I, I, I, I, I, I, P, I, C.c_longlong, P, I, C.c_longlong, P, I, C.c_longlong,
                         F, P, P, I, P, I, I, I, I, U64, U64, F, P, SZ, P],
     "mlvae_lstm_workspace_size": [I, I, I, C.POINTER(SZ)],

@@ -60,7 +60,29 @@ def _time(call, iters, M, Nc, K):
     return ms, 2.0 * M * Nc * K / ms / 1e9
 
 
+def ab(vars_, rounds=3):
+    """Same-process A/B of gemm256 main-loop variants (GEMM_VARS=0,10): interleaved rounds, the
+    median and min per variant (cdna_hip_programming.md §5.4 rule 24)."""
+    l = lib()
+    only = os.environ.get("GEMM_ONLY")
+    for name, ta, tb, M, Nc, K in SHAPES:
+        if (only and only not in name) or K == 32:
+            continue
+        res = {v: [] for v in vars_}
+        for _ in range(rounds):
+            for v in vars_:
+                l.mlvae_gemm_bf16_set_variant(v)
+                res[v].append(run(ta, tb, M, Nc, K, 1)[0])
+        l.mlvae_gemm_bf16_set_variant(0)
+        flops = 2.0 * M * Nc * K
+        print(f"{name} M={M:6d} N={Nc:5d} K={K:6d} | " + " | ".join(
+            f"VAR {v}: med {sorted(t)[len(t) // 2] * 1e3:7.1f} us min {min(t) * 1e3:7.1f} us "
+            f"{flops / min(t) / 1e9:6.1f} TF" for v, t in res.items()), flush=True)
+
+
 def main():
+    if os.environ.get("GEMM_VARS"):
+        return ab([int(v) for v in os.environ["GEMM_VARS"].split(",")])
     only = os.environ.get("GEMM_ONLY")        # substring of a shape name: run just that one
     modes = [int(m) for m in os.environ.get("GEMM_MODES", "0,1,2").split(",")]
     for name, ta, tb, M, Nc, K in SHAPES:
