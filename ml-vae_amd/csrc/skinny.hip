@@ -123,6 +123,72 @@ __global__ __launch_bounds__(256) void skinny_nt_ks_kernel(int M, int K, const u
         ((acc[j] + red[0][j][lane]) + red[1][j][lane]) + red[2][j][lane];
 }
 
+// 128-row workgroups (8 waves x 16 rows, each over the whole K) with Bt streamed through LDS in
+// 256-wide K-chunks that all eight waves share: the ks form above re-read Bt from L2 for every
+// 16 rows (twice the bytes of its A stream) and held 2.5 TB/s on the 1 GB dG of c3 (409 us).
+// A chunk c+1 (16 B x 8 per lane, 64 KB per workgroup in flight) and Bt chunk c+1 are loaded
+// while chunk c's MFMAs run.  K % 256 == 0.
+constexpr int NTL_KC = 256, NTL_LB = NTL_KC + 8;  // K-chunk, LDS row stride (shorts)
+template <int NT>
+__global__ __launch_bounds__(512) void skinny_nt_lds_kernel(int M, int K, const unsigned short* __restrict__ A,
+                                                            int lda, const unsigned short* __restrict__ Bt,
+                                                            int ldb, float* __restrict__ C, int ldc) {
+  constexpr int NB = 16 * NT, BPT = (NB * NTL_KC / 8 + 511) / 512;  // 16-byte Bt pieces per thread
+  __shared__ __attribute__((aligned(16))) short sb[2][NB * NTL_LB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int row = blockIdx.x * 128 + wave * 16 + l15;
+  const bool rv = row < M;
+  const unsigned short* ap = A + (size_t)(rv ? row : 0) * lda + 8 * q;
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 ac[8], an[8];
+  u32x4 br[BPT];
+  auto aload = [&](int k0, bf16x8 (&d)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) d[u] = rv ? *reinterpret_cast<const bf16x8*>(ap + k0 + 32 * u) : z8;
+  };
+  auto bload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int idx = tid + 512 * i, r = idx / (NTL_KC / 8), c8 = idx % (NTL_KC / 8);
+      if (idx < NB * NTL_KC / 8) br[i] = *reinterpret_cast<const u32x4*>(Bt + (size_t)r * ldb + k0 + 8 * c8);
+    }
+  };
+  auto bstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int idx = tid + 512 * i, r = idx / (NTL_KC / 8), c8 = idx % (NTL_KC / 8);
+      if (idx < NB * NTL_KC / 8) *reinterpret_cast<u32x4*>(&sb[buf][r * NTL_LB + 8 * c8]) = br[i];
+    }
+  };
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nc = K / NTL_KC;
+  aload(0, ac);
+  bload(0);
+  bstore(0);
+  __syncthreads();
+  for (int c = 0; c < nc; ++c) {
+    const bool more = c + 1 < nc;
+    if (more) { aload((c + 1) * NTL_KC, an); bload((c + 1) * NTL_KC); }
+    const short* b = sb[c & 1];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[j] = mfma16(*reinterpret_cast<const bf16x8*>(b + (16 * j + l15) * NTL_LB + 32 * u + 8 * q), ac[u], acc[j]);
+    if (more) bstore((c + 1) & 1);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ac[u] = an[u];
+  }
+  if (!rv) return;
+  // swapped operands: lane holds C[row][16j + 4q + r]
+#pragma unroll
+  for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + 16 * j + 4 * q) = acc[j];
+}
+
 // LDS images: A [64 frames][64 m + 8], B [64 frames][NB + 8] (bf16); transposed fragment reads.
 template <int NT>
 __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk,
@@ -283,6 +349,17 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
   const unsigned short* a = static_cast<const unsigned short*>(A);
   const unsigned short* b = static_cast<const unsigned short*>(Bt);
   hipStream_t st = (hipStream_t)stream;
+  if (K % NTL_KC == 0 && M >= 64 * 1024) {  // long row streams: Bt shared through LDS
+    dim3 g128((M + 127) / 128);
+    switch (N / 16) {
+      case 1: skinny_nt_lds_kernel<1><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      case 2: skinny_nt_lds_kernel<2><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      case 3: skinny_nt_lds_kernel<3><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      default: skinny_nt_lds_kernel<4><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+    }
+    MLVAE_CHECK_LAUNCH();
+    return 0;
+  }
   if (K % 128 == 0) {
     dim3 g16((M + 15) / 16);
     switch (N / 16) {

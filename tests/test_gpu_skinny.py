@@ -10,7 +10,8 @@ from mlvae_hip._lib import check, lib
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("M,N,K", [(16000, 32, 4096), (1000, 16, 64), (77, 48, 256), (300, 64, 96)])
+@pytest.mark.parametrize("M,N,K", [(16000, 32, 4096), (1000, 16, 64), (77, 48, 256), (300, 64, 96),
+                                   (65637, 32, 1024), (66000, 48, 256), (65536, 16, 512)])
 def test_skinny_nt(M, N, K):
     need_gpu()
     torch.manual_seed(M + N + K)
