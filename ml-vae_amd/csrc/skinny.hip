@@ -277,6 +277,9 @@ __global__ __launch_bounds__(256) void skinny_reduce(int M, int NB, int S, int n
 
 constexpr int PROJ_CN = 512;  // output columns per workgroup (64 rows x 512 cols)
 
+// Each wave stages its own 16 rows x 128 columns (wave-private LDS: no workgroup barrier) and
+// stores them as 16-byte lanes, 256 contiguous bytes per row of fp16 (the 64-column form with a
+// workgroup barrier per chunk wrote 2.8 TB/s at c3)
 template <bool F16>  // C stored as fp16 (the wide-batch recurrence's gate buffer) or fp32
 __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
                                                           const unsigned short* __restrict__ A, int lda,
@@ -284,19 +287,21 @@ __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
                                                           const float* __restrict__ b1,
                                                           const float* __restrict__ b2,
                                                           void* __restrict__ C, int ldc) {
-  constexpr int LS = 64 + 4;  // staging row stride (floats)
-  __shared__ __attribute__((aligned(16))) float stg[4][16 * LS];  // per wave: 16 rows x 64 cols
+  constexpr int CW = 128, LS = CW + 4;  // columns per pass, staging row stride (floats)
+  __shared__ __attribute__((aligned(16))) float stg[4][16 * LS];  // per wave: 16 rows x 128 cols
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rr = lane & 15, kq = lane >> 4;
-  const int r0 = blockIdx.x * 64 + wave * 16;
-  const int n0 = blockIdx.y * PROJ_CN;
+  // column block fastest: concurrent workgroups write whole rows, not one 1 KB column slice of
+  // many 8 KB rows
+  const int r0 = blockIdx.y * 64 + wave * 16;
+  const int n0 = blockIdx.x * PROJ_CN;
   const bool kin = 8 * kq < K;  // K % 8 == 0 (checked on the host)
   bf16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
   if (kin && r0 + rr < M) a = *reinterpret_cast<const bf16x8*>(A + (size_t)(r0 + rr) * lda + 8 * kq);
   float* sw = stg[wave];
-  for (int c0 = n0; c0 < n0 + PROJ_CN && c0 < N; c0 += 64) {  // N % 16 == 0; 64-column chunks
+  for (int c0 = n0; c0 < n0 + PROJ_CN && c0 < N; c0 += CW) {  // N % 16 == 0
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb) {
+    for (int jb = 0; jb < CW / 16; ++jb) {
       const int cb = c0 + 16 * jb;
       if (cb < N) {
         bf16x8 b = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -306,25 +311,31 @@ __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
         *reinterpret_cast<f32x4*>(sw + rr * LS + 16 * jb + 4 * kq) = acc;
       }
     }
-    __syncthreads();
-    // read back row-contiguous: one store instruction = 4 rows x 256 contiguous bytes
-    const int col = c0 + 4 * (lane & 15);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops complete in order
+    // read back row-contiguous: lane (row 4i + lane / 16, 8 columns at 8 (lane % 16))
+    const int col = c0 + 8 * (lane & 15);
     if (col < N) {
-      f32x4 bias = {0.f, 0.f, 0.f, 0.f};
-      if (b1) bias += *reinterpret_cast<const f32x4*>(b1 + col);
-      if (b2) bias += *reinterpret_cast<const f32x4*>(b2 + col);
+      f32x4 bl = {0.f, 0.f, 0.f, 0.f}, bh = {0.f, 0.f, 0.f, 0.f};
+      if (b1) { bl += *reinterpret_cast<const f32x4*>(b1 + col); bh += *reinterpret_cast<const f32x4*>(b1 + col + 4); }
+      if (b2) { bl += *reinterpret_cast<const f32x4*>(b2 + col); bh += *reinterpret_cast<const f32x4*>(b2 + col + 4); }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 4 * q + (lane >> 4);
-        const f32x4 v = *reinterpret_cast<const f32x4*>(sw + r * LS + 4 * (lane & 15));
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * i + (lane >> 4);
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(sw + r * LS + 8 * (lane & 15)) + bl;
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(sw + r * LS + 8 * (lane & 15) + 4) + bh;
         if (r0 + r >= M) continue;
-        if constexpr (F16)
-          *reinterpret_cast<u32x2*>(static_cast<unsigned short*>(C) + (size_t)(r0 + r) * ldc + col) = f2h4(v + bias);
-        else
-          *reinterpret_cast<f32x4*>(static_cast<float*>(C) + (size_t)(r0 + r) * ldc + col) = v + bias;
+        if constexpr (F16) {
+          const u32x2 l2 = f2h4(lo), h2 = f2h4(hi);
+          *reinterpret_cast<u32x4*>(static_cast<unsigned short*>(C) + (size_t)(r0 + r) * ldc + col) =
+              u32x4{l2[0], l2[1], h2[0], h2[1]};
+        } else {
+          float* cp = static_cast<float*>(C) + (size_t)(r0 + r) * ldc + col;
+          *reinterpret_cast<f32x4*>(cp) = lo;
+          *reinterpret_cast<f32x4*>(cp + 4) = hi;
+        }
       }
     }
-    __syncthreads();  // the staging tile is rewritten by the next chunk
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before the next pass rewrites it
   }
 }
 
@@ -386,13 +397,13 @@ extern "C" int mlvae_skinny_proj_ex(int M, int N, int K, const void* A, int lda,
                                     int ldb, const float* bias1, const float* bias2, void* C,
                                     int ldc, int c_fp16, void* stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (!A || !B || !C || K < 8 || K > 32 || K % 8 || N % 16 || lda % 8 || ldb % 8 || ldc % 4 ||
+  if (!A || !B || !C || K < 8 || K > 32 || K % 8 || N % 16 || lda % 8 || ldb % 8 || ldc % (c_fp16 ? 8 : 4) ||
       ((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16) ||
       ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16)) {
     mlvae_set_error("mlvae_skinny_proj: K in {8,16,24,32}, N %% 16, aligned 16-byte rows");
     return 1;
   }
-  dim3 grid((M + 63) / 64, (N + PROJ_CN - 1) / PROJ_CN);
+  dim3 grid((N + PROJ_CN - 1) / PROJ_CN, (M + 63) / 64);
   auto k = c_fp16 ? skinny_proj_kernel<true> : skinny_proj_kernel<false>;
   k<<<grid, 256, 0, (hipStream_t)stream>>>(
       M, N, K, static_cast<const unsigned short*>(A), lda, static_cast<const unsigned short*>(B),
