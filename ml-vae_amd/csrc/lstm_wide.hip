@@ -232,6 +232,19 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
 #pragma unroll
       for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       char* hb = himg + (s & 1) * HIMG;
+      // this step's input projection (fp16, LDS ring): read before the MFMAs, so the LDS
+      // latency is not exposed between the last MFMA and the cell update
+      float gxv[TPW][4];
+      auto read_gx = [&]() {
+        const unsigned short* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const int u = 4 * (wave * TPW + t) + q;
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = h2f(gx[g4 * HJ + u]);
+        }
+      };
+      if (s == 0) read_gx();
       if (s > 0) {
         if (IO) {
           if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
@@ -269,6 +282,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
         if (IO) io_load(s + 1);
+        read_gx();
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) {
           const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
@@ -282,16 +296,14 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
         STAMP(3);
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
-      const unsigned short* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
       char* ob = outr + (s & 1) * 16 * OUB + bi * OUB;
       float hvals[TPW], gates[TPW][4];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
-        const int u = 4 * (wave * TPW + t) + q;
-        const float ig = sigmoid_fast(acc[t][0] + h2f(gx[u]));
-        const float fg = sigmoid_fast(acc[t][1] + h2f(gx[HJ + u]));
-        const float gg = tanh_fast(acc[t][2] + h2f(gx[2 * HJ + u]));
-        const float og = sigmoid_fast(acc[t][3] + h2f(gx[3 * HJ + u]));
+        const float ig = sigmoid_fast(acc[t][0] + gxv[t][0]);
+        const float fg = sigmoid_fast(acc[t][1] + gxv[t][1]);
+        const float gg = tanh_fast(acc[t][2] + gxv[t][2]);
+        const float og = sigmoid_fast(acc[t][3] + gxv[t][3]);
         c[t] = valid ? fg * c[t] + ig * gg : 0.f;
         hvals[t] = valid ? og * tanh_fast(c[t]) : 0.f;
         gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
@@ -302,9 +314,13 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
         const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * H + j0;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-          const float h1 = __shfl(hvals[t], lane + 16, 64);
-          const float h2 = __shfl(hvals[t], lane + 32, 64);
-          const float h3 = __shfl(hvals[t], lane + 48, 64);
+          // units 4m+1..3 of lane (bi, 0) sit in lanes bi + 16, 32, 48: VALU permlane swaps
+          // (lane row 0 of each result) instead of three LDS-routed ds_bpermute round trips
+          const unsigned hu = __float_as_uint(hvals[t]);
+          const unsigned x1 = __builtin_amdgcn_permlane16_swap(hu, hu, false, false)[1];  // row0 <- row1
+          const unsigned x2 = __builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1];  // row0 <- row2
+          const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];  // row0 <- row3
+          const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
           if (q == 0)
             publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)),
                     pack_bf16(hvals[t], h1, h2, h3, tag), same_xcd);
