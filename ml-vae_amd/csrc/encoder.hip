@@ -250,12 +250,15 @@ constexpr int slab_floats() { return 2 * EW * EW + EW * F + 3 * EW; }
 int bwd_grid(int N) {
   // cap on workgroups (each folds its tiles into one weight-gradient slab); MLVAE_ENC_BWD_GRID
   // overrides it for A/B timing
-  static const int cap = [] {
+  // default: 128 workgroups, which leave CUs to the weight-gradient GEMM beside it when the
+  // recurrence does not fill the chip (c2: 128 -> 256 costs 0.03 ms/step); 512 at B*T >= 64K
+  // frames, where the tail runs serialised on the whole chip (c3: 12.2 -> 12.0 ms/step)
+  static const int env = [] {
     const char* e = getenv("MLVAE_ENC_BWD_GRID");
-    const int v = e ? atoi(e) : 128;
-    return v < 1 ? 128 : v;
+    return e ? atoi(e) : 0;
   }();
   const int tiles = (N + 63) / 64;
+  const int cap = env >= 1 ? env : (tiles >= 1024 ? 512 : 128);
   return tiles > cap ? cap : (tiles < 1 ? 1 : tiles);
 }
 

@@ -40,7 +40,27 @@ struct HeadArgs {
   const float* x; const float* lens; const int* count; float rec_scale;
   float* P1; float* P2[2]; float* OUT[2]; float* dOUT[2]; float* dP2[2]; float* dP1; float* dY;
   float* partials;
+  float* bias_ws;  // train, optional: per-workgroup column sums [gridDim.x][NBS] of dOUT_m | dOUT_v |
+                   // dP2_m | dP2_v | dP1 (the five bias gradients before the workgroup sum)
 };
+
+// bias-gradient column sums per workgroup: [dOUT_m F | dOUT_v F | dP2_m C | dP2_v C | dP1 2C]
+template <int C, int F> constexpr int nbs() { return 2 * F + 2 * C + 2 * C; }
+
+// sum of a lane's 4 columns over the 16 rows (lanes l15) of its wave; lanes l15 == 0 add the
+// result into this wave's slot of the LDS column sums (fixed order: deterministic)
+__device__ __forceinline__ void rows16_to_lds(f32x4 v, float* dst, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float x = v[r];
+    x += __shfl_xor(x, 1, 64);
+    x += __shfl_xor(x, 2, 64);
+    x += __shfl_xor(x, 4, 64);
+    x += __shfl_xor(x, 8, 64);
+    v[r] = x;
+  }
+  if ((lane & 15) == 0) *reinterpret_cast<f32x4*>(dst + 4 * (lane >> 4)) = v;
+}
 
 __device__ __forceinline__ bf16x8 lds8(const short* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void st4bf(short* p, f32x4 v) {
@@ -69,6 +89,9 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
   static_assert(O_END * 2 <= 160 * 1024, "LDS budget");
   extern __shared__ __attribute__((aligned(16))) short sm[];
   __shared__ float red[4];
+  constexpr int NBS = nbs<C, F>();
+  __shared__ __attribute__((aligned(16))) float bred[4][NBS];  // per-wave bias column sums
+  const bool bsum = a.train && a.bias_ws != nullptr;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, q = lane >> 4;
@@ -236,6 +259,10 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       gm[r] = s * gmu;
       gv[r] = s * glv;
     }
+    if (bsum) {
+      rows16_to_lds(gm, &bred[wave][16 * j], lane);
+      rows16_to_lds(gv, &bred[wave][F + 16 * j], lane);
+    }
     if (a.train) {
       st4bf(sm + O_DO + lrow * LF + col, gm);
       st4bf(sm + O_DO + RT * LF + lrow * LF + col, gv);
@@ -279,6 +306,7 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       const int col = 16 * j + 4 * q;
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc5[j][r] *= lrelu_d(acc2[h][j][r]);
+      if (bsum) rows16_to_lds(acc5[j], &bred[wave][2 * F + h * C + 16 * j], lane);
       // dP2 image reuses this head's P2 image (P2 itself is dead after stage 3)
       st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc5[j]);
       if (rv && h < nh) *reinterpret_cast<f32x4*>(a.dP2[h] + (size_t)grow * C + col) = acc5[j];
@@ -300,6 +328,7 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       const int col = h * C + 16 * j + 4 * q;
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc6[j][r] *= lrelu_d(acc1[h * NC + j][r]);
+      if (bsum) rows16_to_lds(acc6[j], &bred[wave][2 * F + 2 * C + h * C + 16 * j], lane);
       st4bf(sm + O_P1 + lrow * L2C + col, acc6[j]);  // dP1 image reuses the P1 image
       if (rv) *reinterpret_cast<f32x4*>(a.dP1 + (size_t)grow * C2 + col) = acc6[j];
     }
@@ -312,6 +341,10 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
   float* dyrow = a.dY + (size_t)grow * H2;
   for (int n0 = 0; n0 < H2; n0 += 128) {
     __syncthreads();  // previous chunk consumed (first pass: every wave is past stage 5)
+    if (bsum && n0 == 0) {  // this workgroup's bias column sums, the four waves in a fixed order
+      for (int c = tid; c < NBS; c += 256)
+        a.bias_ws[(size_t)blockIdx.x * NBS + c] = (bred[0][c] + bred[1][c]) + (bred[2][c] + bred[3][c]);
+    }
     constexpr int PPT = 128 * C2 / 8 / 256;  // 16-byte pieces per thread
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
@@ -329,6 +362,40 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       if (rv) *reinterpret_cast<f32x4*>(dyrow + n0 + 16 * j + 4 * q) = acc;
     }
   }
+}
+
+// bias gradients = the per-workgroup column sums summed over workgroups, in two fixed-order
+// stages (deterministic): stage 1 -- block (column block of 32, slice z of RSL) sums its slice's
+// workgroups with 8 row groups into slices[z]; stage 2 sums the RSL slices in order.  One block
+// per column block walking all 2,000 workgroups took 96 us (latency-bound).
+constexpr int RSL = 32;
+__global__ __launch_bounds__(256) void heads_bias_reduce1(int nwg, int nbs, const float* __restrict__ ws,
+                                                          float* __restrict__ slices) {
+  __shared__ float part[8][32];
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5, z = blockIdx.y;
+  const int per = (nwg + RSL - 1) / RSL, w0 = z * per, w1 = min(nwg, w0 + per);
+  float v = 0.f;
+  if (c < nbs)
+    for (int w = w0 + g; w < w1; w += 8) v += ws[(size_t)w * nbs + c];
+  part[g][threadIdx.x & 31] = v;
+  __syncthreads();
+  if (g != 0 || c >= nbs) return;
+  const int e = threadIdx.x & 31;
+  slices[(size_t)z * nbs + c] = ((part[0][e] + part[1][e]) + (part[2][e] + part[3][e])) +
+                                ((part[4][e] + part[5][e]) + (part[6][e] + part[7][e]));
+}
+__global__ __launch_bounds__(256) void heads_bias_reduce2(int nbs, int F, int C, int n1,
+                                                          const float* __restrict__ slices, float* db3m,
+                                                          float* db3v, float* db2m, float* db2v, float* db1) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= nbs) return;
+  float t = 0.f;
+  for (int z = 0; z < RSL; ++z) t += slices[(size_t)z * nbs + c];
+  if (c < F) db3m[c] = t;
+  else if (c < 2 * F) { if (db3v) db3v[c - F] = t; }
+  else if (c < 2 * F + C) db2m[c - 2 * F] = t;
+  else if (c < 2 * F + 2 * C) { if (db2v) db2v[c - 2 * F - C] = t; }
+  else if (c - 2 * F - 2 * C < n1) db1[c - 2 * F - 2 * C] = t;
 }
 
 template <int C, int F>
@@ -351,6 +418,19 @@ int launch_heads(const HeadArgs& a, hipStream_t st) {
   return 0;
 }
 
+template <int C, int F>
+int launch_bias_reduce(const HeadArgs& a, int n1, float* db3m, float* db3v, float* db2m, float* db2v,
+                       float* db1, hipStream_t st) {
+  constexpr int NBS = nbs<C, F>();
+  const int nwg = (a.N + RT - 1) / RT;
+  float* slices = a.bias_ws + (size_t)nwg * NBS;
+  heads_bias_reduce1<<<dim3((NBS + 31) / 32, RSL), 256, 0, st>>>(nwg, NBS, a.bias_ws, slices);
+  MLVAE_CHECK_LAUNCH();
+  heads_bias_reduce2<<<(NBS + 255) / 256, 256, 0, st>>>(NBS, F, C, n1, slices, db3m, db3v, db2m, db2v, db1);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 extern "C" int mlvae_heads_partials_count(int B, int T) { return (B * T + RT - 1) / RT; }
@@ -358,6 +438,21 @@ extern "C" int mlvae_heads_partials_count(int B, int T) { return (B * T + RT - 1
 extern "C" int mlvae_heads_supported(int C, int F, int H2) {
   return C == 64 && (F == 64 || F == 80) && H2 > 0 && H2 % 128 == 0;
 }
+
+extern "C" size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C) {
+  return (size_t)((B * T + RT - 1) / RT + RSL) * (2 * F + 4 * C) * sizeof(float);
+}
+
+static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int train,
+                      const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
+                      const float* b1, const float* w2m, const float* b2m,
+                      const float* w3m, const float* b3m, const float* w2v,
+                      const float* b2v, const float* w3v, const float* b3v,
+                      const float* x, const float* lens, const int* count,
+                      float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
+                      float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
+                      float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
+                      float* db3m, float* db3v, float* db2m, float* db2v, float* db1, void* stream);
 
 extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int train,
                                  const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
@@ -368,6 +463,40 @@ extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_ty
                                  float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
                                  float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
                                  float* dp1, float* dy, float* partials, void* stream) {
+  return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
+                    b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
+                    dlvx, dp2m, dp2v, dp1, dy, partials, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+                    nullptr, stream);
+}
+
+extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
+                                    const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
+                                    const float* b1, const float* w2m, const float* b2m,
+                                    const float* w3m, const float* b3m, const float* w2v,
+                                    const float* b2v, const float* w3v, const float* b3v,
+                                    const float* x, const float* lens, const int* count,
+                                    float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
+                                    float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
+                                    float* dp1, float* dy, float* partials, float* bias_ws,
+                                    size_t bias_ws_bytes, float* db3m, float* db3v, float* db2m,
+                                    float* db2v, float* db1, void* stream) {
+  return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
+                    b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
+                    dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
+                    db1, stream);
+}
+
+static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int train,
+                                 const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
+                                 const float* b1, const float* w2m, const float* b2m,
+                                 const float* w3m, const float* b3m, const float* w2v,
+                                 const float* b2v, const float* w3v, const float* b3v,
+                                 const float* x, const float* lens, const int* count,
+                                 float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
+                                 float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
+                                 float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
+                                 float* db3m, float* db3v, float* db2m, float* db2v, float* db1,
+                                 void* stream) {
   if (B <= 0 || T <= 0) return 0;
   if (!mlvae_heads_supported(C, F, H2)) {
     mlvae_set_error("heads: unsupported shape C=%d F=%d 2H=%d (C 64, F 64|80, 2H %% 128)", C, F, H2);
@@ -393,6 +522,24 @@ extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_ty
   a.P1 = p1; a.P2[0] = p2m; a.P2[1] = p2v; a.OUT[0] = mux; a.OUT[1] = lvx;
   a.dOUT[0] = dmux; a.dOUT[1] = dlvx; a.dP2[0] = dp2m; a.dP2[1] = dp2v; a.dP1 = dp1; a.dY = dy;
   a.partials = partials;
+  a.bias_ws = nullptr;
+  if (bias_ws) {  // the five bias gradients from in-kernel column sums (train only)
+    const bool mse = loss_type == 1;
+    if (!train || bias_ws_bytes < mlvae_heads_bias_workspace_size(B, T, F, C) || !db3m || !db2m || !db1 ||
+        (!mse && (!db3v || !db2v))) {
+      mlvae_set_error("heads: bias sums need train, a workspace of %zu B and the bias gradients",
+                      mlvae_heads_bias_workspace_size(B, T, F, C));
+      return 1;
+    }
+    a.bias_ws = bias_ws;
+  }
   hipStream_t st = (hipStream_t)stream;
-  return F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
+  int rc = F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
+  if (rc || !bias_ws) return rc;
+  // mse: the log_var head gets no gradient (torch leaves its grads None): its bias gradients and
+  // the log_var half of the stacked first-layer bias are not written
+  const bool mse = loss_type == 1;
+  const int n1 = mse ? C : 2 * C;
+  return F == 80 ? launch_bias_reduce<64, 80>(a, n1, db3m, mse ? nullptr : db3v, db2m, mse ? nullptr : db2v, db1, st)
+                 : launch_bias_reduce<64, 64>(a, n1, db3m, mse ? nullptr : db3v, db2m, mse ? nullptr : db2v, db1, st);
 }

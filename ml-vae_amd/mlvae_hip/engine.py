@@ -241,6 +241,9 @@ class _Work:
         self.dP2m = empty(N, C, **f)
         self.dP2v = empty(N, C, **f)
         self.dP1 = empty(N, 2 * C, **f)
+        # fused heads: per-workgroup bias-gradient column sums (the five head biases)
+        self.heads_bws = empty(lib().mlvae_heads_bias_workspace_size(B, T, F, C) // 4 + 1, **f) \
+            if self.bf else None
         self.dY = [empty(N, 2 * H, **f) for _ in range(L)]
         self.dZs = empty(N, Z, **f)
         self.dML = empty(N, 2 * Z, **f)
@@ -729,9 +732,17 @@ class VAEEngine:
         if w.heads_fused:
             # both heads forward + recon loss (+ gradient) + heads backward + dY in one launch
             hp = lambda name: self._ptr(f"decoder.{name}")
+            hg = lambda name: self._ptr(f"decoder.{name}", self.grad)
             tr = 1 if train else 0
+            # train: the heads' five bias gradients come from in-kernel column sums (the backward
+            # skips their colsum passes)
+            w.heads_bias = bool(train) and w.heads_bws is not None
+            bias_args = (_p(w.heads_bws), w.heads_bws.numel() * 4, hg("mean_fc.blocks.4.bias"),
+                         hg("log_var_fc.blocks.4.bias"), hg("mean_fc.blocks.2.bias"),
+                         hg("log_var_fc.blocks.2.bias"), hg("mean_fc.blocks.0.bias")) \
+                if w.heads_bias else (None, 0, None, None, None, None, None)
             with self._timed("heads"):
-                check(l.mlvae_heads_fused(
+                check(l.mlvae_heads_fused_ex(
                   B, T, Fd, C, 2 * H, lt, tr, _pb(w.rnn_out_bf), wb("decoder.mean_fc.blocks.0.weight"),
                   _pb(self.w1_t) if train else None, hp("mean_fc.blocks.0.bias"),
                   hp("mean_fc.blocks.2.weight"), hp("mean_fc.blocks.2.bias"),
@@ -742,7 +753,7 @@ class VAEEngine:
                   _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
                   _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
                   _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
-                  _p(w.ph), s), "heads_fused")
+                  _p(w.ph), *bias_args, s), "heads_fused")
             check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w
@@ -839,18 +850,22 @@ class VAEEngine:
         for hd, P2, dOut, dP2, off in heads:
             W3, W2 = self._ptr(f"decoder.{hd}.blocks.4.weight"), self._ptr(f"decoder.{hd}.blocks.2.weight")
 
-            def wg3(hd=hd, dOut=dOut, P2=P2):
+            hb = getattr(w, "heads_bias", False)  # bias gradients already summed by the heads kernel
+
+            def wg3(hd=hd, dOut=dOut, P2=P2, hb=hb):
                 self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
-                self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
+                if not hb:
+                    self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
             side(wg3)
             if not fused:
                 self._mm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C,
                          B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
 
-            def wg2(hd=hd, dP2=dP2, off=off):
+            def wg2(hd=hd, dP2=dP2, off=off, hb=hb):
                 self._mm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
                          gp(f"decoder.{hd}.blocks.2.weight"), C)
-                self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
+                if not hb:
+                    self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
             side(wg2)
             if not fused:
                 self._mm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C,
@@ -863,7 +878,8 @@ class VAEEngine:
         def wg1():
             self._mm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
                      gp("decoder.mean_fc.blocks.0.weight"), 2 * H, B_bf=R_bf)
-            self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
+            if not getattr(w, "heads_bias", False):
+                self._colsum(w, N, K1, _p(w.dP1), 2 * C, gp("decoder.mean_fc.blocks.0.bias"))
         side(wg1)
         if not fused:
             self._mm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),

@@ -92,3 +92,63 @@ def test_heads_fused(loss_type, B, T, F, H2, train):
     assert norm_rel(o["dy"], Yd.grad) < 3e-2
     if loss_type == 1:  # mse: the log_var head gets no gradient
         assert o["dp1"][:, C:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("loss_type", [0, 1])
+@pytest.mark.parametrize("B,T,F,H2", [(3, 50, 80, 256), (5, 77, 64, 128)])
+def test_heads_fused_bias_sums(loss_type, B, T, F, H2):
+    """mlvae_heads_fused_ex: the five head bias gradients from in-kernel column sums equal the
+    column sums of the kernel's own dOUT / dP2 / dP1 outputs (fp32, fixed-order reduce); mse
+    leaves the log_var head's biases untouched."""
+    need_gpu()
+    torch.manual_seed(B + T + F + loss_type)
+    C, N = 64, B * T
+    l = lib()
+    f = dict(device="cuda", dtype=torch.float32)
+    Y = torch.randn(N, H2).to(torch.bfloat16).cuda()
+    W1 = (torch.randn(2 * C, H2) / math.sqrt(H2)).to(torch.bfloat16)
+    dW1, dW1t = W1.cuda(), W1.t().contiguous().cuda()
+    b1 = (torch.randn(2 * C) * 0.1).cuda()
+    W2 = [(torch.randn(C, C) / 8).cuda() for _ in range(2)]
+    b2 = [(torch.randn(C) * 0.1).cuda() for _ in range(2)]
+    W3 = [(torch.randn(F, C) / 8).cuda() for _ in range(2)]
+    b3 = [(torch.randn(F) * 0.1).cuda() for _ in range(2)]
+    x = torch.randn(N, F).cuda()
+    lens = torch.tensor([1.0, 0.7, 0.31, 0.9, 0.5][:B]).cuda()
+    o = {k: torch.zeros(N, n, **f) for k, n in (("p1", 2 * C), ("p2m", C), ("p2v", C), ("mux", F),
+                                                  ("lvx", F), ("dmux", F), ("dlvx", F), ("dp2m", C),
+                                                  ("dp2v", C), ("dp1", 2 * C), ("dy", H2))}
+    parts = torch.zeros(l.mlvae_heads_partials_count(B, T), **f)
+    ws = torch.zeros(l.mlvae_heads_bias_workspace_size(B, T, F, C) // 4 + 1, **f)
+    nan = lambda n: torch.full((n,), float("nan"), **f)
+    db3m, db3v, db2m, db2v, db1 = nan(F), nan(F), nan(C), nan(C), nan(2 * C)
+    lik = loss_type == 0
+    check(l.mlvae_heads_fused_ex(B, T, F, C, H2, loss_type, 1, Y.data_ptr(), dW1.data_ptr(), dW1t.data_ptr(),
+                                 P(b1), P(W2[0]), P(b2[0]), P(W3[0]), P(b3[0]), P(W2[1]), P(b2[1]),
+                                 P(W3[1]), P(b3[1]), P(x), P(lens), None, 0.7, P(o["p1"]), P(o["p2m"]),
+                                 P(o["p2v"]), P(o["mux"]), P(o["lvx"]), P(o["dmux"]),
+                                 P(o["dlvx"]) if lik else None, P(o["dp2m"]), P(o["dp2v"]), P(o["dp1"]),
+                                 P(o["dy"]), P(parts), P(ws), ws.numel() * 4, P(db3m), P(db3v), P(db2m),
+                                 P(db2v), P(db1), stream()))
+    torch.cuda.synchronize()
+    cs = lambda t: t.double().sum(0)
+    assert rel_err(db3m, cs(o["dmux"])) < 1e-5
+    assert rel_err(db2m, cs(o["dp2m"])) < 1e-5
+    if lik:
+        assert rel_err(db3v, cs(o["dlvx"])) < 1e-5
+        assert rel_err(db2v, cs(o["dp2v"])) < 1e-5
+        assert rel_err(db1, cs(o["dp1"])) < 1e-5
+    else:
+        assert torch.isnan(db3v).all() and torch.isnan(db2v).all() and torch.isnan(db1[C:]).all()
+        assert rel_err(db1[:C], cs(o["dp1"][:, :C])) < 1e-5
+    # the same launch twice: bit-identical (fixed-order sums)
+    first = db1.clone()
+    check(l.mlvae_heads_fused_ex(B, T, F, C, H2, loss_type, 1, Y.data_ptr(), dW1.data_ptr(), dW1t.data_ptr(),
+                                 P(b1), P(W2[0]), P(b2[0]), P(W3[0]), P(b3[0]), P(W2[1]), P(b2[1]),
+                                 P(W3[1]), P(b3[1]), P(x), P(lens), None, 0.7, P(o["p1"]), P(o["p2m"]),
+                                 P(o["p2v"]), P(o["mux"]), P(o["lvx"]), P(o["dmux"]),
+                                 P(o["dlvx"]) if lik else None, P(o["dp2m"]), P(o["dp2v"]), P(o["dp1"]),
+                                 P(o["dy"]), P(parts), P(ws), ws.numel() * 4, P(db3m), P(db3v), P(db2m),
+                                 P(db2v), P(db1), stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(first[:C], db1[:C])
