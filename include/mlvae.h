@@ -271,7 +271,9 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
  * bytes), then a fixed-order reduce into db3m / db3v (mean_fc / log_var_fc blocks.4.bias [F]),
  * db2m / db2v (blocks.2.bias [C]) and db1 (the stacked blocks.0 biases [2C]; mse: the log_var
  * head gets no gradient, so db3v, db2v and db1[C:] are not written).  Replaces the autograd
- * bias sums of ref:src/modules/fc_block.py:9-16 without re-reading dOUT / dP2 / dP1. */
+ * bias sums of ref:src/modules/fc_block.py:9-16 without re-reading dOUT / dP2 / dP1.
+ * saved_bf16: p1, p2m/p2v, dmux/dlvx, dp2m/dp2v and dp1 are written as bf16 (packed rows, the
+ * weight-gradient GEMMs' operand precision) instead of fp32; mux / lvx / dy stay fp32. */
 size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C);
 int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
                          const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
@@ -281,7 +283,8 @@ int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int 
                          float* p1, float* p2m, float* p2v, float* mux, float* lvx, float* dmux,
                          float* dlvx, float* dp2m, float* dp2v, float* dp1, float* dy,
                          float* partials, float* bias_ws, size_t bias_ws_bytes, float* db3m,
-                         float* db3v, float* db2m, float* db2v, float* db1, void* stream);
+                         float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
+                         void* stream);
 /* Skinny products of the bottom LSTM layer (bf16; one side is the latent width):
  * mlvae_skinny_nt: C [M, N] (fp32, ldc) = A [M, K] . Bt [N, K]^T, bf16 k-contiguous operands,
  *   N in {16, 32, 48, 64}, K % 32 == 0: dZ = dG W_ih over the k-contiguous W_ih^T copy.

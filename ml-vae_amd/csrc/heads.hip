@@ -40,6 +40,7 @@ struct HeadArgs {
   const float* x; const float* lens; const int* count; float rec_scale;
   float* P1; float* P2[2]; float* OUT[2]; float* dOUT[2]; float* dP2[2]; float* dP1; float* dY;
   float* partials;
+  int sbf;         // the saved intermediates (P1, P2, dOUT, dP2, dP1) are bf16 (packed rows)
   float* bias_ws;  // train, optional: per-workgroup column sums [gridDim.x][NBS] of dOUT_m | dOUT_v |
                    // dP2_m | dP2_v | dP1 (the five bias gradients before the workgroup sum)
 };
@@ -65,6 +66,12 @@ __device__ __forceinline__ void rows16_to_lds(f32x4 v, float* dst, int lane) {
 __device__ __forceinline__ bf16x8 lds8(const short* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ void st4bf(short* p, f32x4 v) {
   *reinterpret_cast<bf16x4*>(p) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+}
+// a lane's 4 consecutive values of a saved intermediate: fp32, or bf16 (the weight-gradient
+// GEMMs read bf16 operands either way: same rounding, half the bytes)
+__device__ __forceinline__ void st_saved(float* base, size_t idx, f32x4 v, int sbf) {
+  if (sbf) st4bf(reinterpret_cast<short*>(base) + idx, v);
+  else *reinterpret_cast<f32x4*>(base + idx) = v;
 }
 __device__ __forceinline__ bf16x8 gld8(const unsigned short* p) {
   return *reinterpret_cast<const bf16x8*>(p);
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc1[j][r] = lrelu(acc1[j][r] + a.b1[col + r]);
     st4bf(sm + O_P1 + lrow * L2C + col, acc1[j]);
-    if (rv && a.train) *reinterpret_cast<f32x4*>(a.P1 + (size_t)grow * C2 + col) = acc1[j];
+    if (rv && a.train) st_saved(a.P1, (size_t)grow * C2 + col, acc1[j], a.sbf);
   }
 
   // ---- stages 2-3 per head: P2 = lrelu(P1_h W2^T + b2), OUT = P2 W3^T + b3
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc2[h][j][r] = lrelu(acc2[h][j][r] + a.b2[h][col + r]);
       st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc2[h][j]);
-      if (rv && a.train) *reinterpret_cast<f32x4*>(a.P2[h] + (size_t)grow * C + col) = acc2[h][j];
+      if (rv && a.train) st_saved(a.P2[h], (size_t)grow * C + col, acc2[h][j], a.sbf);
     }
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc3[h][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -267,8 +274,8 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       st4bf(sm + O_DO + lrow * LF + col, gm);
       st4bf(sm + O_DO + RT * LF + lrow * LF + col, gv);
       if (rv) {
-        *reinterpret_cast<f32x4*>(a.dOUT[0] + (size_t)grow * F + col) = gm;
-        if (lik) *reinterpret_cast<f32x4*>(a.dOUT[1] + (size_t)grow * F + col) = gv;
+        st_saved(a.dOUT[0], (size_t)grow * F + col, gm, a.sbf);
+        if (lik) st_saved(a.dOUT[1], (size_t)grow * F + col, gv, a.sbf);
       }
     }
   }
@@ -309,7 +316,7 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       if (bsum) rows16_to_lds(acc5[j], &bred[wave][2 * F + h * C + 16 * j], lane);
       // dP2 image reuses this head's P2 image (P2 itself is dead after stage 3)
       st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc5[j]);
-      if (rv && h < nh) *reinterpret_cast<f32x4*>(a.dP2[h] + (size_t)grow * C + col) = acc5[j];
+      if (rv && h < nh) st_saved(a.dP2[h], (size_t)grow * C + col, acc5[j], a.sbf);
     }
     f32x4 acc6[NC];
 #pragma unroll
@@ -330,7 +337,7 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
       for (int r = 0; r < 4; ++r) acc6[j][r] *= lrelu_d(acc1[h * NC + j][r]);
       if (bsum) rows16_to_lds(acc6[j], &bred[wave][2 * F + 2 * C + h * C + 16 * j], lane);
       st4bf(sm + O_P1 + lrow * L2C + col, acc6[j]);  // dP1 image reuses the P1 image
-      if (rv) *reinterpret_cast<f32x4*>(a.dP1 + (size_t)grow * C2 + col) = acc6[j];
+      if (rv) st_saved(a.dP1, (size_t)grow * C2 + col, acc6[j], a.sbf);
     }
   }
 
@@ -452,7 +459,8 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                       float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
                       float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
                       float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
-                      float* db3m, float* db3v, float* db2m, float* db2v, float* db1, void* stream);
+                      float* db3m, float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
+                      void* stream);
 
 extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int train,
                                  const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
@@ -466,7 +474,7 @@ extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_ty
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
-                    nullptr, stream);
+                    nullptr, 0, stream);
 }
 
 extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
@@ -479,11 +487,11 @@ extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss
                                     float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
                                     float* dp1, float* dy, float* partials, float* bias_ws,
                                     size_t bias_ws_bytes, float* db3m, float* db3v, float* db2m,
-                                    float* db2v, float* db1, void* stream) {
+                                    float* db2v, float* db1, int saved_bf16, void* stream) {
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
-                    db1, stream);
+                    db1, saved_bf16, stream);
 }
 
 static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int train,
@@ -496,7 +504,7 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                                  float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
                                  float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
                                  float* db3m, float* db3v, float* db2m, float* db2v, float* db1,
-                                 void* stream) {
+                                 int saved_bf16, void* stream) {
   if (B <= 0 || T <= 0) return 0;
   if (!mlvae_heads_supported(C, F, H2)) {
     mlvae_set_error("heads: unsupported shape C=%d F=%d 2H=%d (C 64, F 64|80, 2H %% 128)", C, F, H2);
@@ -522,6 +530,7 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
   a.P1 = p1; a.P2[0] = p2m; a.P2[1] = p2v; a.OUT[0] = mux; a.OUT[1] = lvx;
   a.dOUT[0] = dmux; a.dOUT[1] = dlvx; a.dP2[0] = dp2m; a.dP2[1] = dp2v; a.dP1 = dp1; a.dY = dy;
   a.partials = partials;
+  a.sbf = saved_bf16 ? 1 : 0;
   a.bias_ws = nullptr;
   if (bias_ws) {  // the five bias gradients from in-kernel column sums (train only)
     const bool mse = loss_type == 1;

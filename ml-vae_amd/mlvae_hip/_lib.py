@@ -65,7 +65,7 @@ _SIGS = {
                           P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mlvae_heads_bias_workspace_size": [I, I, I, I],
     "mlvae_heads_fused_ex": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
-                             P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, P],
+                             P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, I, P],
     "mlvae_skinny_proj": [I, I, I, P, I, P, I, P, P, P, I, P],
     "mlvae_skinny_proj_ex": [I, I, I, P, I, P, I, P, P, P, I, I, P],
     "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],

@@ -330,6 +330,9 @@ class VAEEngine:
         self.wih_t = {}
         # bf16 mode: the heads run as one fused kernel (heads.hip) when the shape is supported
         self.fused_heads = (cfg.prec == "bf16" and bool(lib().mlvae_heads_supported(cfg.C, cfg.F, 2 * cfg.H)))
+        # fused heads: in-kernel bias sums + bf16 saved intermediates (MLVAE_HEADS_BSUM=0: the
+        # colsum passes over fp32 intermediates, for same-box A/B)
+        self.heads_bias_sums = os.environ.get("MLVAE_HEADS_BSUM", "1") != "0"
         self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
                      if self.fused_heads else None)
         # bf16 mode: the encoder (+ reparameterisation + KL) runs as two fused kernels
@@ -735,8 +738,10 @@ class VAEEngine:
             hg = lambda name: self._ptr(f"decoder.{name}", self.grad)
             tr = 1 if train else 0
             # train: the heads' five bias gradients come from in-kernel column sums (the backward
-            # skips their colsum passes)
-            w.heads_bias = bool(train) and w.heads_bws is not None
+            # skips their colsum passes), and the intermediates the weight-gradient GEMMs read
+            # (P1, P2, dOUT, dP2, dP1) are saved as bf16 -- their operand precision -- in the
+            # fp32 buffers' memory (packed rows)
+            w.heads_bias = bool(train) and w.heads_bws is not None and self.heads_bias_sums
             bias_args = (_p(w.heads_bws), w.heads_bws.numel() * 4, hg("mean_fc.blocks.4.bias"),
                          hg("log_var_fc.blocks.4.bias"), hg("mean_fc.blocks.2.bias"),
                          hg("log_var_fc.blocks.2.bias"), hg("mean_fc.blocks.0.bias")) \
@@ -753,7 +758,7 @@ class VAEEngine:
                   _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
                   _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
                   _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
-                  _p(w.ph), *bias_args, s), "heads_fused")
+                  _p(w.ph), *bias_args, 1 if w.heads_bias else 0, s), "heads_fused")
             check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w
@@ -853,7 +858,11 @@ class VAEEngine:
             hb = getattr(w, "heads_bias", False)  # bias gradients already summed by the heads kernel
 
             def wg3(hd=hd, dOut=dOut, P2=P2, hb=hb):
-                self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
+                if hb:  # bf16 saved intermediates (the heads kernel's saved_bf16)
+                    self._mm(w, 1, 0, Fd, C, N, None, Fd, None, C, gp(f"decoder.{hd}.blocks.4.weight"), C,
+                             A_bf=_p(dOut), B_bf=_p(P2))
+                else:
+                    self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
                 if not hb:
                     self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
             side(wg3)
@@ -862,8 +871,12 @@ class VAEEngine:
                          B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
 
             def wg2(hd=hd, dP2=dP2, off=off, hb=hb):
-                self._mm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
-                         gp(f"decoder.{hd}.blocks.2.weight"), C)
+                if hb:  # bf16 rows: the head's P1 half starts off elements in
+                    self._mm(w, 1, 0, C, C, N, None, C, None, 2 * C, gp(f"decoder.{hd}.blocks.2.weight"), C,
+                             A_bf=_p(dP2), B_bf=_pb(w.P1, off))
+                else:
+                    self._mm(w, 1, 0, C, C, N, _p(dP2), C, _p(w.P1, off), 2 * C,
+                             gp(f"decoder.{hd}.blocks.2.weight"), C)
                 if not hb:
                     self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
             side(wg2)
@@ -876,6 +889,11 @@ class VAEEngine:
         R_bf = _pb(w.rnn_out_bf) if w.bf else None
 
         def wg1():
+            if getattr(w, "heads_bias", False) and R_bf is not None:
+                # bf16 dP1 [N, 2C] and rnn_out: the 256² kernel (m/n-contiguous, split-K)
+                self._fast(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R_bf, 2 * H,
+                           gp("decoder.mean_fc.blocks.0.weight"), 2 * H)
+                return
             self._mm(w, 1, 0, K1, 2 * H, N, _p(w.dP1), 2 * C, R, 2 * H,
                      gp("decoder.mean_fc.blocks.0.weight"), 2 * H, B_bf=R_bf)
             if not getattr(w, "heads_bias", False):

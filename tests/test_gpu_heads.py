@@ -129,7 +129,7 @@ def test_heads_fused_bias_sums(loss_type, B, T, F, H2):
                                  P(o["p2v"]), P(o["mux"]), P(o["lvx"]), P(o["dmux"]),
                                  P(o["dlvx"]) if lik else None, P(o["dp2m"]), P(o["dp2v"]), P(o["dp1"]),
                                  P(o["dy"]), P(parts), P(ws), ws.numel() * 4, P(db3m), P(db3v), P(db2m),
-                                 P(db2v), P(db1), stream()))
+                                 P(db2v), P(db1), 0, stream()))
     torch.cuda.synchronize()
     cs = lambda t: t.double().sum(0)
     assert rel_err(db3m, cs(o["dmux"])) < 1e-5
@@ -149,6 +149,24 @@ def test_heads_fused_bias_sums(loss_type, B, T, F, H2):
                                  P(o["p2v"]), P(o["mux"]), P(o["lvx"]), P(o["dmux"]),
                                  P(o["dlvx"]) if lik else None, P(o["dp2m"]), P(o["dp2v"]), P(o["dp1"]),
                                  P(o["dy"]), P(parts), P(ws), ws.numel() * 4, P(db3m), P(db3v), P(db2m),
-                                 P(db2v), P(db1), stream()))
+                                 P(db2v), P(db1), 0, stream()))
     torch.cuda.synchronize()
     assert torch.equal(first[:C], db1[:C])
+    # saved_bf16: the five saved intermediates as bf16 = the fp32 ones rounded once; the bias
+    # sums (taken from the fp32 registers) and everything else unchanged
+    ob = {k: torch.zeros(N, o[k].shape[1], device="cuda", dtype=torch.bfloat16)
+          for k in ("p1", "p2m", "p2v", "dmux", "dlvx", "dp2m", "dp2v", "dp1")}
+    dy2, mux2 = torch.zeros_like(o["dy"]), torch.zeros_like(o["mux"])
+    b1b = db1.clone().fill_(float("nan"))
+    check(l.mlvae_heads_fused_ex(B, T, F, C, H2, loss_type, 1, Y.data_ptr(), dW1.data_ptr(), dW1t.data_ptr(),
+                                 P(b1), P(W2[0]), P(b2[0]), P(W3[0]), P(b3[0]), P(W2[1]), P(b2[1]),
+                                 P(W3[1]), P(b3[1]), P(x), P(lens), None, 0.7, P(ob["p1"]), P(ob["p2m"]),
+                                 P(ob["p2v"]), P(mux2), P(o["lvx"]), P(ob["dmux"]),
+                                 P(ob["dlvx"]) if lik else None, P(ob["dp2m"]), P(ob["dp2v"]), P(ob["dp1"]),
+                                 P(dy2), P(parts), P(ws), ws.numel() * 4, P(db3m), P(db3v), P(db2m),
+                                 P(db2v), P(b1b), 1, stream()))
+    torch.cuda.synchronize()
+    for k in ("p1", "p2m", "dmux", "dp2m", "dp1") + (("p2v", "dlvx", "dp2v") if lik else ()):
+        assert torch.equal(ob[k], o[k].to(torch.bfloat16)), k
+    assert torch.equal(dy2, o["dy"]) and torch.equal(mux2, o["mux"])
+    assert torch.equal(b1b[:C], first[:C])
