@@ -452,6 +452,7 @@ __global__ __launch_bounds__(256) void encoder_reduce(int G, const float* __rest
   const int g0 = qtr * G / 4, g1 = (qtr + 1) * G / 4;
   float v = 0.f;
   if (i < SLAB)
+#pragma unroll 8  // eight slab loads in flight per thread; the adds keep their order
     for (int g = g0; g < g1; ++g) v += ws[(size_t)g * SLAB + i];
   part[qtr][e] = v;
   __syncthreads();

@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256) void splitk_reduce2(G2Args g) {
     const size_t idx = base + e;
     float s = 0.f;
     if (idx < MN)
+#pragma unroll 8  // loads in flight; the adds keep their order
       for (int z = grp; z < g.splits; z += 4) s += g.ws[z * MN + idx];
     part[grp][e] = s;
     __syncthreads();

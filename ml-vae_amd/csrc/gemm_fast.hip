@@ -529,6 +529,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
                     : g.C + bz * g.c_bs;
   for (size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x; idx < MN; idx += (size_t)gridDim.x * 256) {
     float s = 0.f;
+#pragma unroll 8  // loads in flight; the adds keep their order
     for (int z = 0; z < g.splits; ++z) s += ws[z * MN + idx];
     const int row = (int)(idx / g.N), col = (int)(idx % g.N);
     if (g.bias1) s += g.bias1[col];

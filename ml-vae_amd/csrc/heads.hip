@@ -383,6 +383,7 @@ __global__ __launch_bounds__(256) void heads_bias_reduce1(int nwg, int nbs, cons
   const int per = (nwg + RSL - 1) / RSL, w0 = z * per, w1 = min(nwg, w0 + per);
   float v = 0.f;
   if (c < nbs)
+#pragma unroll 8
     for (int w = w0 + g; w < w1; w += 8) v += ws[(size_t)w * nbs + c];
   part[g][threadIdx.x & 31] = v;
   __syncthreads();
@@ -397,6 +398,7 @@ __global__ __launch_bounds__(256) void heads_bias_reduce2(int nbs, int F, int C,
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= nbs) return;
   float t = 0.f;
+#pragma unroll 8
   for (int z = 0; z < RSL; ++z) t += slices[(size_t)z * nbs + c];
   if (c < F) db3m[c] = t;
   else if (c < 2 * F) { if (db3v) db3v[c - F] = t; }

@@ -266,6 +266,7 @@ __global__ __launch_bounds__(256) void skinny_reduce(int M, int NB, int S, int n
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     const int m = (int)(i / ncol), n = (int)(i % ncol);
     float v = 0.f;
+#pragma unroll 8  // loads in flight; the adds keep their order
     for (int s = 0; s < S; ++s) v += ws[((size_t)s * M + m) * NB + n];
     if (n < nw) W[(size_t)m * nw + n] = v;
     else {
