@@ -405,7 +405,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
         continue;
       }
       // operands swapped (D = B^T A^T): a lane's 4 results are 4 consecutive columns of one
-      // row, so the epilogue stores 16 B per lane
+      // row, so the epilogue stores 16 B per lane (s_setprio(1) around these MFMAs measured
+      // 7-8 % slower on the weight gradients: profiles/r02_gemm_wgrad_var_ab.txt)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
