@@ -52,6 +52,7 @@ CONFIGS = {
     "c5": (80, 64, 32, 512, 2, 64, 64, 500, False),   # configs[4]: B=512 over 8 GPUs = 64 per GPU
 }
 CONFIGS["c5bf16"] = CONFIGS["c5"]   # the same per-GPU shard in bf16 (the fp8 comparison)
+CONFIGS["c3h"] = (80, 64, 32, 512, 2, 64, 128, 500, False)  # the metric's B=256 over 2 GPUs: one shard
 FP8 = {"c5"}             # configs[4]: fp8 e4m3 layer-1 input projection (VAEConfig.fp8)
 ENC_CONV = {"c4": 5}     # configs[3]: Conv1d encoder variant (kernel size 5), modules/conv_vae.py
 TIMER_EVERY = 4          # time kernels with HIP events on every 4th timed step
@@ -92,10 +93,11 @@ def encoder_bwd_bytes(N, F, E, Z):
 
 
 def heads_bytes(N, F, C, H):
-    """heads_kernel (train): reads h (2H bf16) and x (F fp32); writes P1 (2C), P2m, P2v (C each),
-    mu_x, log_var_x (F each), d mu_x, d log_var_x (F each), dP2m, dP2v (C each), dP1 (2C) fp32
-    and dY (2H fp32)."""
-    return N * (2 * 2 * H + 4 * F + 4 * (2 * C + 2 * C + 2 * F + 2 * F + 2 * C + 2 * C) + 4 * 2 * H)
+    """heads_kernel (train, the engine's fused mode): reads h (2H bf16) and x (F fp32); writes
+    mu_x, log_var_x (F each, fp32), dY (2H fp32) and, as bf16 (the weight-gradient GEMMs' operand
+    precision), P1 (2C), P2m, P2v (C each), d mu_x, d log_var_x (F each), dP2m, dP2v (C each),
+    dP1 (2C)."""
+    return N * (2 * 2 * H + 4 * F + 4 * 2 * F + 4 * 2 * H + 2 * (2 * C + 2 * C + 2 * F + 2 * C + 2 * C))
 
 
 def conv_fwd_bytes(N, F, E):

@@ -26,6 +26,7 @@
 //             each workgroup sums its NJ producers' partials with a DPP reduce-scatter.
 // Hand-off protocol, slots and tags: lstm_common.h / lstm.hip header.
 #include "lstm_common.h"
+#include <stdlib.h>
 #include <type_traits>
 
 namespace {
@@ -707,7 +708,11 @@ WidePlan wide_plan(int B, int H, bool fwd) {
   p.nkc = H / 32;
   p.NB = (B + BG - 1) / BG;
   const int cus = wide_cus();
-  for (int tpw = 1; tpw <= 2; ++tpw) {
+  static const int tpw0 = [] {  // MLVAE_WIDE_TPW=2: start at HJ = 64 units per workgroup (A/B)
+    const char* e = getenv("MLVAE_WIDE_TPW");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  for (int tpw = tpw0; tpw <= 2; ++tpw) {
     if (fwd && tpw * p.nkc * 4 > 128) break;   // resident A-fragments <= 128 VGPRs
     const int hj = 32 * tpw, nj = H / hj;
     if (!fwd && (nj < 8 || nj % 8)) continue;   // reduce-scatter: NJ multiple of 8
