@@ -361,7 +361,8 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
   const unsigned short* a = static_cast<const unsigned short*>(A);
   const unsigned short* b = static_cast<const unsigned short*>(Bt);
   hipStream_t st = (hipStream_t)stream;
-  if (K % NTL_KC == 0 && M >= 64 * 1024) {  // long row streams: Bt shared through LDS
+  if (K % NTL_KC == 0 && M >= 4096) {  // row streams of >= 32 workgroups: Bt shared through LDS
+                                         // (c3 409 -> 210 us, c2 52 -> 49 us)
     dim3 g128((M + 127) / 128);
     switch (N / 16) {
       case 1: skinny_nt_lds_kernel<1><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
