@@ -344,6 +344,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the N=1 c2 / fp32 extra runs")
     ap.add_argument("--dry-run", action="store_true", help="process model only (gloo, no GPU)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend of the ranks (nccl = RCCL over xGMI; gloo: the "
+                         "one-GPU rehearsal of the worker path in tests/test_gpu_bench_dp.py)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -354,11 +357,18 @@ def main():
     if args.dry_run:
         return dry_run(rank, world)
 
+    # one GPU per rank; ranks beyond the visible devices share them (the gloo rehearsal on a
+    # one-GPU box: device_count() does not initialise the GPU)
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev
     torch.cuda.set_device(local)
     device = f"cuda:{local}"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     F, E, Z, H, L, C, batch, T, is_global = CONFIGS[args.config]
     if is_global:

@@ -359,6 +359,14 @@ int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const floa
                     int* nonfinite, float lr, float beta1, float beta2, float eps,
                     float max_norm, float* norm_out, float* hyp_scratch, int advance,
                     void* stream);
+/* As mlvae_adam_step, plus the persistent recurrences' hand-off timeout word `err` (optional):
+ * while *err != 0 the update is skipped (parameters and Adam state untouched, step counter not
+ * advanced) and *err_skips (optional) counts the skipped steps, apart from non-finite losses. */
+int mlvae_adam_step_ex(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
+                       size_t n, const double* partials, int nparts, const float* loss, int* step,
+                       int* nonfinite, const int* err, int* err_skips, float lr, float beta1,
+                       float beta2, float eps, float max_norm, float* norm_out, float* hyp_scratch,
+                       int advance, void* stream);
 
 /* clip_grad_norm_ over several separately stored grads: every grad's sum-of-squares
  * partials go to one buffer (offsets), then each grad is scaled by min(max/(total+1e-6),1). */

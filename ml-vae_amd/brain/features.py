@@ -33,15 +33,21 @@ class InputNormalization(torch.nn.Module):
         mask = (torch.arange(T, device=x.device, dtype=torch.float32).unsqueeze(0) < n.unsqueeze(1))
         mask = mask.to(x.dtype).reshape(B, T, *([1] * (x.dim() - 2)))
         nb = n.to(x.dtype).reshape(B, *([1] * (x.dim() - 2)))
+        # zero-length utterances (the fillers of a short data-parallel evaluation slice) carry no
+        # statistics: they are left out of the batch averages
+        valid = (n > 0).to(x.dtype).reshape(B, *([1] * (x.dim() - 2)))
+        nb = nb.clamp(min=1)
         means = (x * mask).sum(1) / nb
         var = (((x - means.unsqueeze(1)) * mask) ** 2).sum(1) / (nb - 1)
         stds = torch.clamp(var.sqrt(), min=self.eps)
-        cur_mean = means.mean(0)
-        cur_std = stds.mean(0)
+        stds = torch.where(valid > 0, stds, torch.zeros_like(stds))  # 0/0 of an empty utterance
+        nvalid = valid.sum(0).clamp(min=1)
+        cur_mean = (means * valid).sum(0) / nvalid
+        cur_std = (stds * valid).sum(0) / nvalid
         from brain.distributed import all_reduce_sum_, world_size
         if self.training and world_size() > 1:  # data parallel: the statistics of the global batch
-            acc = torch.cat([means.sum(0).reshape(-1), stds.sum(0).reshape(-1),
-                             torch.tensor([float(B)], device=x.device, dtype=means.dtype)])
+            acc = torch.cat([(means * valid).sum(0).reshape(-1), (stds * valid).sum(0).reshape(-1),
+                             valid.sum().reshape(1)])
             all_reduce_sum_(acc)
             k = cur_mean.numel()
             cur_mean = (acc[:k] / acc[-1]).reshape(cur_mean.shape)

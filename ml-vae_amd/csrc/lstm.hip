@@ -1146,8 +1146,10 @@ extern "C" int mlvae_lstm_set_debug(void* buf) {
 // groups take whole XCDs from the side-stream GEMMs), bit2 disables it for the forward,
 // bit3 reserves 100 KB LDS per recurrence workgroup, bit4 polls with s_sleep 1 instead of 4,
 // bits 5-10 delay the first poll sweep of every step by that many s_sleep 1, bit 11 times the
-// batch-group kernels without their prefetch, bit 12 runs the wide-batch kernels at any batch.
+// batch-group kernels without their prefetch, bit 12 runs the wide-batch kernels at any batch,
+// bit 21 keeps the wide kernels at one workgroup per CU (no two-per-CU plan; A/B and tests).
 extern "C" int mlvae_lstm_set_debug_mode(int mode) {
   g_dbg_mode = mode;
+  lstm_wide_set_mode(mode);
   return 0;
 }

@@ -117,6 +117,8 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
                   unsigned long long* dbg, int dbg_mode);
+// debug-mode bits the wide plans read (bit 21: one workgroup per CU, no two-per-CU plan)
+void lstm_wide_set_mode(int mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply
 size_t lstm_wide_xbytes(int B, int H, bool fwd);
 // workgroups of the wide launch at (B, H), or 0 when it does not apply

@@ -55,8 +55,10 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
-template <int TPW, int NKC>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
-__global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
+// OCC = minimum waves per SIMD: 2 = one workgroup per CU, 4 = two co-resident workgroups per CU
+// (<= 128 VGPRs), whose step chains then overlap each other's hand-off waits
+template <int TPW, int NKC, int OCC>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
+__global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
   constexpr int PL = NKC / 4;                 // poll loads (k-chunks) per lane, waves 0-3
@@ -354,8 +356,8 @@ __global__ __launch_bounds__(512) void lstm_fwd_wide_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------------------
 // backward (BPTT), reduce-scatter form
 // ---------------------------------------------------------------------------------------
-template <int TPW, int NKC>  // HJ = 32 * TPW units per workgroup, H = 32 * NKC
-__global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
+template <int TPW, int NKC, int OCC>  // HJ = 32 * TPW units per workgroup, H = 32 * NKC; OCC as fwd
+__global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = 32 * TPW;
   constexpr int H = NKC * 32;
   constexpr int NJ = H / HJ;                  // workgroups per (dir, group) = producers = consumers
@@ -689,6 +691,7 @@ __global__ __launch_bounds__(512) void lstm_bwd_wide_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------------------
 struct WidePlan {
   int tpw, nkc, NB, NJ, HJ;
+  int per_cu;  // co-resident recurrence workgroups per CU (1, or 2 at OCC = 4)
   size_t lds, xbytes, xtab_off;
   bool ok;
 };
@@ -701,12 +704,46 @@ int wide_cus() {
   return cus;
 }
 
+size_t wide_lds(int H, int hj, bool fwd) {
+  if (fwd)
+    return (size_t)2 * 16 * H * 2 + (size_t)2 * 16 * (4 * hj + 8) * 2 +  // h image, gx ring
+           (size_t)2 * 16 * (4 * hj * 2 + 2 * hj * 4 + 16) +              // out ring
+           (size_t)8 * (hj / 32) * 2 * 64 * 16 +  // + the LDS-resident A-fragments (KLF = 2)
+           (size_t)2 * (16 * hj / 8) * 4;         // + dropout keep bits
+  return (size_t)2 * 16 * 4 * hj * 2 +
+         (size_t)8 * (H / 128) * (hj / 32) * 64 * 16 +  // + LDS-resident B-fragments (KLB = KC/4)
+         (size_t)2 * 16 * ((4 * hj * 2 + 16) + 2 * (hj * 4 + 32));  // + staged cell inputs
+}
+
+int g_wide_mode = 0;  // lstm_wide_set_mode
+
+// Two co-resident workgroups per CU (HJ = 32 at the OCC = 4 instantiation): checked against the
+// occupancy API for the exact kernel and LDS size; never assumed.  MLVAE_WIDE_2CU=0 or debug
+// bit 21 disables.
+bool two_per_cu_ok(int H, bool fwd) {
+  static const bool enabled = [] {
+    const char* e = getenv("MLVAE_WIDE_2CU");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!enabled || (g_wide_mode & (1 << 21)) || H != 512) return false;
+  const size_t lds = wide_lds(H, 32, fwd);
+  if (2 * lds > (size_t)160 * 1024) return false;
+  const void* k = fwd ? (const void*)lstm_fwd_wide_kernel<1, 16, 4> : (const void*)lstm_bwd_wide_kernel<1, 16, 4>;
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 512, lds) != hipSuccess) return false;
+  hipFuncAttributes at{};
+  if (hipFuncGetAttributes(&at, k) != hipSuccess || at.numRegs > 128) return false;
+  return nb >= 2;
+}
+
 WidePlan wide_plan(int B, int H, bool fwd) {
   WidePlan p{};
   p.ok = false;
   if (H != 512) return p;  // the decoder's H (c2-c5); other H run the batch-group kernels
   p.nkc = H / 32;
   p.NB = (B + BG - 1) / BG;
+  p.per_cu = 1;
   const int cus = wide_cus();
   static const int tpw0 = [] {  // MLVAE_WIDE_TPW=2: start at HJ = 64 units per workgroup (A/B)
     const char* e = getenv("MLVAE_WIDE_TPW");
@@ -716,33 +753,28 @@ WidePlan wide_plan(int B, int H, bool fwd) {
     if (fwd && tpw * p.nkc * 4 > 128) break;   // resident A-fragments <= 128 VGPRs
     const int hj = 32 * tpw, nj = H / hj;
     if (!fwd && (nj < 8 || nj % 8)) continue;   // reduce-scatter: NJ multiple of 8
-    if (2 * p.NB * nj <= cus) {
+    const int wgs = 2 * p.NB * nj;
+    if (wgs <= cus || (tpw == 1 && wgs <= 2 * cus && two_per_cu_ok(H, fwd))) {
       p.tpw = tpw; p.HJ = hj; p.NJ = nj; p.ok = true;
+      p.per_cu = wgs <= cus ? 1 : 2;
       break;
     }
   }
   if (!p.ok) return p;
-  if (fwd) {
-    p.lds = (size_t)2 * 16 * H * 2 + (size_t)2 * 16 * (4 * p.HJ + 8) * 2 +  // h image, gx ring
-            (size_t)2 * 16 * (4 * p.HJ * 2 + 2 * p.HJ * 4 + 16) +              // out ring
-            (size_t)8 * p.tpw * 2 * 64 * 16 +  // + the LDS-resident A-fragments (KLF = 2)
-            (size_t)2 * (16 * p.HJ / 8) * 4;   // + dropout keep bits
-    p.xbytes = (size_t)2 * p.NB * NSLOT * BG * H * 2;
-  } else {
-    p.lds = (size_t)2 * 16 * 4 * p.HJ * 2 +
-            (size_t)8 * (H / 128) * (p.HJ / 32) * 64 * 16 +  // + LDS-resident B-fragments (KLB = KC/4)
-            (size_t)2 * 16 * ((4 * p.HJ * 2 + 16) + 2 * (p.HJ * 4 + 32));  // + staged cell inputs
-    p.xbytes = (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * p.HJ * 16 * 2;
-  }
-  if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;  // one recurrence workgroup per CU
+  p.lds = wide_lds(H, p.HJ, fwd);
+  if (fwd) p.xbytes = (size_t)2 * p.NB * NSLOT * BG * H * 2;
+  else p.xbytes = (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * p.HJ * 16 * 2;
+  // one recurrence workgroup per CU unless two were planned (then > 1/3 of the LDS keeps it to two)
+  if (p.per_cu == 1 && p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;
+  if (p.per_cu == 2 && p.lds < (size_t)(160 * 1024 / 3 + 16)) p.lds = 160 * 1024 / 3 + 16;
   p.xtab_off = p.xbytes;                          // + [groups][NJ] XCC ids (placement check)
   p.xbytes += (size_t)2 * p.NB * p.NJ * sizeof(unsigned);
   return p;
 }
 
-template <int TPW, int NKC>
+template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC> : lstm_bwd_wide_kernel<TPW, NKC>;
+  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC> : lstm_bwd_wide_kernel<TPW, NKC, OCC>;
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
     mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
     return 2;
@@ -753,6 +785,8 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
 }
 
 }  // namespace
+
+void lstm_wide_set_mode(int mode) { g_wide_mode = mode; }
 
 int lstm_wide_workgroups(int B, int H, bool fwd) {
   WidePlan p = wide_plan(B, H, fwd);
@@ -788,5 +822,6 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
     mlvae_set_error("lstm_wide: memset failed");
     return 2;
   }
-  return p.tpw == 2 ? launch_wide<2, 16>(fwd, a, p, st) : launch_wide<1, 16>(fwd, a, p, st);
+  if (p.tpw == 2) return launch_wide<2, 16, 2>(fwd, a, p, st);
+  return p.per_cu == 2 ? launch_wide<1, 16, 4>(fwd, a, p, st) : launch_wide<1, 16, 2>(fwd, a, p, st);
 }

@@ -40,10 +40,12 @@ struct AdamArgs {
 
 // clip coefficient, non-finite skip and bias corrections, once per step (one block):
 // total = ||g||_2 from the sum-of-squares partials folded in a fixed order.
+// err (optional): the persistent recurrences' hand-off timeout word -- once set, this step's
+// gradients are undefined and the update is skipped like a non-finite loss's.
 __global__ __launch_bounds__(256) void adam_prologue(const double* partials, int nparts,
                                                      const float* loss, const int* step, float lr,
                                                      float b1, float b2, float max_norm,
-                                                     float* hyp, float* norm_out) {
+                                                     float* hyp, float* norm_out, const int* err) {
   __shared__ double red[256];
   double a = 0.0;
   for (int i = threadIdx.x; i < nparts; i += 256) a += partials[i];
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(256) void adam_prologue(const double* partials, int
   const double bc1 = 1.0 - pow((double)b1, (double)t);
   const double bc2 = 1.0 - pow((double)b2, (double)t);
   hyp[0] = coef;
-  hyp[1] = (loss && !isfinite(*loss)) ? 1.f : 0.f;
+  hyp[1] = ((loss && !isfinite(*loss)) || (err && *err != 0)) ? 1.f : 0.f;
   hyp[2] = (float)((double)lr / bc1);
   hyp[3] = (float)sqrt(bc2);
   if (norm_out) *norm_out = total;
@@ -100,9 +102,11 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
   }
 }
 
-__global__ void step_counter_kernel(const float* loss, int* step, int* nonfinite) {
+__global__ void step_counter_kernel(const float* loss, int* step, int* nonfinite, const int* err,
+                                    int* err_skips) {
   if (threadIdx.x || blockIdx.x) return;
-  if (loss && !isfinite(*loss)) { if (nonfinite) *nonfinite += 1; }
+  if (err && *err != 0) { if (err_skips) *err_skips += 1; }  // counted apart from non-finite losses
+  else if (loss && !isfinite(*loss)) { if (nonfinite) *nonfinite += 1; }
   else *step += 1;
 }
 
@@ -254,11 +258,11 @@ extern "C" int mlvae_grad_sumsq(const float* g, size_t n, double* partials, void
 }
 
 // hyp: device scratch of >= 4 floats (clip coef, skip flag, step size, sqrt(bias corr 2))
-extern "C" int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
-                               size_t n, const double* partials, int nparts, const float* loss,
-                               int* step, int* nonfinite, float lr, float beta1, float beta2,
-                               float eps, float max_norm, float* norm_out, float* hyp,
-                               int advance, void* stream) {
+extern "C" int mlvae_adam_step_ex(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
+                                  size_t n, const double* partials, int nparts, const float* loss,
+                                  int* step, int* nonfinite, const int* err, int* err_skips, float lr,
+                                  float beta1, float beta2, float eps, float max_norm, float* norm_out,
+                                  float* hyp, int advance, void* stream) {
   if (!hyp || (((uintptr_t)params | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq | (uintptr_t)grads) & 15)) {
     mlvae_set_error("adam_step: needs hyp scratch and 16-byte aligned buffers");
     return 1;
@@ -266,14 +270,24 @@ extern "C" int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq,
   hipStream_t s = (hipStream_t)stream;
   if (advance >= 0)  // advance < 0: reuse hyp from an earlier call of this optimizer step
     adam_prologue<<<1, 256, 0, s>>>(partials, nparts, loss, step, lr, beta1, beta2, max_norm, hyp,
-                                    norm_out);
+                                    norm_out, err);
   AdamArgs a;
   a.p = params; a.m = exp_avg; a.v = exp_avg_sq; a.g = grads; a.n = n; a.hyp = hyp;
   a.b1 = beta1; a.b2 = beta2; a.eps = eps;
   adam_kernel<<<grid_for(n / 4 + 1, 2048), 256, 0, s>>>(a);
-  if (advance > 0) step_counter_kernel<<<1, 64, 0, s>>>(loss, step, nonfinite);
+  if (advance > 0) step_counter_kernel<<<1, 64, 0, s>>>(loss, step, nonfinite, err, err_skips);
   MLVAE_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int mlvae_adam_step(float* params, float* exp_avg, float* exp_avg_sq, const float* grads,
+                               size_t n, const double* partials, int nparts, const float* loss,
+                               int* step, int* nonfinite, float lr, float beta1, float beta2,
+                               float eps, float max_norm, float* norm_out, float* hyp,
+                               int advance, void* stream) {
+  return mlvae_adam_step_ex(params, exp_avg, exp_avg_sq, grads, n, partials, nparts, loss, step,
+                            nonfinite, nullptr, nullptr, lr, beta1, beta2, eps, max_norm, norm_out,
+                            hyp, advance, stream);
 }
 
 extern "C" int mlvae_clip_scale(float* g, size_t n, const double* partials, int nparts,

@@ -86,6 +86,7 @@ _SIGS = {
     "mlvae_sumsq_partials_count": [SZ],
     "mlvae_grad_sumsq": [P, SZ, P, P],
     "mlvae_adam_step": [P, P, P, P, SZ, P, I, P, P, P, F, F, F, F, F, P, P, I, P],
+    "mlvae_adam_step_ex": [P, P, P, P, SZ, P, I, P, P, P, P, P, F, F, F, F, F, P, P, I, P],
     "mlvae_colsum_workspace_size": [I, I],
     "mlvae_colsum": [I, I, P, I, P, P, F, P, SZ, P],
     "mlvae_colsum_ex": [I, I, P, I, I, P, P, F, P, SZ, P],

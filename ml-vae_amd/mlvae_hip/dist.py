@@ -11,8 +11,10 @@ ROCm, gloo for CPU tests).  SURVEY.md 8(e):
   single-GPU gradient of the global batch (no 1/world rescale, exact for unequal lengths);
 * the loss scalars ride along so every rank takes the same non-finite-skip decision and
   clips with the same global norm;
-* eps is drawn from a counter-based stream indexed by the global utterance offset, so the
-  sampled noise is independent of the rank count.
+* eps and the dropout masks are drawn from counter-based streams indexed by (global utterance,
+  frame), so the sampled noise is independent of the rank count; this needs every rank's batch
+  padded to the same T -- the global batch's longest utterance (utils/data_io.py _batched does
+  that), exactly the single-process batch's padding.
 """
 import torch
 import torch.distributed as dist
@@ -22,6 +24,9 @@ def attach(engine, rank, world, batch_per_rank, group=None):
     """Make a VAEEngine data-parallel: shard offset, process group, identical weights."""
     engine.process_group = group
     engine.world = world
+    engine.rank = rank
+    # first global utterance of this shard; re-derived from every batch's own size in
+    # VAEEngine.forward (rank * B), so the loader's batch size -- not a config value -- decides
     engine.global_offset = rank * batch_per_rank
     broadcast_params(engine.flat, group)
     return engine

@@ -323,6 +323,9 @@ class VAEEngine:
         # spin-timeout word of the persistent recurrences (set on a hand-off timeout; the
         # launch then completes with undefined outputs): checked by check_errors()
         self.err = torch.zeros(1, device=self.device, dtype=torch.int32)
+        # optimizer steps skipped because `err` was set (their gradients are undefined): the
+        # fused Adam reads the word on the device, so a timeout never reaches the weights
+        self.err_skips = torch.zeros(1, device=self.device, dtype=torch.int32)
         self._nonfinite_seen = 0   # nonfinite_ctr value at the last check_health()
         # bf16 mode: bf16 copy of the weights, refreshed at the start of every forward
         self.flat_bf = torch.empty(n, device=self.device, dtype=torch.bfloat16) if cfg.prec == "bf16" else None
@@ -378,6 +381,7 @@ class VAEEngine:
         self.kernel_timers = None   # {name: [(start_event, end_event), ...]} when profiling
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
+        self.rank = 0
         self.global_offset = 0      # first global utterance index of this shard
         # data parallel: the gradient suffix from the top LSTM layer on (top layer + heads) is
         # all-reduced on comm_stream during the lower layers' BPTT, the prefix in optimizer_step
@@ -603,6 +607,8 @@ class VAEEngine:
         w = self.work(B, T)
         w.x, w.lens = x, lens
         self._T = T
+        if self.world > 1:  # every rank holds B utterances of the global batch: shard r starts at r * B
+            self.global_offset = self.rank * B
         N, E, Z, H, C, Fd = w.N, cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
         X = _p(x)
@@ -1074,11 +1080,12 @@ class VAEEngine:
             self._allreduce_grads(w)
         check(l.mlvae_grad_sumsq(_p(self.grad), self.layout.total, self.sq_parts.data_ptr(), s), "sumsq")
         b1, b2 = cfg.betas
-        check(l.mlvae_adam_step(_p(self.flat), _p(self.exp_avg), _p(self.exp_avg_sq), _p(self.grad),
-                                self.layout.total, self.sq_parts.data_ptr(), self.nparts,
-                                _p(w.loss, 2), self.step_ctr.data_ptr(), self.nonfinite_ctr.data_ptr(),
-                                cfg.lr, b1, b2, cfg.adam_eps, cfg.max_grad_norm,
-                                _p(self.grad_norm), _p(self.hyp), 1, s), "adam")
+        check(l.mlvae_adam_step_ex(_p(self.flat), _p(self.exp_avg), _p(self.exp_avg_sq), _p(self.grad),
+                                   self.layout.total, self.sq_parts.data_ptr(), self.nparts,
+                                   _p(w.loss, 2), self.step_ctr.data_ptr(), self.nonfinite_ctr.data_ptr(),
+                                   self.err.data_ptr(), self.err_skips.data_ptr(),
+                                   cfg.lr, b1, b2, cfg.adam_eps, cfg.max_grad_norm,
+                                   _p(self.grad_norm), _p(self.hyp), 1, s), "adam")
 
     def _start_suffix_allreduce(self):
         """Everything the top LSTM layer's and the heads' gradients depend on is queued (the
@@ -1147,10 +1154,13 @@ class VAEEngine:
         return w.loss
 
     def check_errors(self):
-        """Host-synchronising check of the persistent kernels' spin-timeout word."""
+        """Host-synchronising check of the persistent kernels' spin-timeout word.  The steps
+        since the timeout were skipped by the fused Adam (err_skips), so the weights and the
+        Adam state are those from before it."""
         if int(self.err.item()) != 0:
             raise RuntimeError("LSTM recurrence hand-off timed out (err word set): the outputs "
-                               "and gradients of the affected steps are undefined")
+                               "of the affected steps are undefined; their optimizer updates were "
+                               f"skipped ({int(self.err_skips.item())} steps)")
 
     def check_health(self, nonfinite_patience=3, where=""):
         """Once-per-stage host check (Brain.fit calls it at every stage end): the recurrence

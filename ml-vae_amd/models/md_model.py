@@ -117,6 +117,11 @@ class MDModel(Brain):
                         info = functools.partial(hip_optim.Adam, *info.args, **info.keywords)
                     opt = info(self.modules.parameters())
                 self.optimizers[key] = opt
+            if self.auto_mix_prec:
+                # SpeechBrain builds the GradScaler with the Brain, before on_fit_start recovers:
+                # registered here (init_optimizers runs right before recover_if_possible), a
+                # resumed run restores its loss scale and growth tracker
+                self._amp_scaler()
         if self.checkpointer is not None:
             for key, opt in self.optimizers.items():
                 self.checkpointer.add_recoverable(key, opt)

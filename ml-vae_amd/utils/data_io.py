@@ -9,8 +9,11 @@
 
 Batches follow SpeechBrain's PaddedBatch: batch['feat'] = (padded [B, Tmax, F], relative lengths
 [B]).  Under data parallelism rank r of W reads utterances [r*bs, (r+1)*bs) of every global batch
-of W*bs (an incomplete last global batch is dropped, so every rank runs the same number of
-steps)."""
+of W*bs, padded to that global batch's longest utterance (so every rank sees the single-process
+batch's T and relative lengths).  TRAIN drops an incomplete last global batch (every rank runs
+the same number of optimizer steps); VALID / TEST keep it: ranks whose slice of the remainder is
+short fill it with zero-length utterances, which every masked mean and frame count excludes."""
+import io
 import pickle
 from pathlib import Path
 
@@ -28,14 +31,75 @@ output_keys = [
 ]
 
 
-def _batched(items, batch_size, rank=0, world=1):
+def _seq_max(items):
+    """{field: longest sequence} over the given utterances (tensor fields with a time axis)."""
+    out = {}
+    for e in items:
+        for k, v in e.items():
+            if torch.is_tensor(v) and v.dim() >= 1:
+                out[k] = max(out.get(k, 0), v.shape[0])
+    return out
+
+
+def _empty_like(e):
+    """A zero-length utterance with the fields of e (fills a short rank slice in evaluation)."""
+    d = {"id": "__pad__"}
+    for k, v in e.items():
+        if k == "id":
+            continue
+        d[k] = v.new_zeros((0,) + tuple(v.shape[1:])) if torch.is_tensor(v) and v.dim() >= 1 else v
+    return d
+
+
+def _batched(items, batch_size, rank=0, world=1, stage=None):
     if world <= 1:
         for i in range(0, len(items), batch_size):
             yield PaddedBatch(items[i:i + batch_size])
         return
     g = batch_size * world
-    for i in range(0, len(items) - g + 1, g):
-        yield PaddedBatch(items[i + rank * batch_size:i + (rank + 1) * batch_size])
+    train = stage is None or getattr(stage, "name", str(stage)).upper() == "TRAIN"
+    end = len(items) - g + 1 if train else len(items)
+    for i in range(0, max(end, 0), g):
+        glob = items[i:i + g]
+        mine = glob[rank * batch_size:(rank + 1) * batch_size]
+        mine = mine + [_empty_like(glob[0])] * (batch_size - len(mine))
+        yield PaddedBatch(mine, pad_to=_seq_max(glob))
+
+
+def _storage_from_bytes(b):
+    """torch.storage._load_from_bytes without its weights_only=False: the tensor storages the
+    reference's pickles hold load through torch's restricted (weights-only) unpickler."""
+    return torch.load(io.BytesIO(b), weights_only=True)
+
+
+class _CorpusUnpickler(pickle.Unpickler):
+    """The reference's computed_dataset/*.pkl holds plain containers, numbers, strings, numpy
+    arrays and torch tensors (SpeechBrain pipeline outputs); anything else (an arbitrary callable
+    a crafted file could name) is refused."""
+    _ALLOWED = {
+        ("builtins", "dict"), ("builtins", "list"), ("builtins", "tuple"), ("builtins", "set"),
+        ("builtins", "frozenset"), ("builtins", "int"), ("builtins", "float"), ("builtins", "str"),
+        ("builtins", "bytes"), ("builtins", "bool"), ("builtins", "complex"),
+        ("collections", "OrderedDict"),
+        ("numpy", "ndarray"), ("numpy", "dtype"), ("numpy.core.multiarray", "_reconstruct"),
+        ("numpy._core.multiarray", "_reconstruct"), ("numpy.core.multiarray", "scalar"),
+        ("numpy._core.multiarray", "scalar"), ("torch._utils", "_rebuild_tensor_v2"),
+        ("torch", "Size"), ("torch", "float32"), ("torch", "float64"), ("torch", "int64"),
+    }
+
+    def find_class(self, module, name):
+        if (module, name) == ("torch.storage", "_load_from_bytes"):
+            return _storage_from_bytes
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"computed dataset pickle names {module}.{name}: refused "
+                                     "(only containers, numbers, strings and numpy arrays load)")
+
+
+def load_corpus_pickle(path):
+    """Restricted load of a computed_dataset/*.pkl (no code from the file is executed)."""
+    with open(path, "rb") as f:
+        return _CorpusUnpickler(io.BytesIO(f.read())).load()
 
 
 def _sort(items, sorting):
@@ -50,8 +114,7 @@ class PickledSet:
     """One split of the reference's computed dataset (a dict of per-utterance dicts)."""
 
     def __init__(self, pkl_path, sorting="descending"):
-        with open(pkl_path, "rb") as f:
-            data = pickle.load(f)  # the user's own corpus files, in the reference's format
+        data = load_corpus_pickle(pkl_path)  # restricted: containers / numbers / numpy arrays
         self.items = []
         for utt_id, d in data.items():
             e = {"id": utt_id}
@@ -70,7 +133,7 @@ class PickledSet:
         return len(self.items)
 
     def batches(self, stage=None, batch_size=8, rank=0, world=1, **_):
-        return _batched(self.items, batch_size, rank, world)
+        return _batched(self.items, batch_size, rank, world, stage)
 
 
 class SyntheticSet:
@@ -88,7 +151,7 @@ class SyntheticSet:
         return len(self.items)
 
     def batches(self, stage=None, batch_size=8, rank=0, world=1, **_):
-        return _batched(self.items, batch_size, rank, world)
+        return _batched(self.items, batch_size, rank, world, stage)
 
 
 def computed_dataset_dir(hparams):

@@ -1,0 +1,97 @@
+"""Whole-step parity of the fused engine against the CPU oracle (oracle/vae_cpu.py), shared by
+the -m gpu parity tests.
+
+One ``VAEEngine.train_step`` runs on the GPU with its own in-kernel randomness (Philox eps in the
+encoder, Philox dropout masks in the recurrence / dgrad epilogue); the eps it drew is read back
+and the masks are replayed on the host (tests/philox_np.py), so the oracle sees the SAME
+randomness through the SAME fused path that bench.py times.
+
+Post-Adam check.  Adam's first step moves every weight by about lr in the direction of -sign(g),
+so a max-|delta| bound cannot tell a right update from a wrong one.  Two checks that can:
+  * sign agreement of the update (new - old) with the oracle's update, over the weights whose
+    oracle gradient is not negligible (|g| > FLOOR x the rms of its tensor's gradient);
+  * the norm-relative error of the update vector over those weights.
+A step that moved every parameter the wrong way scores 0 % agreement and error 2.
+"""
+import numpy as np
+import torch
+
+from gpu_utils import norm_rel
+from oracle import vae_cpu as O
+from philox_np import dropout_mask
+
+FLOOR = 0.1   # |g| > FLOOR * rms(g of the tensor): the weights whose update direction is defined
+
+
+def run_step(cfg, B, T, seed, lens, x=None):
+    """One fused train step on the GPU and the oracle's step on the same inputs/randomness.
+    Returns (engine, work, oracle record, oracle post-Adam params, initial params)."""
+    from mlvae_hip.engine import VAEEngine
+    g = torch.Generator().manual_seed(seed)
+    params = O.init_params(cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C, seed=seed, enc_conv=cfg.enc_conv)
+    if x is None:
+        x = torch.randn(B, T, cfg.F, generator=g)
+    eng = VAEEngine(cfg, params=params, seed=seed)
+    eng.train_step(x.cuda(), lens.cuda())
+    torch.cuda.synchronize()
+    eng.check_errors()
+    w = eng.work(B, T)
+    eps = w.eps_used.detach().cpu().view(B, T, cfg.Z)
+    masks = None
+    if cfg.dropout > 0 and cfg.L > 1:
+        ms = []
+        for li in range(cfg.L - 1):
+            s = (eng.seed * 1000003 + 0 * 131 + li) & ((1 << 63) - 1)   # engine._drop_seed, rng_step 0
+            ms.append(torch.from_numpy(dropout_mask(s, B * T * 2 * cfg.H, cfg.dropout)).view(B, T, 2 * cfg.H))
+        masks = torch.stack(ms)
+    new_ref, rec = O.train_step(params, {}, x, lens, eps,
+                                dict(L=cfg.L, loss_type=cfg.loss_type, kld_weight=cfg.kld_weight),
+                                masks, impl="aten")
+    return eng, w, rec, new_ref, params
+
+
+def update_errors(eng, rec, new_ref, params):
+    """(sign agreement over the defined-direction weights, norm-relative update error over them,
+    max |param - oracle|)."""
+    agree = tot = 0
+    num = den = 0.0
+    dmax = 0.0
+    for k, old in params.items():
+        gr = rec["grads"][k].double()
+        rms = gr.pow(2).mean().sqrt().item()
+        new = eng.view(k).detach().cpu().double()
+        ref = new_ref[k].double()
+        dmax = max(dmax, (new - ref).abs().max().item())
+        if rms == 0.0:
+            continue
+        m = gr.abs() > FLOOR * rms
+        dg = (new - old.double())[m]
+        dr = (ref - old.double())[m]
+        agree += int((torch.sign(dg) == torch.sign(dr)).sum().item())
+        tot += int(m.sum().item())
+        num += (dg - dr).pow(2).sum().item()
+        den += dr.pow(2).sum().item()
+    return agree / max(tot, 1), (num / max(den, 1e-300)) ** 0.5, dmax
+
+
+def errors(eng, w, rec, new_ref, params, B, T):
+    """Relative errors of the step's outputs, gradients and update against the oracle."""
+    Z = eng.cfg.Z
+    out = rec["out"]
+    rel = lambda a, b: abs(a - b) / abs(b)
+    e = {"loss": rel(w.loss[2].item(), out["loss"].item()),
+         "kld_loss": rel(w.loss[0].item(), out["kld_loss"].item()),
+         "recon_loss": rel(w.loss[1].item(), out["recon_loss"].item()),
+         "mu": norm_rel(w.ML[:, :Z].reshape(B, T, Z), out["enc"]["mean"]),
+         "log_var": norm_rel(w.ML[:, Z:].reshape(B, T, Z), out["enc"]["log_var"]),
+         "mu_x": norm_rel(w.MUX.reshape(B, T, -1), out["dec"]["mean"]),
+         "log_var_x": norm_rel(w.LVX.reshape(B, T, -1), out["dec"]["log_var"])}
+    grads = {k: norm_rel(g, rec["grads"][k]) for k, g in eng.named_grads().items()}
+    e["update_sign"], e["update_err"], e["param_maxabs"] = update_errors(eng, rec, new_ref, params)
+    return e, grads
+
+
+def report(tag, e, grads):
+    worst = max(grads, key=grads.get)
+    print(f"\n[{tag}] " + " ".join(f"{k} {v:.2e}" for k, v in e.items()) +
+          f" | grads max {grads[worst]:.2e} ({worst}) median {float(np.median(list(grads.values()))):.2e}")

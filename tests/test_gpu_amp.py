@@ -67,3 +67,21 @@ def test_fused_engine_amp_selects_bf16_mode(tmp_path):
     m = _model(tmp_path, True, True, "fused")
     _fit(m)
     assert m.engine is not None and m.engine.cfg.prec == "bf16"
+
+
+def test_amp_scaler_state_survives_resume(tmp_path):
+    """The GradScaler is registered before on_fit_start's recovery (SpeechBrain builds it with
+    the Brain), so a resumed run restores the loss scale and the growth tracker."""
+    need_gpu()
+    from brain.checkpoints import Checkpointer
+    a = _model(tmp_path, True, False, "amp_a")
+    a.checkpointer = Checkpointer(tmp_path / "ckpt")
+    _fit(a)
+    a.scaler.update(new_scale=1024.0)  # a state the defaults cannot reproduce
+    scale, tracker = a.scaler.get_scale(), a.scaler.state_dict()["_growth_tracker"]
+    a.checkpointer.save_checkpoint(meta={"loss": 1.0})
+    b = _model(tmp_path, True, False, "amp_b")
+    b.checkpointer = Checkpointer(tmp_path / "ckpt")
+    b.on_fit_start()
+    sd = b.scaler.state_dict()
+    assert sd["scale"] == scale == 1024.0 and sd["_growth_tracker"] == tracker

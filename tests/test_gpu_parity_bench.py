@@ -1,0 +1,82 @@
+"""Whole-step parity at the sizes bench.py measures, against the CPU oracle (tests/step_parity.py).
+
+* c3 (the headline): B=256, T=500 -- the wide-batch recurrence instantiation the bench runs
+  (two co-resident workgroups per CU by default; MLVAE_WIDE_2CU=0 / debug bit 21 keeps one);
+* c4 (configs[3]): Conv1d K=5 encoder, B=64, T=2000;
+* c5 (configs[4]): fp8 mode, per-GPU batch B=64 (512 over 8 GPUs), T=500.
+
+Bounds (SURVEY.md 8(d) for bf16: loss 1e-3 relative, mu / log_var 1e-2 norm-relative) and the
+update-direction check of step_parity.py: >= 99.5 % sign agreement of the Adam update with the
+oracle's over the weights whose gradient is defined (|g| > 0.1 rms of its tensor), and the
+update vector within 0.15 norm-relative there.  The measured values are printed."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_utils import need_gpu
+from step_parity import errors, report, run_step
+
+pytestmark = pytest.mark.gpu
+
+SIGN_MIN = 0.995
+UPDATE_ERR = 0.15
+
+
+def _check(e, grads, grad_max, grad_med, out_max=1e-2):
+    assert e["loss"] <= 1e-3 and e["recon_loss"] <= 1e-3, e
+    assert e["kld_loss"] <= 1e-2, e
+    for k in ("mu", "log_var", "mu_x", "log_var_x"):
+        assert e[k] <= out_max, (k, e[k])
+    for k, v in grads.items():
+        assert v <= grad_max, (k, v)
+    assert float(np.median(list(grads.values()))) <= grad_med
+    assert e["update_sign"] >= SIGN_MIN, e["update_sign"]
+    assert e["update_err"] <= UPDATE_ERR, e["update_err"]
+
+
+@pytest.mark.parametrize("two_per_cu", [1, 0])
+def test_c3_headline_B256_T500_matches_oracle(two_per_cu):
+    """The benchmarked step at the metric's batch: B=256, T=500, dropout 0.15, bf16."""
+    need_gpu()
+    from mlvae_hip._lib import lib
+    from mlvae_hip.engine import VAEConfig
+    cfg = VAEConfig(F=80, E=64, Z=32, H=512, L=2, C=64, dropout=0.15, prec="bf16")
+    B, T = 256, 500
+    lens = torch.linspace(0.6, 1.0, B)
+    lens[5], lens[9] = 127 / 500, 254 / 500
+    lib().mlvae_lstm_set_debug_mode(0 if two_per_cu else (1 << 21))
+    try:
+        wgs = lib().mlvae_lstm_launch_workgroups(B, 512, 1, 0)
+        eng, w, rec, new_ref, params = run_step(cfg, B, T, 2718, lens)
+    finally:
+        lib().mlvae_lstm_set_debug_mode(0)
+    e, grads = errors(eng, w, rec, new_ref, params, B, T)
+    report(f"c3 B=256 T=500 wide {wgs} WGs", e, grads)
+    _check(e, grads, 4e-2, 1.5e-2)
+
+
+def test_c4_conv_B64_T2000_matches_oracle():
+    """configs[3] at its benchmarked size: Conv1d K=5 encoder, B=64, T=2000, dropout 0.15."""
+    need_gpu()
+    from mlvae_hip.engine import VAEConfig
+    cfg = VAEConfig(F=80, E=64, Z=32, H=512, L=2, C=64, dropout=0.15, prec="bf16", enc_conv=5)
+    B, T = 64, 2000
+    lens = torch.linspace(0.55, 1.0, B)
+    eng, w, rec, new_ref, params = run_step(cfg, B, T, 4243, lens)
+    e, grads = errors(eng, w, rec, new_ref, params, B, T)
+    report("c4 conv K=5 B=64 T=2000", e, grads)
+    _check(e, grads, 4e-2, 1.5e-2)
+
+
+def test_c5_fp8_B64_T500_matches_oracle():
+    """configs[4]'s per-GPU shard in fp8 mode at T=500 (the fp8 products' own bounds: e4m3 keeps
+    3 mantissa bits)."""
+    need_gpu()
+    from mlvae_hip.engine import VAEConfig
+    cfg = VAEConfig(F=80, E=64, Z=32, H=512, L=2, C=64, dropout=0.15, prec="bf16", fp8=True)
+    B, T = 64, 500
+    lens = torch.linspace(0.6, 1.0, B)
+    eng, w, rec, new_ref, params = run_step(cfg, B, T, 809, lens)
+    e, grads = errors(eng, w, rec, new_ref, params, B, T)
+    report("c5 fp8 B=64 T=500", e, grads)
+    _check(e, grads, 0.12, 3e-2)

@@ -60,6 +60,32 @@ def test_err_word_raises_at_the_stage_check():
         eng.check_health()
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_err_word_mid_stage_leaves_weights_and_adam_state_untouched(prec):
+    """A recurrence hand-off timeout (the err word, set here as the kernels would set it) in the
+    middle of a stage: the fused Adam reads the word on the device and skips every update from
+    then on, counted in err_skips apart from non-finite losses; the stage-end check raises."""
+    need_gpu()
+    eng = VAEEngine(_tiny_cfg(prec), params=O.init_params(16, 16, 8, 32, 2, 16, seed=4))
+    B, T = 3, 10
+    x = torch.randn(B, T, 16).cuda()
+    lens = torch.ones(B).cuda()
+    eng.train_step(x, lens)                 # a good step first: the state moves
+    torch.cuda.synchronize()
+    before = [t.clone() for t in (eng.flat, eng.exp_avg, eng.exp_avg_sq)]
+    step = int(eng.step_ctr.item())
+    eng.err.fill_(1)                         # the timeout
+    for _ in range(3):
+        eng.train_step(x, lens)
+    torch.cuda.synchronize()
+    for a, b in zip(before, (eng.flat, eng.exp_avg, eng.exp_avg_sq)):
+        assert torch.equal(a, b)
+    assert int(eng.step_ctr.item()) == step and int(eng.err_skips.item()) == 3
+    assert int(eng.nonfinite_ctr.item()) == 0
+    with pytest.raises(RuntimeError, match="skipped \\(3 steps\\)"):
+        eng.check_health()
+
+
 def test_varying_padded_length_reuses_workspace_and_matches_oracle():
     """PaddedBatch's Tmax changes every batch: the engine reuses its pooled workspace (no
     reallocation once the largest B*T has been seen) and each step still matches the oracle,
