@@ -121,12 +121,12 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(cfg_name, budget_s=12.0):
+def cpu_baseline(cfg_name, budget_s=15.0):
     """The CPU oracle (torch CPU, ATen LSTM as the reference calls it) on this host, on a
-    bounded sample: full train steps of the same model and T at B=32 (configs[1])."""
+    bounded sample of the same workload: whole train steps at the benchmarked shape (the
+    headline's B=256, T=500), as many as fit the budget (at least one)."""
     from oracle import vae_cpu as O
-    F, E, Z, H, L, C, _, T, _ = CONFIGS[cfg_name]
-    B = 32 if cfg_name in ("c2", "c3") else CONFIGS[cfg_name][6]
+    F, E, Z, H, L, C, B, T, _ = CONFIGS[cfg_name]
     threads = os.cpu_count() or 1
     cap = int(os.environ.get("OMP_NUM_THREADS", threads))
     torch.set_num_threads(max(1, min(threads, cap)))
@@ -237,7 +237,10 @@ def global_batch_shard(B, T, F, rank, device):
     return xg[rank * B:].contiguous()
 
 
-def timed_run(eng, x, lens, steps, warmup, world, timers=None):
+def timed_run(eng, x, lens, steps, warmup, world, timers=None, norm=None):
+    """Warm up, then time exactly `steps` fused train steps between barrier + synchronize
+    brackets.  norm: the recipe's InputNormalization, run on the device inside every step
+    (ref:src/models/test_vanilla_vae/model.py:24-25 normalises each batch before the encoder)."""
     def barrier():
         if world > 1:
             import torch.distributed as dist
@@ -245,14 +248,14 @@ def timed_run(eng, x, lens, steps, warmup, world, timers=None):
         torch.cuda.synchronize()
 
     for _ in range(warmup):
-        eng.train_step(x, lens)
+        eng.train_step(x, lens, normalizer=norm)
     barrier()
     eng.check_errors()
     t0 = time.perf_counter()
     loss = None
     for i in range(steps):
         eng.kernel_timers = timers if (timers is not None and i % TIMER_EVERY == 0) else None
-        loss = eng.train_step(x, lens)
+        loss = eng.train_step(x, lens, normalizer=norm)
     barrier()
     dt = time.perf_counter() - t0
     eng.kernel_timers = None
@@ -306,7 +309,9 @@ def extra_runs(args, device):
         x = global_batch_shard(B, T, F, 0, device)
         lens = torch.ones(B, device=device)
         timers = {}
-        dt, loss = timed_run(eng, x, lens, steps, warm, 1, timers if cname in ("c4", "c5", "c5bf16") else None)
+        from brain.features import InputNormalization
+        dt, loss = timed_run(eng, x, lens, steps, warm, 1, timers if cname in ("c4", "c5", "c5bf16") else None,
+                             InputNormalization())
         lv = loss.tolist()
         out[key] = {"global_batch": B, "seq_len": T, "dtype": prec, "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
@@ -378,10 +383,12 @@ def main():
     else:
         B = batch
     eng = make_engine(args.config, args.prec, device, world, rank, B)
-    x = global_batch_shard(B, T, F, rank, device)   # synthetic normalised log-mel
+    x = global_batch_shard(B, T, F, rank, device)   # synthetic log-mel stand-in
     lens = torch.ones(B, device=device)
     timers = {}
-    dt, loss = timed_run(eng, x, lens, args.steps, args.warmup, world, timers)
+    from brain.features import InputNormalization   # the recipe's normaliser (model.yaml:14-15)
+    norm = InputNormalization()
+    dt, loss = timed_run(eng, x, lens, args.steps, args.warmup, world, timers, norm)
     ms = dt / args.steps * 1e3
     value = B * T * world * args.steps / dt
     lv = loss.tolist()
@@ -410,7 +417,8 @@ def main():
             "scaling": "strong" if is_global else "weak",
             "vs_baseline": None,
             "dtype": args.prec,
-            "data": "synthetic N(0,1) 80-d frames (normalised log-mel stand-in), lens=1, "
+            "data": "synthetic N(0,1) 80-d frames (log-mel stand-in), lens=1, globally normalised "
+                    "inside every timed step by the recipe's InputNormalization on the device, "
                     "random-init weights (PyTorch default init, seed 123456)",
             "config": {"workload": f"{args.config}: {enc_desc} enc [{F},{E},{E}] z={Z}, BiLSTM "
                                    f"{L}x{H} (dropout 0.15), dec-FC [{2 * H},{C},{C},{F}], T={T}, "

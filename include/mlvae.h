@@ -348,6 +348,24 @@ int mlvae_randn(size_t n, unsigned long long seed, unsigned long long offset, fl
 int mlvae_masked_mean(int B, int T, int C, const float* loss, const float* lens, int reduction,
                       float* out, void* stream);
 
+/* InputNormalization(norm_type='global') inside the fused step: SpeechBrain's normaliser
+ * (un-vendored; parity unpinned, restated in brain/features.py), built at
+ * ref:src/models/test_vanilla_vae/model.yaml:14-15 and applied at
+ * ref:src/models/test_vanilla_vae/model.py:24-25.  F % 4 == 0, 16-byte aligned buffers.
+ *   stats:  per-utterance mean / std over the first round(rel_len*T) frames -> utt_stats [B][2F];
+ *           sums [2F+1] = the sums of those over the utterances with frames, and their count
+ *           (what a data-parallel run all-reduces before the update)
+ *   update: mode 0 keep, 1 set the global statistics to the batch's, 2 running average with
+ *           weight w of the batch (epoch < update_until_epoch): g = w_old g + w_new cur
+ *   apply:  out = (x - glob_mean) / glob_std over rows x F */
+int mlvae_norm_supported(int F);
+int mlvae_norm_stats(int B, int T, int F, const float* x, const float* rel_lens, float* utt_stats,
+                     float* sums, float eps, void* stream);
+int mlvae_norm_update(int F, const float* sums, float* glob_mean, float* glob_std, int mode,
+                      float w_old, float w_new, void* stream);  /* mode 2: w_old = 1 - w, w_new = w */
+int mlvae_norm_apply(size_t rows, int F, const float* x, const float* glob_mean, const float* glob_std,
+                     float* out, void* stream);
+
 /* check_gradients + Adam (ref:src/models/md_model.py:82-86, model.yaml:45-47). */
 int mlvae_sumsq_partials_count(size_t n);
 int mlvae_grad_sumsq(const float* grads, size_t n, double* partials, void* stream);

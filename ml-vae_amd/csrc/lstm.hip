@@ -1147,7 +1147,7 @@ extern "C" int mlvae_lstm_set_debug(void* buf) {
 // bit3 reserves 100 KB LDS per recurrence workgroup, bit4 polls with s_sleep 1 instead of 4,
 // bits 5-10 delay the first poll sweep of every step by that many s_sleep 1, bit 11 times the
 // batch-group kernels without their prefetch, bit 12 runs the wide-batch kernels at any batch,
-// bit 21 keeps the wide kernels at one workgroup per CU (no two-per-CU plan; A/B and tests).
+// bit 22 runs the wide forward as two interleaved chains per workgroup (lstm_fwd_il_kernel).
 extern "C" int mlvae_lstm_set_debug_mode(int mode) {
   g_dbg_mode = mode;
   lstm_wide_set_mode(mode);

@@ -55,8 +55,7 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
-// OCC = minimum waves per SIMD: 2 = one workgroup per CU, 4 = two co-resident workgroups per CU
-// (<= 128 VGPRs), whose step chains then overlap each other's hand-off waits
+// OCC = minimum waves per SIMD (2: one 512-thread workgroup per CU)
 template <int TPW, int NKC, int OCC>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
@@ -351,6 +350,304 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   };
   if (io) run(std::true_type{});
   else run(std::false_type{});
+}
+
+// ---------------------------------------------------------------------------------------
+// forward, two chains per workgroup (interleaved)
+// ---------------------------------------------------------------------------------------
+// A workgroup owns the same HJ units of TWO batch groups (chains) of one direction and
+// alternates between them: while chain A's h_t travels to the other workgroups of its group,
+// the workgroup computes chain B's step, so the inter-CU hand-off overlaps MFMA work instead
+// of idling the CU.  The W_hh fragments (registers + LDS) serve both chains.  Sub-step (s, c):
+//   pollers (waves 0-3)  poll chain c's h_{t-1} into its LDS image          | barrier |
+//   every wave           MFMA over the image, cell update (chain c's state), publish h_t,
+//                        chain c's step-s outputs into its out ring
+//   loaders (waves 4-5)  after the barrier: LDS-DMA of chain c's gx(s+1); after publish: the
+//                        dropout keep bits of chain c's step s
+//   storers (waves 6-7)  after publish: the previous sub-step's outputs LDS -> HBM
+// Loaders issue a fixed number of DMAs per sub-step (padded rows read a clamped valid row), so
+// a counted vmcnt waits for chain c's gx without waiting for the other chain's; storers never
+// wait on their stores.  The number of batch groups is padded to even (a padded group runs on
+// zeros and stores nothing).
+template <int TPW, int NKC>
+__global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
+  constexpr int HJ = WW * TPW * 4;
+  constexpr int H = NKC * 32;
+  constexpr int PL = NKC / 4;                 // poll loads (k-chunks) per lane, waves 0-3
+  constexpr int ROWB = H * 2;
+  constexpr int HIMG = 16 * ROWB;             // one chain's h image (single-buffered)
+  constexpr int GXU = 4 * HJ + 8;             // gx halfs per utterance: [gate][unit] + 16 B
+  constexpr int GXS = 16 * GXU;               // halfs per gx slot
+  constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;  // gates fp16 | c fp32 | h fp32 | 16 B
+  constexpr int NC8 = 16 * HJ / 8;
+  constexpr int KLF = 2;
+  constexpr int KR = NKC - KLF;
+  constexpr int UPL = 16 / 2;                 // utterances (DMAs) per loader wave and sub-step
+  static_assert(NC8 <= 128, "one keep-bit chunk per loader / storer thread");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* himg = smem;                                                         // [2 ch][HIMG]
+  unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2 ch][2 slot][GXS]
+  char* outr = reinterpret_cast<char*>(gxr + 4 * GXS);                      // [2 ch][16][OUB]
+  bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUB);            // [wave][TPW][KLF][lane]
+  unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);   // [2 ch][NC8]
+  __shared__ int abort_flag;
+
+  const int NBe = (a.NB + 1) & ~1, npair = NBe / 2;
+  const int ngroups = 2 * npair, gstride = (ngroups + 7) & ~7;
+  const int gid = blockIdx.x % gstride, js = blockIdx.x / gstride;
+  if (gid >= ngroups) return;
+  const int dir = gid / npair, pr = gid % npair;
+  const int T = a.T, j0 = js * HJ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* W = dir ? a.W1 : a.W0;
+  const int bi = lane & 15, q = lane >> 4;
+
+  bf16x8 wreg[TPW][KR];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int m = wave * TPW + t;
+    const float* wrow = W + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * H;
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q + 4);
+      bf16x8 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[e] = f2bf(w0[e]); v[4 + e] = f2bf(w1[e]); }
+      if (kc < KR) wreg[t][kc < KR ? kc : 0] = v;
+      else wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane] = v;
+    }
+  }
+  __shared__ int placement;
+  const bool same_xcd = group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement) &&
+                        !(a.dbg_mode & 32768);
+  if (tid == 0) abort_flag = 0;
+
+  const size_t xslot = (size_t)BG * H;
+  short* const xbase = reinterpret_cast<short*>(a.xbuf);
+  // chain c = batch group 2 pr + c of this direction: its own exchange (the wide layout)
+  auto xrc = [&](int c) {
+    return make_rsrc(xbase + (size_t)(dir * NBe + 2 * pr + c) * NSLOT * xslot,
+                     (unsigned)(NSLOT * xslot * sizeof(short)));
+  };
+  const auto xr0 = xrc(0), xr1 = xrc(1);
+
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
+  const int role = wave < 4 ? 0 : (wave < 6 ? 1 : 2);  // poller / loader / storer (uniform)
+  const int lw = wave - 4, sw = tid - 384;             // loader wave 0-1, storer thread 0-127
+  auto io_load = [&](int c, int s_) {  // chain c's gx of step s_ -> slot s_ & 1 (fixed DMA count)
+    const int sc = s_ < T ? s_ : T - 1;
+    const int t_ = dir ? T - 1 - sc : sc;
+#pragma unroll
+    for (int i = 0; i < UPL; ++i) {
+      const int u = lw * UPL + i;
+      const int b = min((2 * pr + c) * BG + u, a.B - 1);  // padded rows: a clamped valid row
+      const auto rs = make_rsrc(G16 + (size_t)b * T * 8 * H, (unsigned)((size_t)T * 8 * H * 2));
+      const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
+      const unsigned off = (unsigned)(((size_t)t_ * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
+      unsigned short* dst = gxr + (c * 2 + (s_ & 1)) * GXS + u * GXU;
+      if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
+    }
+  };
+  auto drop_bits = [&](int c, int s_, int c8) -> unsigned {
+    const int u = c8 / (HJ / 8), uu = (c8 % (HJ / 8)) * 8;
+    const int t_ = dir ? T - 1 - s_ : s_;
+    const size_t o = ((size_t)((2 * pr + c) * BG + u) * T + t_) * 2 * H + dir * H + j0 + uu;
+    unsigned w0[4], w1[4];
+    philox4(a.dseed, (a.doff + o) >> 2, w0);
+    philox4(a.dseed, (a.doff + o + 4) >> 2, w1);
+    unsigned bits = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bits |= (dropout_word_scale(w0[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
+      bits |= (dropout_word_scale(w1[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
+    }
+    return bits;
+  };
+  auto io_store = [&](int c, int s_) {  // chain c's saved step-s_ activations (storer threads)
+    if (a.dbg_mode & 1) return;
+    const int t_ = dir ? T - 1 - s_ : s_;
+    const char* src = outr + c * 16 * OUB;
+    const int g0 = (2 * pr + c) * BG;
+    constexpr int NG8 = 16 * 4 * HJ / 8;
+    for (int ci = sw; ci < NG8; ci += 128) {
+      const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
+      const int u = row >> 2, g = row & 3, b = g0 + u;
+      if (b >= a.B) continue;
+      *reinterpret_cast<u32x4*>(G16 + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
+          *reinterpret_cast<const u32x4*>(src + u * OUB + (g * HJ + uu) * 2);
+    }
+    constexpr int NQ2 = 16 * HJ / 4;
+    for (int qi = sw; qi < NQ2; qi += 128) {
+      const int u = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4, b = g0 + u;
+      if (b >= a.B) continue;
+      const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
+      const float* cf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ);
+      *reinterpret_cast<f32x4*>(a.Cs + o) = *reinterpret_cast<const f32x4*>(cf + uu);
+      if (a.Y) *reinterpret_cast<f32x4*>(a.Y + o) = *reinterpret_cast<const f32x4*>(cf + HJ + uu);
+    }
+    if (sw < NC8) {  // h (bf16) and dropout(h) (bf16) of one 8-unit chunk per thread
+      const int u = sw / (HJ / 8), uu = (sw % (HJ / 8)) * 8, b = g0 + u;
+      if (b < a.B) {
+        const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
+        const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
+        if (a.Yb)
+          *reinterpret_cast<bf16x8*>(a.Yb + o) =
+              bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
+                     f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+        if (a.Ydb) {
+          const unsigned bits = dbl[c * NC8 + sw];
+          f32x4 d0, d1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            d0[e] = (bits >> e) & 1 ? v0[e] * a.dscale : 0.f;
+            d1[e] = (bits >> (4 + e)) & 1 ? v1[e] * a.dscale : 0.f;
+          }
+          *reinterpret_cast<bf16x8*>(a.Ydb + o) =
+              bf16x8{f2bf(d0[0]), f2bf(d0[1]), f2bf(d0[2]), f2bf(d0[3]),
+                     f2bf(d1[0]), f2bf(d1[1]), f2bf(d1[2]), f2bf(d1[3])};
+        }
+      }
+    }
+  };
+
+  auto run = [&](auto role_tag) {
+    constexpr int ROLE = decltype(role_tag)::value;
+    if (ROLE == 1) {
+      io_load(0, 0); io_load(0, 1); io_load(1, 0); io_load(1, 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    float cst[2][TPW];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) cst[c][t] = 0.f;
+    int pend_c = -1, pend_s = 0;  // storers: the last completed sub-step not yet stored
+    bool aborted = false;
+    for (int s = 0; s < T && !aborted; ++s) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        // step 0 has no poll / barrier: one here orders chain 0's out ring before its store
+        if (s == 0 && c == 1) __syncthreads();
+        STAMP(c * 8 + 0);
+        char* hb = himg + c * HIMG;
+        const auto xr = c ? xr1 : xr0;
+        const bool valid = (2 * pr + c) * BG + bi < a.B;
+        f32x4 acc[TPW];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float gxv[TPW][4];
+        auto read_gx = [&]() {
+          const unsigned short* gx = gxr + (c * 2 + (s & 1)) * GXS + bi * GXU;
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            const int u = 4 * (wave * TPW + t) + q;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = h2f(gx[g4 * HJ + u]);
+          }
+        };
+        if (s == 0) read_gx();
+        if (s > 0) {
+          if (ROLE == 1) {
+            // chain c's gx(s) was issued two sub-steps ago; younger than it: this wave's TPW
+            // publishes of chain c, the other chain's UPL = 8 DMAs and (but at the last step)
+            // its TPW publishes -- at least 8 + TPW ops, so vmcnt(8 + TPW) covers gx(s)
+            if constexpr (TPW == 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+          } else if (ROLE == 0) {
+            const unsigned tag = step_tag(s - 1);
+            const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * H + wave * PL * 32 + 8 * q;
+            u32x4 hv[PL];
+            unsigned spins = 0;
+            while (true) {
+#pragma unroll
+              for (int i = 0; i < PL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
+              bool ok = true;
+#pragma unroll
+              for (int i = 0; i < PL; ++i) ok &= tags_ok(hv[i], tag, true, true);
+              if (__all(ok)) break;
+              if (++spins > SPIN_LIMIT) {
+                if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+            STAMP(c * 8 + 1);
+#pragma unroll
+            for (int i = 0; i < PL; ++i)
+              *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
+          }
+          __syncthreads();
+          STAMP(c * 8 + 2);
+          if (abort_flag) { aborted = true; break; }
+          if (ROLE == 1) io_load(c, s + 1);
+          read_gx();
+#pragma unroll
+          for (int kc = 0; kc < NKC; ++kc) {
+            const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+              const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
+                                        : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag, acc[t], 0, 0, 0);
+            }
+          }
+          STAMP(c * 8 + 3);
+        }
+        float hvals[TPW], gates[TPW][4];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const float ig = sigmoid_fast(acc[t][0] + gxv[t][0]);
+          const float fg = sigmoid_fast(acc[t][1] + gxv[t][1]);
+          const float gg = tanh_fast(acc[t][2] + gxv[t][2]);
+          const float og = sigmoid_fast(acc[t][3] + gxv[t][3]);
+          cst[c][t] = valid ? fg * cst[c][t] + ig * gg : 0.f;
+          hvals[t] = valid ? og * tanh_fast(cst[c][t]) : 0.f;
+          gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
+        }
+        if (s + 1 < T) {
+          const unsigned tag = step_tag(s);
+          const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * H + j0;
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            const unsigned hu = __float_as_uint(hvals[t]);
+            const unsigned x1 = __builtin_amdgcn_permlane16_swap(hu, hu, false, false)[1];
+            const unsigned x2 = __builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1];
+            const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];
+            if (q == 0)
+              publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)),
+                      pack_bf16(hvals[t], __uint_as_float(x1), __uint_as_float(x2), __uint_as_float(x3), tag),
+                      same_xcd);
+          }
+        }
+        STAMP(c * 8 + 4);
+        if (ROLE == 2 && pend_c >= 0) io_store(pend_c, pend_s);
+        char* ob = outr + c * 16 * OUB + bi * OUB;
+        unsigned short* og = reinterpret_cast<unsigned short*>(ob);
+        float* of = reinterpret_cast<float*>(ob + 8 * HJ);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const int u = 4 * (wave * TPW + t) + q;
+          og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
+          og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
+          of[u] = cst[c][t]; of[HJ + u] = hvals[t];
+        }
+        if (ROLE == 1 && a.Ydb && (tid - 256) < NC8) dbl[c * NC8 + (tid - 256)] = drop_bits(c, s, tid - 256);
+        pend_c = c; pend_s = s;
+      }
+    }
+    __syncthreads();
+    if (ROLE == 2) io_store(pend_c, pend_s);
+    if (ROLE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
+  };
+  if (role == 0) run(std::integral_constant<int, 0>{});
+  else if (role == 1) run(std::integral_constant<int, 1>{});
+  else run(std::integral_constant<int, 2>{});
 }
 
 // ---------------------------------------------------------------------------------------
@@ -691,10 +988,17 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------------------
 struct WidePlan {
   int tpw, nkc, NB, NJ, HJ;
-  int per_cu;  // co-resident recurrence workgroups per CU (1, or 2 at OCC = 4)
   size_t lds, xbytes, xtab_off;
   bool ok;
+  bool il;  // forward: two chains (batch groups) per workgroup, lstm_fwd_il_kernel
 };
+
+// Interleaved forward (lstm_fwd_il_kernel): MLVAE_WIDE_IL=0/1 (default off until measured),
+// MLVAE_IL_TPW=1/2 its units per workgroup (HJ = 32 / 64)
+int il_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 
 int wide_cus() {
   int dev = 0, cus = 256;
@@ -715,35 +1019,32 @@ size_t wide_lds(int H, int hj, bool fwd) {
          (size_t)2 * 16 * ((4 * hj * 2 + 16) + 2 * (hj * 4 + 32));  // + staged cell inputs
 }
 
-int g_wide_mode = 0;  // lstm_wide_set_mode
-
-// Two co-resident workgroups per CU (HJ = 32 at the OCC = 4 instantiation): checked against the
-// occupancy API for the exact kernel and LDS size; never assumed.  MLVAE_WIDE_2CU=0 or debug
-// bit 21 disables.
-bool two_per_cu_ok(int H, bool fwd) {
-  static const bool enabled = [] {
-    const char* e = getenv("MLVAE_WIDE_2CU");
-    return !(e && atoi(e) == 0);
-  }();
-  if (!enabled || (g_wide_mode & (1 << 21)) || H != 512) return false;
-  const size_t lds = wide_lds(H, 32, fwd);
-  if (2 * lds > (size_t)160 * 1024) return false;
-  const void* k = fwd ? (const void*)lstm_fwd_wide_kernel<1, 16, 4> : (const void*)lstm_bwd_wide_kernel<1, 16, 4>;
-  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 512, lds) != hipSuccess) return false;
-  hipFuncAttributes at{};
-  if (hipFuncGetAttributes(&at, k) != hipSuccess || at.numRegs > 128) return false;
-  return nb >= 2;
-}
+int g_wide_mode = 0;  // lstm_wide_set_mode (debug bits; none read by the plans at present)
 
 WidePlan wide_plan(int B, int H, bool fwd) {
   WidePlan p{};
   p.ok = false;
+  p.il = false;
   if (H != 512) return p;  // the decoder's H (c2-c5); other H run the batch-group kernels
   p.nkc = H / 32;
   p.NB = (B + BG - 1) / BG;
-  p.per_cu = 1;
+  static const int il = il_env("MLVAE_WIDE_IL", 0), il_tpw = il_env("MLVAE_IL_TPW", 2) == 1 ? 1 : 2;
+  if (fwd && (il || (g_wide_mode & (1 << 22)))) {
+    const int npair = (p.NB + 1) / 2, NBe = 2 * npair;
+    for (int tpw = il_tpw; tpw >= 1; --tpw) {
+      const int hj = 32 * tpw, nj = H / hj;
+      if (2 * npair * nj > wide_cus()) continue;
+      p.tpw = tpw; p.HJ = hj; p.NJ = nj; p.ok = true; p.il = true;
+      const int gxs = 16 * (4 * hj + 8);
+      p.lds = (size_t)2 * 16 * H * 2 + (size_t)4 * gxs * 2 + (size_t)2 * 16 * (4 * hj * 2 + 2 * hj * 4 + 16) +
+              (size_t)8 * tpw * 2 * 64 * 16 + (size_t)2 * (16 * hj / 8) * 4;
+      if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;
+      p.xbytes = (size_t)2 * NBe * NSLOT * BG * H * 2;
+      p.xtab_off = p.xbytes;
+      p.xbytes += (size_t)2 * NBe * p.NJ * sizeof(unsigned);
+      return p;
+    }
+  }
   const int cus = wide_cus();
   static const int tpw0 = [] {  // MLVAE_WIDE_TPW=2: start at HJ = 64 units per workgroup (A/B)
     const char* e = getenv("MLVAE_WIDE_TPW");
@@ -753,10 +1054,12 @@ WidePlan wide_plan(int B, int H, bool fwd) {
     if (fwd && tpw * p.nkc * 4 > 128) break;   // resident A-fragments <= 128 VGPRs
     const int hj = 32 * tpw, nj = H / hj;
     if (!fwd && (nj < 8 || nj % 8)) continue;   // reduce-scatter: NJ multiple of 8
-    const int wgs = 2 * p.NB * nj;
-    if (wgs <= cus || (tpw == 1 && wgs <= 2 * cus && two_per_cu_ok(H, fwd))) {
+    // one workgroup per CU.  (Two co-resident HJ = 32 workgroups per CU at B = 256, whose step
+    // chains could overlap each other's hand-off waits, measured slower: forward 1.70 vs 1.33 ms,
+    // BPTT 1.93 vs 1.38 ms per launch -- 16 producers per consumer and twice the pollers per CU
+    // lengthened the hand-off, 2,896 -> 4,320 ticks)
+    if (2 * p.NB * nj <= cus) {
       p.tpw = tpw; p.HJ = hj; p.NJ = nj; p.ok = true;
-      p.per_cu = wgs <= cus ? 1 : 2;
       break;
     }
   }
@@ -764,9 +1067,7 @@ WidePlan wide_plan(int B, int H, bool fwd) {
   p.lds = wide_lds(H, p.HJ, fwd);
   if (fwd) p.xbytes = (size_t)2 * p.NB * NSLOT * BG * H * 2;
   else p.xbytes = (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * p.HJ * 16 * 2;
-  // one recurrence workgroup per CU unless two were planned (then > 1/3 of the LDS keeps it to two)
-  if (p.per_cu == 1 && p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;
-  if (p.per_cu == 2 && p.lds < (size_t)(160 * 1024 / 3 + 16)) p.lds = 160 * 1024 / 3 + 16;
+  if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;  // one recurrence workgroup per CU (residency)
   p.xtab_off = p.xbytes;                          // + [groups][NJ] XCC ids (placement check)
   p.xbytes += (size_t)2 * p.NB * p.NJ * sizeof(unsigned);
   return p;
@@ -784,13 +1085,27 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   return 0;
 }
 
+template <int TPW, int NKC>
+int launch_il(const LstmArgs& a, const WidePlan& p, hipStream_t s) {
+  auto k = lstm_fwd_il_kernel<TPW, NKC>;
+  if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
+    mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
+    return 2;
+  }
+  const int npair = (p.NB + 1) / 2;
+  k<<<dim3(((2 * npair + 7) & ~7) * p.NJ), 512, p.lds, s>>>(a);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 void lstm_wide_set_mode(int mode) { g_wide_mode = mode; }
 
 int lstm_wide_workgroups(int B, int H, bool fwd) {
   WidePlan p = wide_plan(B, H, fwd);
-  return p.ok ? 2 * p.NB * p.NJ : 0;
+  if (!p.ok) return 0;
+  return p.il ? ((p.NB + 1) / 2) * 2 * p.NJ : 2 * p.NB * p.NJ;
 }
 
 size_t lstm_wide_xbytes(int B, int H, bool fwd) {
@@ -822,6 +1137,6 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
     mlvae_set_error("lstm_wide: memset failed");
     return 2;
   }
-  if (p.tpw == 2) return launch_wide<2, 16, 2>(fwd, a, p, st);
-  return p.per_cu == 2 ? launch_wide<1, 16, 4>(fwd, a, p, st) : launch_wide<1, 16, 2>(fwd, a, p, st);
+  if (p.il) return p.tpw == 2 ? launch_il<2, 16>(a, p, st) : launch_il<1, 16>(a, p, st);
+  return p.tpw == 2 ? launch_wide<2, 16, 2>(fwd, a, p, st) : launch_wide<1, 16, 2>(fwd, a, p, st);
 }

@@ -102,6 +102,10 @@ _SIGS = {
     "mlvae_lstm_launch_workgroups": [I, I, I, I],
     "mlvae_lstm_set_debug": [P],
     "mlvae_lstm_set_debug_mode": [I],
+    "mlvae_norm_supported": [I],
+    "mlvae_norm_stats": [I, I, I, P, P, P, P, F, P],
+    "mlvae_norm_update": [I, P, P, P, I, F, F, P],
+    "mlvae_norm_apply": [SZ, I, P, P, P, P, P],
 }
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,

@@ -13,7 +13,7 @@ PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(HERE, "libmlvae.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["capi.cpp", "gemm.hip", "gemm_bf16.hip", "gemm_fast.hip", "heads.hip", "skinny.hip", "encoder.hip", "lstm.hip", "lstm_wide.hip", "elbo.hip", "gmm.hip", "md.hip", "decode.hip", "conv.hip", "fp8.hip", "optim.hip"]
+SOURCES = ["capi.cpp", "gemm.hip", "gemm_bf16.hip", "gemm_fast.hip", "heads.hip", "skinny.hip", "encoder.hip", "lstm.hip", "lstm_wide.hip", "elbo.hip", "gmm.hip", "md.hip", "decode.hip", "conv.hip", "fp8.hip", "norm.hip", "optim.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
          "-I" + CSRC]
 

@@ -1132,20 +1132,74 @@ class VAEEngine:
                 self_.caller.wait_stream(eng.main_stream)
         return _M()
 
-    def train_step(self, x, lens, eps=None, dropout_masks=None):
-        """One fit_batch: forward, backward, clip + Adam.  Returns the device tensor
-        [kld_loss, recon_loss, loss] (no host synchronisation)."""
+    # ------------------------------------------------------------------ input normalisation
+    def normalise(self, x, lens, norm, epoch=0):
+        """The recipe's InputNormalization(norm_type='global') (SpeechBrain, un-vendored; built at
+        ref:src/models/test_vanilla_vae/model.yaml:14-15, called at
+        ref:src/models/test_vanilla_vae/model.py:24-25) on the device, as the first launches of
+        the step (csrc/norm.hip): per-utterance statistics, the global running statistics
+        updated in place in `norm` (a brain.features.InputNormalization: its glob_mean /
+        glob_std buffers and host-side count, with that module's semantics), then
+        (x - mean) / std into an engine buffer.  Under data parallelism the batch statistics
+        are all-reduced in training, as the module does.  Returns the normalised [B, T, F]."""
+        B, T, F = x.shape
+        l, s = lib(), self._stream()
+        if not l.mlvae_norm_supported(F):
+            raise ValueError(f"input normalisation kernels need F % 4 == 0 (F={F})")
+        x = x.contiguous()
+        if x.data_ptr() % 16:
+            x = x.clone()
+        lens = lens.to(device=self.device, dtype=torch.float32).contiguous()
+        utt = self._pool("norm_utt", (B, 2 * F))
+        sums = self._pool("norm_sums", (2 * F + 4,))
+        out = self._pool("norm_x", (B, T, F))
+        with self._timed("norm"):
+            check(l.mlvae_norm_stats(B, T, F, _p(x), _p(lens), _p(utt), _p(sums), float(norm.eps), s),
+                  "norm_stats")
+            if norm.training and self.world > 1:
+                from . import dist as mdist
+                mdist.allreduce_loss(sums[:2 * F + 1], self.process_group)   # sum over ranks
+            gm, gs = norm.glob_mean, norm.glob_std
+            fresh = gm.numel() == 0
+            if fresh:
+                gm = torch.zeros(F, device=self.device)
+                gs = torch.zeros(F, device=self.device)
+            elif gm.device != self.device or gm.dtype != torch.float32 or not gm.is_contiguous() \
+                    or gm.data_ptr() % 16 or gs.data_ptr() % 16:
+                gm = gm.to(self.device, torch.float32).contiguous().clone()
+                gs = gs.to(self.device, torch.float32).contiguous().clone()
+            norm.glob_mean, norm.glob_std = gm, gs
+            mode, w_old, w_new = (1 if fresh else 0), 0.0, 0.0
+            if norm.training:
+                if norm.count == 0:
+                    mode = 1
+                elif epoch < norm.update_until_epoch:
+                    wt = norm.avg_factor if norm.avg_factor is not None else 1.0 / (norm.count + 1)
+                    mode, w_old, w_new = 2, 1 - wt, wt
+                norm.count += 1
+            check(l.mlvae_norm_update(F, _p(sums), _p(gm), _p(gs), mode, w_old, w_new, s), "norm_update")
+            check(l.mlvae_norm_apply(B * T, F, _p(x), _p(gm), _p(gs), _p(out), s), "norm_apply")
+        return out
+
+    def train_step(self, x, lens, eps=None, dropout_masks=None, normalizer=None, epoch=0):
+        """One fit_batch: [input normalisation,] forward, backward, clip + Adam.  Returns the
+        device tensor [kld_loss, recon_loss, loss] (no host synchronisation).  normalizer: the
+        recipe's InputNormalization (brain.features), run on the device inside the step."""
         with self._main():
+            if normalizer is not None:
+                x = self.normalise(x, lens, normalizer, epoch)
             w = self.forward(x, lens, eps=eps, train=True, dropout_masks=dropout_masks)
             self.backward(w)
             self.optimizer_step(w)
         self.rng_step += 1
         return w.loss
 
-    def eval_step(self, x, lens, eps=None):
+    def eval_step(self, x, lens, eps=None, normalizer=None, epoch=0):
         """Forward only; under data parallelism the returned [kld, recon, loss] is the global
         batch's (each rank's share uses the all-reduced frame count; the shares are summed)."""
         with self._main():
+            if normalizer is not None:
+                x = self.normalise(x, lens, normalizer, epoch)
             w = self.forward(x, lens, eps=eps, train=False)
             if self.world > 1:
                 from . import dist as mdist

@@ -389,10 +389,22 @@ class LSTMFn(torch.autograd.Function):
                 seeds.append(None)
         ctx.save_for_backward(*inputs, *saved, *weights)
         ctx.H, ctx.L, ctx.ndir, ctx.dropout, ctx.seeds = H, L, ndir, dropout, seeds
-        return h
+        # nn.LSTM's (h_n, c_n) [L*ndir, B, H]: every layer's state after its last step (t = T-1
+        # forward, t = 0 reverse; no packing, as nn.LSTM on a padded batch)
+        hn = torch.empty(L * ndir, B, H, device=x.device, dtype=torch.float32)
+        cn = torch.empty_like(hn)
+        for li in range(L):
+            G_, Cs_, Y_ = saved[3 * li:3 * li + 3]
+            Cv = Cs_.view(B, T, H * ndir)
+            for d in range(ndir):
+                t_last = 0 if d else T - 1
+                hn[li * ndir + d] = Y_[:, t_last, d * H:(d + 1) * H]
+                cn[li * ndir + d] = Cv[:, t_last, d * H:(d + 1) * H]
+        ctx.mark_non_differentiable(hn, cn)
+        return h, hn, cn
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dhn=None, _dcn=None):
         H, L, ndir = ctx.H, ctx.L, ctx.ndir
         nw, GL = 4 * ndir, 4 * H * ndir
         t = ctx.saved_tensors
@@ -453,7 +465,23 @@ def lstm(x, lstm_module, train):
                 weights.append(getattr(lstm_module, f"{kind}_l{li}{sfx}"))
     p = float(lstm_module.dropout) if train else 0.0
     seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
-    return LSTMFn.apply(x, H, L, ndir, p, seed, *weights)
+    return LSTMFn.apply(x, H, L, ndir, p, seed, *weights)[0]
+
+
+def lstm_full(x, lstm_module, train, seed=None):
+    """nn.LSTM's whole forward on the HIP recurrence: (output, (h_n, c_n)).  seed: the
+    inter-layer dropout's Philox key (drawn from torch's generator when None)."""
+    if not lstm_module.batch_first:
+        raise ValueError("the HIP LSTM path is batch_first only (as every reference LSTM)")
+    H, L = lstm_module.hidden_size, lstm_module.num_layers
+    ndir = 2 if lstm_module.bidirectional else 1
+    weights = [getattr(lstm_module, f"{kind}_l{li}{sfx}") for li in range(L)
+               for sfx in ("", "_reverse")[:ndir] for kind in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
+    p = float(lstm_module.dropout) if train else 0.0
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+    out, hn, cn = LSTMFn.apply(x, H, L, ndir, p, seed, *weights)
+    return out, (hn, cn)
 
 
 def bilstm(x, lstm_module, train):

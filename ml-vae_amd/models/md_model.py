@@ -129,8 +129,9 @@ class MDModel(Brain):
     # ------------------------------------------------------------------ batches
     def fit_batch(self, batch):
         if self.engine is not None:
-            feats, lens = self._normalised_feats(batch, Stage.TRAIN)
-            loss = self.engine.train_step(feats, lens)
+            feats, lens, norm = self._engine_inputs(batch)
+            loss = self.engine.train_step(feats, lens, normalizer=norm,
+                                          epoch=self.hparams.epoch_counter.current)
             self._log_losses(loss)
             self.optimizer_step += 1
             return loss[2].detach()
@@ -186,11 +187,27 @@ class MDModel(Brain):
 
     def evaluate_batch(self, batch, stage):
         if self.engine is not None:
-            feats, lens = self._normalised_feats(batch, stage)
-            loss = self.engine.eval_step(feats, lens)
+            feats, lens, norm = self._engine_inputs(batch)
+            loss = self.engine.eval_step(feats, lens, normalizer=norm,
+                                         epoch=self.hparams.epoch_counter.current)
             self._log_losses(loss)
             return loss[2].detach()
         return super().evaluate_batch(batch, stage)
+
+    def _engine_inputs(self, batch):
+        """(feats, lens, normaliser) for the fused step: the recipe's InputNormalization
+        (brain.features) runs inside the step on the device (csrc/norm.hip) with the module's
+        own state and semantics; any other normaliser object is applied here first."""
+        from brain.features import InputNormalization
+        from mlvae_hip._lib import lib
+        batch = batch.to(self.device)
+        feats, lens = batch["feat"]
+        norm = getattr(self.hparams, "normalizer", None)
+        if isinstance(norm, InputNormalization) and lib().mlvae_norm_supported(feats.shape[-1]):
+            return feats.contiguous(), lens, norm
+        if norm is not None:
+            feats = norm(feats, lens, epoch=self.hparams.epoch_counter.current)
+        return feats.contiguous(), lens, None
 
     def _normalised_feats(self, batch, stage):
         batch = batch.to(self.device)

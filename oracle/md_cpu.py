@@ -28,13 +28,17 @@ EPS_V = 1e-5                  # ref:src/modules/boundary_detector.py:66-67
 N_SAMPLES = 10                # ref:src/modules/boundary_detector.py:55
 
 
-def uni_lstm(p, x, L, prefix="rnn."):
-    """Unidirectional L-layer nn.LSTM, batch_first, h0 = c0 = 0, no dropout
-    (ref:src/modules/phoneme_recognizer.py:13; boundary_detector.py:19)."""
+def uni_lstm(p, x, L, prefix="rnn.", dropout_masks=None):
+    """Unidirectional L-layer nn.LSTM, batch_first, h0 = c0 = 0
+    (ref:src/modules/phoneme_recognizer.py:13; boundary_detector.py:19; the MD-VAE's 512-unit
+    rnn ref:src/models/MD_VAE/model.yaml:78-83).  dropout_masks[l] (scaled keep masks of layer
+    l's output, l < L-1): nn.LSTM's train-mode inter-layer dropout with injected masks."""
     h = x
     for li in range(L):
         h = lstm_direction_loop(h, p[f"{prefix}weight_ih_l{li}"], p[f"{prefix}weight_hh_l{li}"],
                                 p[f"{prefix}bias_ih_l{li}"], p[f"{prefix}bias_hh_l{li}"], False)
+        if dropout_masks is not None and li < L - 1:
+            h = h * dropout_masks[li]
     return h
 
 

@@ -139,3 +139,38 @@ def test_gate_buffer_format_is_checked():
     assert l.mlvae_lstm_fwd_ex2(1, 8, T, H2, P(W2), P(W2), P(G32), 0, P(Cs2), None, None, None, 0, 0, 0.0,
                                 P(xbuf), xb.value, P(err), stream()) != 0
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("B,T", [(256, 40, ), (200, 23), (32, 37), (48, 11)])
+def test_interleaved_forward_is_bit_identical(B, T):
+    """lstm_fwd_il_kernel (two batch groups per workgroup, debug bit 22) computes every unit with
+    the same MFMA sequence and cell arithmetic as the one-group kernel: every output -- saved
+    gates, c, h (fp32 / bf16) and the fused dropout(h) -- is bit-identical, including a padded
+    (fully invalid) group at odd group counts (B = 200, 48)."""
+    need_gpu()
+    w, gx, *_ = _reference(B, T, 7 * B + T)
+    N = B * T
+    W0, W1 = w[0].float().cuda(), w[1].float().cuda()
+    seed, doff, p = 0xD0 + B, 8 * 2 * H, 0.15
+    outs = []
+    for mode in (0, 1 << 22):
+        lib().mlvae_lstm_set_debug_mode(mode)
+        try:
+            G = gx.reshape(N, 8 * H).to(torch.float16).cuda().contiguous()
+            Cs = torch.zeros(N, 2 * H, device="cuda")
+            Y = torch.zeros(N, 2 * H, device="cuda")
+            Yb = torch.zeros(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+            Ydb = torch.zeros(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+            xb = ctypes.c_size_t()
+            check(lib().mlvae_lstm_workspace_size(B, H, 1, ctypes.byref(xb)))
+            xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
+            err = torch.zeros(1, device="cuda", dtype=torch.int32)
+            check(lib().mlvae_lstm_fwd_ex2(1, B, T, H, P(W0), P(W1), P(G), 1, P(Cs), P(Y), Yb.data_ptr(),
+                                           Ydb.data_ptr(), seed, doff, p, P(xbuf), xb.value, P(err), stream()))
+            torch.cuda.synchronize()
+            assert err.item() == 0, mode
+            outs.append((G, Cs, Y, Yb, Ydb))
+        finally:
+            lib().mlvae_lstm_set_debug_mode(0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
