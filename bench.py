@@ -327,11 +327,16 @@ def extra_runs(args, device):
                                                     ("conv_fwd_layer", "conv_dgrad", "conv_wgrad")}
             else:
                 sec = secondary(kern, B, T, cname)
-                if cname in FP8 and "proj_l1" in sec:  # against the fp8 (block-scaled) MFMA peak
-                    sec["proj_l1"].update(what="layer-1 input projection on fp8 e4m3 operands (incl. the "
-                                               "x / W_ih casts)", peak=MFMA_PEAK_TFLOPS["fp8"])
-                    sec["proj_l1"]["frac"] = sec["proj_l1"]["achieved"] / MFMA_PEAK_TFLOPS["fp8"]
-                out[key]["kernels"] = {k: v for k, v in sec.items() if k == "proj_l1"}
+                if cname in FP8:  # against the fp8 (block-scaled) MFMA peak
+                    what = {"proj_l1": "layer-1 input projection on fp8 e4m3 operands (incl. the W_ih "
+                                       "scale + casts; the input arrives as e4m3 from the recurrence)",
+                            "dgrad_l1": "layer-1 dgrad on fp8 e4m3 operands (dG from the BPTT, delayed "
+                                        "scaling) + dropout bwd"}
+                    for kk in ("proj_l1", "dgrad_l1"):
+                        if kk in sec:
+                            sec[kk].update(what=what[kk], peak=MFMA_PEAK_TFLOPS["fp8"])
+                            sec[kk]["frac"] = sec[kk]["achieved"] / MFMA_PEAK_TFLOPS["fp8"]
+                out[key]["kernels"] = {k: v for k, v in sec.items() if k in ("proj_l1", "dgrad_l1")}
                 out[key]["fp8"] = cname in FP8
             out[key]["kernel_ms"] = kern
         del eng, x

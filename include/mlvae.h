@@ -152,6 +152,20 @@ int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, con
                        void* gates, int gates_fp16, const float* cells, const float* dy,
                        void* dg_bf16, float* dbias_rows, void* xbuf, size_t xbytes, int* err,
                        void* stream);
+/* fp8 mode (BASELINE.json configs[4]) of the wide-batch recurrences (gates_fp16 shapes, bf16):
+ *   fwd: as mlvae_lstm_fwd_ex2 without the fp32 h, plus y_drop_fp8 = e4m3(dropout(h) * x8_scale):
+ *        the next layer's fp8 input-projection operand, written by the recurrence itself
+ *        (replaces a cast pass over the bf16 copy; ref:src/modules/decoder.py:14-15,22)
+ *   bwd: as mlvae_lstm_bwd_ex2, plus dg_fp8 = e4m3(dG * *dg8_scale) (NULL: none) -- the fp8
+ *        dgrad's operand under delayed scaling -- and max |dG| max-ed into *dg_amax (float bits) */
+int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
+                       float* cells, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
+                       unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                       void* xbuf, size_t xbytes, int* err, void* stream);
+int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
+                       const float* cells, const float* dy, void* dg_bf16, float* dbias_rows,
+                       void* dg_fp8, const float* dg8_scale, unsigned* dg_amax, void* xbuf,
+                       size_t xbytes, int* err, void* stream);
 /* Workgroups (one per CU, co-resident) of the recurrence launch for this shape as the engine
  * runs it (fp16 gates where mlvae_lstm_gates_fp16): the wide kernels fill the chip. */
 int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd);
@@ -206,11 +220,23 @@ int mlvae_viterbi_md(int B, int T, int N, int L, const float* logits, int ldl, c
  *   cast_fp8:  dst = e4m3(clamp(src * scale, +-448)), RNE; scale = *scale_p if non-null. */
 int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
                    const float* alpha, const float* bias1, const float* bias2, int epi, void* stream);
+/* As mlvae_gemm_fp8 with epi = EPI_DROPOUT allowed (fp32 C): C *= the inter-layer dropout mask of
+ * element drop_offset + row * ldc + col -- the fp8 layer-1 dgrad with the dropout backward fused
+ * (ref:src/modules/decoder.py:14-15: the dropout between the LSTM layers). */
+int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C,
+                      int ldc, const float* alpha, const float* bias1, const float* bias2, int epi,
+                      unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                      void* stream);
 size_t mlvae_fp8_scale_workspace_size(void);
 int mlvae_fp8_scale(size_t n, const float* x, float other_scale, float* out, float* ws, size_t ws_bytes,
                     void* stream);
 int mlvae_cast_fp8(size_t n, const void* src, int src_bf16, const float* scale_p, float scale, void* dst,
                    void* stream);
+/* Delayed (previous-step) scaling: from an amax word a producer max-ed (float bits),
+ * out[0] = q = 448 / (margin * amax_prev) (1 without a usable amax), out[1] = 1 / (q * *other_q)
+ * (the fp8 GEMM's alpha); *amax_next (distinct word, optional) is cleared for this step's producer. */
+int mlvae_fp8_delayed_scale(const unsigned* amax_prev, unsigned* amax_next, const float* other_q,
+                            float margin, float* out, void* stream);
 
 /* Conv1d encoder layers (csrc/conv.hip), BASELINE.json configs[3]'s "Conv1d encoder variant":
  * the reference has none (SURVEY.md Appendix A); semantics = torch.nn.Conv1d(Cin, Cout, K,

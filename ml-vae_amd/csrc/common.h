@@ -144,3 +144,16 @@ __device__ __forceinline__ float dropout_scale(unsigned long long seed, unsigned
   const unsigned w = (i & 2) ? ((i & 1) ? r[3] : r[2]) : ((i & 1) ? r[1] : r[0]);
   return dropout_word_scale(w, keep, scale);
 }
+
+// ---- fp8 e4m3 (OCP, gfx950's native format): saturating pack of four floats, round to nearest
+// even (v_cvt_pk_fp8_f32).  Shared by the casts (fp8.hip) and the recurrences' fused fp8 outputs.
+constexpr float E4M3_MAX = 448.f;
+__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -E4M3_MAX), E4M3_MAX);
+  b = fminf(fmaxf(b, -E4M3_MAX), E4M3_MAX);
+  c = fminf(fmaxf(c, -E4M3_MAX), E4M3_MAX);
+  d = fminf(fmaxf(d, -E4M3_MAX), E4M3_MAX);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (unsigned)w;
+}

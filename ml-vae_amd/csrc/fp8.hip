@@ -14,7 +14,6 @@ namespace {
 
 constexpr int RB = 256;          // threads
 constexpr int RBLOCKS = 512;     // first-pass blocks
-constexpr float E4M3_MAX = 448.f;
 
 __global__ __launch_bounds__(RB) void amax_partial_kernel(size_t n, const float* x, float* part) {
   float m = 0.f;
@@ -51,16 +50,6 @@ __global__ __launch_bounds__(RB) void amax_final_kernel(int np, const float* par
   }
 }
 
-__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
-  a = fminf(fmaxf(a, -E4M3_MAX), E4M3_MAX);
-  b = fminf(fmaxf(b, -E4M3_MAX), E4M3_MAX);
-  c = fminf(fmaxf(c, -E4M3_MAX), E4M3_MAX);
-  d = fminf(fmaxf(d, -E4M3_MAX), E4M3_MAX);
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-  return (unsigned)w;
-}
-
 template <bool BF>
 __global__ __launch_bounds__(RB) void cast_fp8_kernel(size_t n8, const void* src, const float* scale_p, float scale,
                                                        u32x2* dst) {
@@ -80,6 +69,19 @@ __global__ __launch_bounds__(RB) void cast_fp8_kernel(size_t n8, const void* src
     }
     dst[i] = u32x2{pack4_fp8(v[0] * s, v[1] * s, v[2] * s, v[3] * s), pack4_fp8(v[4] * s, v[5] * s, v[6] * s, v[7] * s)};
   }
+}
+
+// delayed (previous-step) scaling of an operand whose amax a producer kernel max-ed into a word
+// as float bits: q = 448 / (margin * amax_prev), 1 without a usable amax; out[1] = the GEMM's
+// alpha 1 / (q * other_q); the next step's amax word is cleared for its producer
+__global__ void delayed_scale_kernel(const unsigned* amax_prev, unsigned* amax_next, const float* other_q,
+                                     float margin, float* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  const float am = __uint_as_float(*amax_prev) * margin;
+  const float q = (am > 0.f && am < INFINITY) ? E4M3_MAX / am : 1.f;
+  out[0] = q;
+  out[1] = 1.f / (q * *other_q);
+  if (amax_next) *amax_next = 0u;
 }
 
 int grid_for(size_t n) {
@@ -121,6 +123,18 @@ extern "C" int mlvae_cast_fp8(size_t n, const void* src, int src_bf16, const flo
   else
     hipLaunchKernelGGL(cast_fp8_kernel<false>, dim3(grid_for(n8)), dim3(RB), 0, s, n8, src, scale_p, scale,
                        static_cast<u32x2*>(dst));
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mlvae_fp8_delayed_scale(const unsigned* amax_prev, unsigned* amax_next, const float* other_q,
+                                       float margin, float* out, void* stream) {
+  if (!amax_prev || !other_q || !out || !(margin >= 1.f) || amax_prev == amax_next) {
+    mlvae_set_error("mlvae_fp8_delayed_scale: amax words (distinct), other scale, out, margin >= 1");
+    return 1;
+  }
+  hipLaunchKernelGGL(delayed_scale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amax_prev, amax_next,
+                     other_q, margin, out);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -741,8 +741,22 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
 
 // C[M,N] (fp32, or fp16 with EPI_OUT_F16) = (*alpha) * A . B^T + bias1 + bias2 over fp8 e4m3 (OCP)
 // operands A [M][K], B [N][K] (k-contiguous, leading dims in elements).  gemm256_kernel VAR 8.
+extern "C" int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C,
+                                 int ldc, const float* alpha, const float* bias1, const float* bias2, int epi,
+                                 unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                                 void* stream);
+
 extern "C" int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
                               const float* alpha, const float* bias1, const float* bias2, int epi, void* stream) {
+  return mlvae_gemm_fp8_ex(M, N, K, A, lda, B, ldb, C, ldc, alpha, bias1, bias2, epi, 0ull, 0ull, 0.f, stream);
+}
+
+// epi: EPI_NONE or EPI_DROPOUT (the inter-layer dropout's backward: C *= mask of element
+// drop_offset + row * ldc + col, the Philox mask of the forward), optionally | EPI_OUT_F16
+extern "C" int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C,
+                                 int ldc, const float* alpha, const float* bias1, const float* bias2, int epi,
+                                 unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                                 void* stream) {
   if (M < 0 || N < 0 || K < 0 || !C || (K > 0 && (!A || !B))) {
     mlvae_set_error("mlvae_gemm_fp8: bad shape/ptr");
     return 1;
@@ -750,9 +764,9 @@ extern "C" int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const
   if (M == 0 || N == 0) return 0;
   const int c16 = (epi & EPI_OUT_F16) ? 1 : 0;
   epi &= ~EPI_OUT_F16;
-  if (epi != EPI_NONE || N % 4 || ldc % 4 || ((uintptr_t)C % 16) || ((uintptr_t)bias1 % 16) ||
-      ((uintptr_t)bias2 % 16)) {
-    mlvae_set_error("mlvae_gemm_fp8: epilogue none (+ fp16 C), N and ldc %% 4, aligned C / bias");
+  if ((epi != EPI_NONE && epi != EPI_DROPOUT) || N % 4 || ldc % 4 || ((uintptr_t)C % 16) ||
+      ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16) || (epi == EPI_DROPOUT && (c16 || !(drop_p >= 0.f && drop_p < 1.f)))) {
+    mlvae_set_error("mlvae_gemm_fp8: epilogue none (+ fp16 C) or dropout (fp32 C), N and ldc %% 4, aligned C / bias");
     return 1;
   }
   if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || (lda % 16) || (ldb % 16) || (K % 16)) {
@@ -769,9 +783,10 @@ extern "C" int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const
   g.A = static_cast<const short*>(A); g.lda = lda / 2; g.a_bs = 0;
   g.B = static_cast<const short*>(B); g.ldb = ldb / 2; g.b_bs = 0;
   g.C = static_cast<float*>(C); g.ldc = ldc; g.c_bs = 0; g.beta = 0.f;
-  g.bias1 = bias1; g.bias2 = bias2; g.epi = EPI_NONE; g.aux = nullptr; g.ldaux = 0;
+  g.bias1 = bias1; g.bias2 = bias2; g.epi = epi; g.aux = nullptr; g.ldaux = 0;
   g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
-  g.dseed = 0; g.doff = 0; g.dkeep = 1.f; g.dscale = 1.f;
+  g.dseed = drop_seed; g.doff = drop_offset; g.dkeep = 1.f - drop_p;
+  g.dscale = drop_p < 1.f ? 1.f / (1.f - drop_p) : 0.f;
   g.ws = nullptr; g.alpha = alpha; g.abl = 0;
   g.splits = 1; g.kchunk = ((g.K + TBK - 1) / TBK) * TBK;
   if (g.K == 0) g.kchunk = TBK;

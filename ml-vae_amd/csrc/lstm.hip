@@ -951,6 +951,7 @@ struct WideExtra {  // outputs only the wide kernels write
   float* dbias = nullptr;         // backward: per batch group bias-gradient rows
   unsigned long long seed = 0, off = 0;
   float p = 0.f;
+  WideFp8 f8;                     // fp8 mode: e4m3 dropout(h) / dG copies, dG amax
 };
 
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
@@ -972,7 +973,7 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     if (!fwd && !dgb) { mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 (NULL)"); return 1; }
     if (ex.ydb && !(ex.p >= 0.f && ex.p < 1.f)) { mlvae_set_error("lstm: dropout p=%g", ex.p); return 1; }
     return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.dbias, ex.ydb,
-                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode);
+                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode, ex.f8);
   }
   if (ex.ydb || ex.dbias || !Y) {
     mlvae_set_error("lstm: fused dropout / bias-gradient outputs, Y = NULL only on the wide-batch path");
@@ -1072,6 +1073,44 @@ extern "C" int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_
   return run(true, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, y, xbuf,
              xbytes, err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr,
              gates_fp16, ex);
+}
+
+// fp8 mode (configs[4]) of the wide kernels: the forward also writes dropout(h) * x8_scale as
+// e4m3 (the next layer's fp8 projection operand); the backward also writes dG * (*dg8_scale) as
+// e4m3 (the fp8 dgrad's operand; NULL: amax only) and max-es max |dG| into *dg_amax (float bits)
+extern "C" int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                  void* gates, float* cells, void* y_bf16, void* y_drop_bf16,
+                                  void* y_drop_fp8, float x8_scale, unsigned long long drop_seed,
+                                  unsigned long long drop_offset, float drop_p, void* xbuf,
+                                  size_t xbytes, int* err, void* stream) {
+  if (!use_wide(B, H, PREC_BF16) || !y_drop_fp8 || !y_drop_bf16 || !(x8_scale > 0.f)) {
+    mlvae_set_error("lstm_fwd_fp8: wide-batch shapes with a dropout output and a positive scale only");
+    return 1;
+  }
+  WideExtra ex;
+  ex.ydb = static_cast<unsigned short*>(y_drop_bf16);
+  ex.seed = drop_seed; ex.off = drop_offset; ex.p = drop_p;
+  ex.f8.y8 = static_cast<unsigned char*>(y_drop_fp8);
+  ex.f8.x8scale = x8_scale;
+  return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, nullptr,
+             xbuf, xbytes, err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
+}
+extern "C" int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                  void* gates, const float* cells, const float* dy, void* dg_bf16,
+                                  float* dbias_rows, void* dg_fp8, const float* dg8_scale,
+                                  unsigned* dg_amax, void* xbuf, size_t xbytes, int* err, void* stream) {
+  if (!use_wide(B, H, PREC_BF16) || !dg_amax || (dg_fp8 && !dg8_scale)) {
+    mlvae_set_error("lstm_bwd_fp8: wide-batch shapes; the amax word, and a scale with the fp8 copy");
+    return 1;
+  }
+  WideExtra ex;
+  ex.dbias = dbias_rows;
+  ex.f8.dg8 = static_cast<unsigned char*>(dg_fp8);
+  ex.f8.g8scale = dg8_scale;
+  ex.f8.g8amax = dg_amax;
+  return run(false, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
+             const_cast<float*>(cells), const_cast<float*>(dy), xbuf, xbytes, err,
+             (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), 1, ex);
 }
 
 extern "C" int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd,

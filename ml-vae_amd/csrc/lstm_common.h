@@ -39,6 +39,15 @@ struct LstmArgs {
   unsigned short* Ydb;
   unsigned long long dseed, doff;
   float dkeep, dscale;
+  // fp8 mode (configs[4]), wide kernels, optional: the forward's e4m3 copy of dropout(h) scaled
+  // by x8scale (the next layer's fp8 projection operand); the BPTT's e4m3 copy of dG scaled by
+  // *g8scale (delayed scaling: from the previous step's amax) and this launch's max |dG|
+  // atomically max-ed into *g8amax as float bits (g8amax alone: amax only)
+  unsigned char* Y8;
+  float x8scale;
+  unsigned char* dG8;
+  const float* g8scale;
+  unsigned* g8amax;
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -112,11 +121,18 @@ __device__ __forceinline__ bool tags_ok(u32x4 v, unsigned tag, bool g0, bool g1)
 // Wide-batch recurrences (lstm_wide.hip): one launch covers every utterance of a layer when
 // the batch-group kernels would need several chunks.  Return -1 when the shape is not
 // supported (the caller then falls back to chunked batch-group launches), else a status.
+struct WideFp8 {  // the fp8 mode's fused outputs of the wide kernels (LstmArgs fields)
+  unsigned char* y8 = nullptr;
+  float x8scale = 0.f;
+  unsigned char* dg8 = nullptr;
+  const float* g8scale = nullptr;
+  unsigned* g8amax = nullptr;
+};
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
-                  unsigned long long* dbg, int dbg_mode);
+                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8 = WideFp8());
 // debug-mode bits the wide plans read (bit 21: one workgroup per CU, no two-per-CU plan)
 void lstm_wide_set_mode(int mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply

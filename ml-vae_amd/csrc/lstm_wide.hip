@@ -211,6 +211,12 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         *reinterpret_cast<bf16x8*>((drop8 ? a.Ydb : a.Yb) + o) =
             bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
                    f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+        if (drop8 && a.Y8) {  // fp8 mode: the next layer's e4m3 projection operand, fixed scale
+          const float xs = a.x8scale;
+          *reinterpret_cast<u32x2*>(a.Y8 + o) =
+              u32x2{pack4_fp8(v0[0] * xs, v0[1] * xs, v0[2] * xs, v0[3] * xs),
+                    pack4_fp8(v1[0] * xs, v1[1] * xs, v1[2] * xs, v1[3] * xs)};
+        }
       }
     }
   };
@@ -331,8 +337,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       STAMP(4);
       // Behind the publish, off the hand-off's path: the io waves store step s-1's saved
       // activations (right after the barrier they delayed the io waves' own publish: 4.2 vs
-      // 3.7 us/step at B = 256); every wave puts step s's into the out ring (gates as fp16);
-      // the pollers draw step s's dropout bits before polling for step s+1.
+      // 3.7 us/step at B = 256); every wave puts step s's into the out ring (gates as fp16).
       if (IO && s > 0) io_store(s - 1);
       unsigned short* og = reinterpret_cast<unsigned short*>(ob);
       float* of = reinterpret_cast<float*>(ob + 8 * HJ);
@@ -343,6 +348,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
         of[u] = c[t]; of[HJ + u] = hvals[t];
       }
+      // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
+      // waves 4-5 instead, they held the barrier: 1.38 vs 1.33 ms per forward launch at c3)
       if (!IO && a.Ydb && tid < NC8) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
     }
     __syncthreads();
@@ -653,7 +660,9 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------------------
 // backward (BPTT), reduce-scatter form
 // ---------------------------------------------------------------------------------------
-template <int TPW, int NKC, int OCC>  // HJ = 32 * TPW units per workgroup, H = 32 * NKC; OCC as fwd
+// F8: the fp8 mode's e4m3 dG copy + amax (a separate instantiation: the bf16 path's registers
+// stay as they are)
+template <int TPW, int NKC, int OCC, bool F8 = false>  // HJ = 32 * TPW, H = 32 * NKC; OCC as fwd
 __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = 32 * TPW;
   constexpr int H = NKC * 32;
@@ -800,6 +809,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   stage_cell(0);   // (waits for the loads: prologue only)
   load_cell(1);
   __syncthreads();
+  float g8max = 0.f;                                        // fp8 mode: running max |dG|
+  const float g8s = (F8 && a.dG8) ? *a.g8scale : 0.f;       // fp8 mode: this step's dG scale
 
   auto step = [&](int s) -> bool {
     STAMP(0);
@@ -943,6 +954,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     }
     STAMP(4);
     // dG of this step for the weight-gradient GEMMs: 16-byte rows out of the A-image
+    // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|)
     if (!(a.dbg_mode & 1)) {
       constexpr int NSL = 16 * 4 * HJ / 8;  // 16-byte slots
       const int t = dir ? s : T - 1 - s;
@@ -954,12 +966,32 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(ab + r * ROWB + swz(r, kslot) * 16);
         const size_t o = ((size_t)b * T + t) * 8 * H + dir * 4 * H + g * H + j0 + u;
         *reinterpret_cast<u32x4*>(a.dGb + o) = v;  // G is fp16 here: dG always goes to dGb
+        if constexpr (F8) {
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[2 * e] = __uint_as_float(v[e] << 16);
+            f[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g8max = fmaxf(g8max, fabsf(f[e]));
+          if (a.dG8)
+            *reinterpret_cast<u32x2*>(a.dG8 + o) =
+                u32x2{pack4_fp8(f[0] * g8s, f[1] * g8s, f[2] * g8s, f[3] * g8s),
+                      pack4_fp8(f[4] * g8s, f[5] * g8s, f[6] * g8s, f[7] * g8s)};
+        }
       }
     }
     return true;
   };
   for (int s = 0; s < T; ++s)
     if (!step(s)) break;
+  if constexpr (F8) {  // this launch's max |dG| (the next step's fp8 scale): one atomic per wave
+    float m = g8max;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) atomicMax(a.g8amax, __float_as_uint(m));  // |x| >= 0: float order = uint order
+  }
   // bias gradients of this workgroup's units: the lane sums over its steps, then over the
   // group's 16 utterances (8 lanes x CPG halves; fixed order), one row per batch group
   if (a.dbias) {
@@ -1075,7 +1107,8 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC> : lstm_bwd_wide_kernel<TPW, NKC, OCC>;
+  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC>
+               : (a.g8amax ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true> : lstm_bwd_wide_kernel<TPW, NKC, OCC, false>);
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
     mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
     return 2;
@@ -1117,7 +1150,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
-                  unsigned long long* dbg, int dbg_mode) {
+                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return -1;
   if (!xbuf || xbytes < p.xbytes || !err) {
@@ -1130,6 +1163,15 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.W0 = W0; a.W1 = W1; a.G = G; a.Cs = Cs; a.Y = Y; a.xbuf = xbuf; a.err = err;
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;
   a.dbias = dbias; a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
+  a.Y8 = f8.y8; a.x8scale = f8.x8scale; a.dG8 = f8.dg8; a.g8scale = f8.g8scale; a.g8amax = f8.g8amax;
+  if (a.Y8 && (!ydb || p.il)) {
+    mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one (one-group forward)");
+    return 1;
+  }
+  if (a.dG8 && (!a.g8scale || !a.g8amax)) {
+    mlvae_set_error("lstm_wide: the fp8 dG copy needs its scale and amax words");
+    return 1;
+  }
   a.dscale = dp < 1.f ? 1.f / (1.f - dp) : 0.f;
   a.xtab = reinterpret_cast<unsigned*>(static_cast<char*>(xbuf) + p.xtab_off);
   // zero fill = a stale tag in every granule (and an empty placement table)

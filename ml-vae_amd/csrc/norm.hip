@@ -39,10 +39,19 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(int T, int F, const floa
   const int n = norm_frames(lens[b], T);
   const f32x4* xb = reinterpret_cast<const f32x4*>(x + (size_t)b * T * F);
   const bool act = rl < RL;
+  // four independent rows in flight per thread (a dependent load per row would make the
+  // pass latency-bound: ~40 HBM round trips per thread at T = 500)
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (act)
-    for (int r = rl; r < n; r += RL) s += xb[(size_t)r * FQ + q];
-  if (act) red[rl * FQ + q] = s;
+  if (act) {
+    int r = rl;
+    for (; r + 3 * RL < n; r += 4 * RL) {
+      const f32x4 a0 = xb[(size_t)r * FQ + q], a1 = xb[(size_t)(r + RL) * FQ + q];
+      const f32x4 a2 = xb[(size_t)(r + 2 * RL) * FQ + q], a3 = xb[(size_t)(r + 3 * RL) * FQ + q];
+      s += a0; s += a1; s += a2; s += a3;
+    }
+    for (; r < n; r += RL) s += xb[(size_t)r * FQ + q];
+    red[rl * FQ + q] = s;
+  }
   __syncthreads();
   f32x4 mean = {0.f, 0.f, 0.f, 0.f};
   if (n > 0) {
@@ -52,12 +61,19 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(int T, int F, const floa
   }
   __syncthreads();
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (act)
-    for (int r = rl; r < n; r += RL) {
+  if (act) {
+    int r = rl;
+    for (; r + 3 * RL < n; r += 4 * RL) {
+      const f32x4 d0 = xb[(size_t)r * FQ + q] - mean, d1 = xb[(size_t)(r + RL) * FQ + q] - mean;
+      const f32x4 d2 = xb[(size_t)(r + 2 * RL) * FQ + q] - mean, d3 = xb[(size_t)(r + 3 * RL) * FQ + q] - mean;
+      v += d0 * d0; v += d1 * d1; v += d2 * d2; v += d3 * d3;
+    }
+    for (; r < n; r += RL) {
       const f32x4 d = xb[(size_t)r * FQ + q] - mean;
       v += d * d;
     }
-  if (act) red[rl * FQ + q] = v;
+    red[rl * FQ + q] = v;
+  }
   __syncthreads();
   if (rl == 0) {
     f32x4 t = red[q];

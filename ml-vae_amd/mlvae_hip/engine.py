@@ -31,7 +31,16 @@ PREC = {"fp32": 0, "bf16": 1}
 LOSS = {"likelihood": 0, "mse": 1}
 EPI_NONE, EPI_LRELU, EPI_DLRELU, EPI_DROPOUT = 0, 1, 2, 3
 EPI_OUT_F16 = 16  # flag: mlvae_gemm_bf16 stores C as fp16
-X8_SCALE = 256.0  # fp8 mode: scale of the layer inputs (|dropout(h)| <= 1/(1-p) -> <= 302 < 448)
+G8_MARGIN = 2.0   # fp8 mode: headroom of the delayed dG scale over the previous step's amax
+
+
+def x8_scale(p):
+    """fp8 mode: the fixed e4m3 scale of a layer input dropout(h): |h| < 1, so |dropout(h)| <=
+    1/(1-p); the largest power of two keeping that under e4m3's 448 (256 at p = 0.15)."""
+    s, lim = 1.0, 448.0 * (1.0 - p)
+    while s * 2.0 <= lim:
+        s *= 2.0
+    return s
 
 
 @dataclass
@@ -70,6 +79,8 @@ class VAEConfig:
             raise ValueError(f"prec must be one of {list(PREC)}")
         if self.fp8 and self.prec != "bf16":
             raise ValueError("fp8 projections run inside the bf16 mode: prec must be 'bf16'")
+        if self.fp8 and not (0.0 <= self.dropout < 0.99):
+            raise ValueError("fp8 mode: the layer-input scale needs dropout p < 0.99")
         if self.enc_conv:
             if self.enc_conv % 2 != 1:
                 raise ValueError("enc_conv: the Conv1d kernel size must be odd")
@@ -226,6 +237,8 @@ class _Work:
         self.ZA = Z + 16 if self.enc_fused else Z
         self.Zb = empty(N, self.ZA, **b16) if self.bf else None  # first layer's GEMM operand
         self.X8 = empty(N, 2 * H, dtype=torch.uint8) if (self.bf and cfg.fp8) else None  # fp8 layer input
+        # fp8 mode: the top layer's e4m3 dG (the fp8 dgrad operand, written by the BPTT)
+        self.dG8 = empty(N, 8 * H, dtype=torch.uint8) if (self.bf and cfg.fp8) else None
         self.E1b = empty(N, E, **b16) if self.enc_fused else None
         self.E2b = empty(N, E, **b16) if self.enc_fused else None
         if self.bf:
@@ -349,6 +362,14 @@ class VAEEngine:
                 self.w8 = {li: torch.empty(8 * cfg.H * 2 * cfg.H, device=self.device, dtype=torch.uint8)
                            for li in range(1, cfg.L)}
                 self.w8s = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
+                # the fp8 dgrad: W_ih^T as e4m3 (scale w8s[li][0]), [q_dG, alpha] from delayed
+                # scaling, and the amax words the BPTT writes (two: this step's / the last step's)
+                self.w8t = {li: torch.empty(2 * cfg.H * 8 * cfg.H, device=self.device, dtype=torch.uint8)
+                            for li in range(1, cfg.L)}
+                self.g8 = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
+                self.g8_amax = {li: torch.zeros(2, device=self.device, dtype=torch.int32) for li in range(1, cfg.L)}
+                self.g8_ready = False  # a previous step's amax exists (the first step's dgrad is bf16)
+                self.g8_par = 0
                 self.f8ws = torch.empty(lib().mlvae_fp8_scale_workspace_size() // 4 + 1, device=self.device)
             if self.fused_encoder:  # dZ = dG W_ih_l0 over its k-contiguous transpose
                 self.wih_t[0] = torch.empty(cfg.Z * 8 * cfg.H, device=self.device, dtype=torch.bfloat16)
@@ -684,13 +705,18 @@ class VAEEngine:
             elif w.bf and cfg.fp8 and li > 0 and din % 16 == 0 and ldx == din:
                 # configs[4]: fp8 e4m3 operands, per-tensor scales (x: the fixed 2^8, |x| <= 1/(1-p);
                 # W_ih: 448 / max|W_ih|), block-scaled MFMA, alpha = 1 / (2^8 q_w) (fp8.hip)
+                xs = x8_scale(cfg.dropout)
                 with self._timed(f"proj_l{li}"):
                     wih = self._ptr(f"decoder.rnn.weight_ih_l{li}")
-                    check(l.mlvae_fp8_scale(8 * H * din, wih, X8_SCALE, _p(self.w8s[li]), _p(self.f8ws),
+                    check(l.mlvae_fp8_scale(8 * H * din, wih, xs, _p(self.w8s[li]), _p(self.f8ws),
                                             self.f8ws.numel() * 4, s), "fp8_scale")
                     check(l.mlvae_cast_fp8(8 * H * din, wih, 0, _p(self.w8s[li]), 0.0, self.w8[li].data_ptr(), s),
                           "cast_fp8")
-                    check(l.mlvae_cast_fp8(N * din, _pb(xin_bf), 1, None, X8_SCALE, w.X8.data_ptr(), s), "cast_fp8")
+                    if train and li in self.wih_t:  # the fp8 dgrad's W_ih^T, same scale
+                        check(l.mlvae_cast_fp8(8 * H * din, _pb(self.wih_t[li]), 1, _p(self.w8s[li]), 0.0,
+                                               self.w8t[li].data_ptr(), s), "cast_fp8")
+                    if not w.__dict__.get("x8_fused", {}).get(li):  # else the recurrence wrote it
+                        check(l.mlvae_cast_fp8(N * din, _pb(xin_bf), 1, None, xs, w.X8.data_ptr(), s), "cast_fp8")
                     check(l.mlvae_gemm_fp8(N, 8 * H, din, w.X8.data_ptr(), din, self.w8[li].data_ptr(), din,
                                            _p(w.G[li]), 8 * H, _p(self.w8s[li], 1),
                                            self._ptr(f"decoder.rnn.bias_ih_l{li}"),
@@ -717,14 +743,24 @@ class VAEEngine:
             need_y = (not w.g16 or (drop and not fuse_drop) or
                       (li == cfg.L - 1 and not (self.fused_heads and w.bf)))
             seed = self._drop_seed(li) if fuse_drop else 0
+            # fp8 mode: the recurrence also writes the next layer's e4m3 input (no cast pass)
+            x8_fused = (cfg.fp8 and fuse_drop and not need_y and w.X8 is not None and 2 * H % 16 == 0)
+            w.__dict__.setdefault("x8_fused", {})[li + 1] = x8_fused
             with self._timed("lstm_fwd"):
-                check(l.mlvae_lstm_fwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                           int(w.g16), _p(w.Cs[li]), _p(w.Y[li]) if need_y else None,
-                                           _pb(w.Yb[li]) if w.bf else None,
-                                           _pb(w.Ydb[li]) if fuse_drop else None, seed, self._drop_off,
-                                           cfg.dropout if fuse_drop else 0.0,
-                                           _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd")
+                if x8_fused:
+                    check(l.mlvae_lstm_fwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                               self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                               _p(w.Cs[li]), _pb(w.Yb[li]), _pb(w.Ydb[li]), w.X8.data_ptr(),
+                                               x8_scale(cfg.dropout), seed, self._drop_off, cfg.dropout,
+                                               _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd_fp8")
+                else:
+                    check(l.mlvae_lstm_fwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                               self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                               int(w.g16), _p(w.Cs[li]), _p(w.Y[li]) if need_y else None,
+                                               _pb(w.Yb[li]) if w.bf else None,
+                                               _pb(w.Ydb[li]) if fuse_drop else None, seed, self._drop_off,
+                                               cfg.dropout if fuse_drop else 0.0,
+                                               _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd")
             xin, xin_bf, din, ldx = w.Y[li], (w.Yb[li] if w.bf else None), 2 * H, 2 * H
             if drop:
                 xin, xin_bf = w.Yd[li], (w.Ydb[li] if w.bf else None)
@@ -913,15 +949,33 @@ class VAEEngine:
             xin, xin_bf, din, ldx = w.layer_in[li]
             Gl = w.G[li]
             dGb = w.dGb[li] if w.bf else None
+            # fp8 mode: the layer's BPTT also writes dG as e4m3 under delayed scaling (the scale
+            # from the previous step's amax, this step's amax for the next) for the fp8 dgrad;
+            # the first step has no amax yet and keeps the bf16 dgrad
+            f8 = bool(cfg.fp8 and w.g16 and w.dG8 is not None and li in getattr(self, "g8", {}))
+            f8_dgrad = f8 and self.g8_ready
             with self._timed("lstm_bwd"):
                 # the layer-0 biases come with dW_ih_l0 from skinny_tn when the encoder is fused
                 rows = w.dbias_rows[li] if (w.g16 and not (li == 0 and w.enc_fused)) else None
-                check(l.mlvae_lstm_bwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                           self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                           int(w.g16), _p(w.Cs[li]), _p(w.dY[li]),
-                                           _pb(dGb) if dGb is not None else None,
-                                           _p(rows) if rows is not None else None,
-                                           _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
+                if f8:
+                    par = self.g8_par   # this step's amax word; the other holds the last step's
+                    am = self.g8_amax[li].data_ptr()
+                    check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), am + 4 * par, _p(self.w8s[li]), G8_MARGIN,
+                                                    _p(self.g8[li]), s), "fp8_delayed_scale")
+                    check(l.mlvae_lstm_bwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                               self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
+                                               _p(w.Cs[li]), _p(w.dY[li]), _pb(dGb),
+                                               _p(rows) if rows is not None else None,
+                                               w.dG8.data_ptr() if f8_dgrad else None, _p(self.g8[li]),
+                                               am + 4 * par, _p(w.xbuf), w.xbuf.numel(), _p(self.err), s),
+                          "lstm_bwd_fp8")
+                else:
+                    check(l.mlvae_lstm_bwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                               self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
+                                               int(w.g16), _p(w.Cs[li]), _p(w.dY[li]),
+                                               _pb(dGb) if dGb is not None else None,
+                                               _p(rows) if rows is not None else None,
+                                               _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
             self._flush_side(pending)
             # dG: fp32 in G (fp32 mode) or bf16 in dGb (bf16 mode)
             dG, dG_bf = (None, dGb) if dGb is not None else (Gl, None)
@@ -992,6 +1046,16 @@ class VAEEngine:
                                         _p(w.dZs), Z, s), "skinny_nt")
                 self._flush_side(pending)
                 fused = False
+            elif f8_dgrad:
+                # configs[4]: dX = dG W_ih on e4m3 operands (dG from the BPTT, W_ih^T cast with the
+                # forward's scale), alpha = 1 / (q_dG q_W), the dropout backward in the epilogue
+                epi8 = EPI_DROPOUT if (drop and mask_ptr is None) else EPI_NONE
+                with self._timed(f"dgrad_l{li}"):
+                    check(l.mlvae_gemm_fp8_ex(N, din, 8 * H, w.dG8.data_ptr(), 8 * H, self.w8t[li].data_ptr(),
+                                              8 * H, _p(dx), din, _p(self.g8[li], 1), None, None, epi8,
+                                              (seed or 0) if epi8 else 0, self._drop_off, cfg.dropout, s),
+                          "gemm_fp8_ex")
+                fused = epi8 == EPI_DROPOUT
             elif dG_bf is not None and li in self.wih_t and din >= 256:
                 # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy
                 with self._timed(f"dgrad_l{li}"):
@@ -1015,6 +1079,9 @@ class VAEEngine:
             if li == cfg.L - 1 and self.world > 1 and self.bucket_allreduce and not full:
                 self._flush_side(pending)  # the bucket waits on the side stream: issue it all
                 self._start_suffix_allreduce()
+        if getattr(self, "g8", None):
+            self.g8_ready = True   # this step's BPTT recorded the amax the next step scales by
+            self.g8_par ^= 1
         # ---- encoder
         w_kl, _ = self.loss_weights()
         if w.enc_fused:

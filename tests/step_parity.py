@@ -50,6 +50,40 @@ def run_step(cfg, B, T, seed, lens, x=None):
     return eng, w, rec, new_ref, params
 
 
+def run_second_step(cfg, B, T, seed, lens):
+    """Two fused steps on the GPU; the oracle replays the SECOND from the engine's state after
+    the first (parameters, Adam moments and step count), with step 2's eps and dropout masks.
+    For paths whose first step differs (the fp8 mode's delayed scaling needs a previous amax).
+    Returns (engine, work, record, oracle post-Adam params, params before step 2)."""
+    from mlvae_hip.engine import VAEEngine
+    g = torch.Generator().manual_seed(seed)
+    params = O.init_params(cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C, seed=seed, enc_conv=cfg.enc_conv)
+    x1 = torch.randn(B, T, cfg.F, generator=g)
+    x2 = torch.randn(B, T, cfg.F, generator=g)
+    eng = VAEEngine(cfg, params=params, seed=seed)
+    eng.train_step(x1.cuda(), lens.cuda())
+    torch.cuda.synchronize()
+    before = {k: v.detach().cpu().clone() for k, v in eng.named_parameters().items()}
+    state = {"step": int(eng.step_ctr.item()),
+             "m": {k: eng.view(k, eng.exp_avg).detach().cpu().clone() for k in before},
+             "v": {k: eng.view(k, eng.exp_avg_sq).detach().cpu().clone() for k in before}}
+    eng.train_step(x2.cuda(), lens.cuda())
+    torch.cuda.synchronize()
+    eng.check_errors()
+    w = eng.work(B, T)
+    eps = w.eps_used.detach().cpu().view(B, T, cfg.Z)
+    masks = None
+    if cfg.dropout > 0 and cfg.L > 1:
+        ms = [torch.from_numpy(dropout_mask((eng.seed * 1000003 + 1 * 131 + li) & ((1 << 63) - 1),
+                                            B * T * 2 * cfg.H, cfg.dropout)).view(B, T, 2 * cfg.H)
+              for li in range(cfg.L - 1)]
+        masks = torch.stack(ms)
+    new_ref, rec = O.train_step(before, state, x2, lens, eps,
+                                dict(L=cfg.L, loss_type=cfg.loss_type, kld_weight=cfg.kld_weight),
+                                masks, impl="aten")
+    return eng, w, rec, new_ref, before
+
+
 def update_errors(eng, rec, new_ref, params):
     """(sign agreement over the defined-direction weights, norm-relative update error over them,
     max |param - oracle|)."""

@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from gpu_utils import need_gpu
-from step_parity import errors, report, run_step
+from step_parity import errors, report, run_second_step, run_step
 
 pytestmark = pytest.mark.gpu
 
@@ -74,4 +74,22 @@ def test_c5_fp8_B64_T500_matches_oracle():
     eng, w, rec, new_ref, params = run_step(cfg, B, T, 809, lens)
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report("c5 fp8 B=64 T=500", e, grads)
+    _check(e, grads, 0.12, 3e-2)
+
+
+def test_c5_fp8_second_step_fp8_dgrad_matches_oracle():
+    """configs[4] in its steady state: from the second step on the fp8 mode also runs the layer-1
+    dgrad on e4m3 operands (dG written by the BPTT under delayed scaling from the first step's
+    amax, W_ih^T with the forward's scale, the dropout backward in the epilogue) and the layer
+    input arrives as e4m3 from the recurrence itself.  The oracle replays step 2 from the engine's
+    state after step 1 (parameters, Adam moments)."""
+    need_gpu()
+    from mlvae_hip.engine import VAEConfig
+    cfg = VAEConfig(F=80, E=64, Z=32, H=512, L=2, C=64, dropout=0.15, prec="bf16", fp8=True)
+    B, T = 64, 500
+    lens = torch.linspace(0.6, 1.0, B)
+    eng, w, rec, new_ref, params = run_second_step(cfg, B, T, 810, lens)
+    assert eng.g8_ready and float(eng.g8[1][0].item()) != 1.0   # a real delayed scale was used
+    e, grads = errors(eng, w, rec, new_ref, params, B, T)
+    report("c5 fp8 step 2 (fp8 dgrad) B=64 T=500", e, grads)
     _check(e, grads, 0.12, 3e-2)
