@@ -274,10 +274,16 @@ def secondary(kern, B, T, cfg_name):
     N = B * T
     out = {}
     gemm_flops = 2.0 * N * 8 * H * 2 * H
+    wg_flops = {"wgrad_ih_l1": 2.0 * N * 8 * H * 2 * H,           # dW_ih_l1 = dG^T X   (K = frames)
+                "wgrad_hh_l1": 2.0 * N * 8 * H * H,               # both directions' dW_hh_l1
+                "wgrad_hh_l0": 2.0 * N * 8 * H * H}
     for name, what in (("proj_l1", "layer-1 input projection [N x 2H] x [2H x 8H] (gemm256)"),
-                       ("dgrad_l1", "layer-1 dgrad [N x 8H] x [8H x 2H] + dropout bwd (gemm256)")):
+                       ("dgrad_l1", "layer-1 dgrad [N x 8H] x [8H x 2H] + dropout bwd (gemm256)"),
+                       ("wgrad_ih_l1", "layer-1 weight gradient dW_ih = dG^T X, K = frames, split-K (gemm256)"),
+                       ("wgrad_hh_l1", "layer-1 dW_hh, both directions, time-shifted h (gemm256, batch 2)"),
+                       ("wgrad_hh_l0", "layer-0 dW_hh, both directions, time-shifted h (gemm256, batch 2)")):
         if name in kern:
-            tf = gemm_flops / (kern[name] * 1e-3) / 1e12
+            tf = wg_flops.get(name, gemm_flops) / (kern[name] * 1e-3) / 1e12
             out[name] = {"what": what, "bound": "mfma", "avg_launch_ms": kern[name],
                          "achieved": tf, "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
                          "frac": tf / MFMA_PEAK_TFLOPS["bf16"]}

@@ -335,6 +335,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         }
       }
       STAMP(4);
+      if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(5);
+      }
       // Behind the publish, off the hand-off's path: the io waves store step s-1's saved
       // activations (right after the barrier they delayed the io waves' own publish: 4.2 vs
       // 3.7 us/step at B = 256); every wave puts step s's into the out ring (gates as fp16).

@@ -591,17 +591,19 @@ class VAEEngine:
         pending.clear()
 
     def _timed(self, name):
-        """HIP events around one launch on the main stream (bench.py's roofline timing)."""
+        """HIP events around one launch on the main stream (bench.py's roofline timing; launches
+        issued to the side stream are not bracketed and are skipped)."""
         eng = self
 
         class _T:
             def __enter__(self_):
-                if eng.kernel_timers is not None:
+                self_.on = eng.kernel_timers is not None and not eng._on_side
+                if self_.on:
                     self_.a = torch.cuda.Event(enable_timing=True)
                     self_.a.record(torch.cuda.current_stream(eng.device))
 
             def __exit__(self_, *exc):
-                if eng.kernel_timers is not None:
+                if self_.on:
                     b = torch.cuda.Event(enable_timing=True)
                     b.record(torch.cuda.current_stream(eng.device))
                     eng.kernel_timers.setdefault(name, []).append((self_.a, b))
@@ -1005,12 +1007,15 @@ class VAEEngine:
                     return
                 if dG_bf is not None and xin_bf is not None and din % 8 == 0 and H % 8 == 0:
                     # 256² GEMMs: dW_ih = dG^T X, and both directions' dW_hh = sum_t dG_t^T h_{t-/+1}
-                    # in one batched launch (the two weights are adjacent in the flat gradient)
-                    self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
-                               gp(f"decoder.rnn.weight_ih_l{li}"), din)
-                    self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
-                               gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
-                               c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                    # in one batched launch (the two weights are adjacent in the flat gradient);
+                    # HIP-event timed when they run on the main stream (the full-chip case)
+                    with self._timed(f"wgrad_ih_l{li}"):
+                        self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
+                                   gp(f"decoder.rnn.weight_ih_l{li}"), din)
+                    with self._timed(f"wgrad_hh_l{li}"):
+                        self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
+                                   gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
+                                   c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
                 else:
                     self._mm(w, 1, 0, 8 * H, din, N, pg(dG), 8 * H, pg(xin), din,
                              gp(f"decoder.rnn.weight_ih_l{li}"), din, A_bf=pgb(dG_bf), B_bf=pgb(xin_bf))

@@ -80,6 +80,9 @@ def main():
             dd = d[2:, b] - d[2:, b - 1]
             print(f"c1 {nm:11s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
         print(f"{'c0 end->c1':14s} median {(d[2:, 8] - d[2:, 4]).median().item():8.0f}")
+    if a.mode & (1 << 23):  # publish -> own stores acknowledged (slot 5)
+        dd = d[2:, 5] - d[2:, 4]
+        print(f"{'publish ack':14s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
     nxt = d[3:, 0] - d[2:-1, 4]
     print(f"{'tail->next':14s} median {nxt.median().item():8.0f}")
     tot = d[3:, 0] - d[2:-1, 0]
