@@ -673,7 +673,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int NJ = H / HJ;                  // workgroups per (dir, group) = producers = consumers
   constexpr int NTW = NKC / 4;                // N-tiles (16 units) per wave: 8 waves cover H
   constexpr int KC = 4 * HJ / 32;             // k-chunks of the own-dG operand (K = 4 HJ)
-  constexpr int KLB = KC / 4;                 // k-chunks whose B-fragments live in LDS (VGPR budget)
+  // k-chunks whose B-fragments live in LDS (VGPR budget).  The <2,16> build reloads ~11 spilled
+  // dwords once, in the prologue (not in the step loop: checked in the ISA)
+  constexpr int KLB = KC / 4;
   constexpr int KR = KC - KLB;
   constexpr int ROWB = 4 * HJ * 2;            // bytes of one A-image row
   constexpr int AIMG = 16 * ROWB;

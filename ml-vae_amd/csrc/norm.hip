@@ -91,18 +91,34 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(int T, int F, const floa
   }
 }
 
-// sums[f] = sum_b valid_b stats[b][f] (f < 2F, b ascending), sums[2F] = number of valid utterances
+// sums[f] = sum_b valid_b stats[b][f] (f < 2F), sums[2F] = number of valid utterances.  Block =
+// 64 columns x 4 utterance lanes (lane l sums b = l, l + 4, ... with four loads in flight), the
+// four lane sums folded in a fixed order: deterministic, and no 256-long dependent load chain
+// (one thread per column walking every utterance took 80 us at B = 256).
 __global__ __launch_bounds__(NT) void norm_sums_kernel(int B, int T, int F, const float* __restrict__ lens,
                                                        const float* __restrict__ stats,
                                                        float* __restrict__ sums) {
-  for (int f = threadIdx.x; f <= 2 * F; f += NT) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) {
-      if (norm_frames(lens[b], T) == 0) continue;
-      s += f < 2 * F ? stats[(size_t)b * 2 * F + f] : 1.f;
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, lb = threadIdx.x >> 6, f = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (f <= 2 * F) {
+    int b = lb;
+    for (; b + 12 < B; b += 16) {
+      float v[4], m[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        m[i] = norm_frames(lens[b + 4 * i], T) > 0 ? 1.f : 0.f;
+        v[i] = f < 2 * F ? stats[(size_t)(b + 4 * i) * 2 * F + f] : 1.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s += m[i] * v[i];
     }
-    sums[f] = s;
+    for (; b < B; b += 4)
+      if (norm_frames(lens[b], T) > 0) s += f < 2 * F ? stats[(size_t)b * 2 * F + f] : 1.f;
   }
+  red[lb][c] = s;
+  __syncthreads();
+  if (lb == 0 && f <= 2 * F) sums[f] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
 }
 
 // mode 0: keep; 1: set to the batch's; 2: global = (1 - w) global + w cur
@@ -146,7 +162,7 @@ extern "C" int mlvae_norm_stats(int B, int T, int F, const float* x, const float
   hipStream_t s = (hipStream_t)stream;
   const int FQ = F / 4, RL = NT / FQ;
   norm_stats_kernel<<<B, NT, (size_t)RL * FQ * sizeof(f32x4), s>>>(T, F, x, rel_lens, utt_stats, eps);
-  norm_sums_kernel<<<1, NT, 0, s>>>(B, T, F, rel_lens, utt_stats, sums);
+  norm_sums_kernel<<<(2 * F + 1 + 63) / 64, NT, 0, s>>>(B, T, F, rel_lens, utt_stats, sums);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
