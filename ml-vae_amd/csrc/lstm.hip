@@ -1186,7 +1186,10 @@ extern "C" int mlvae_lstm_set_debug(void* buf) {
 // bit3 reserves 100 KB LDS per recurrence workgroup, bit4 polls with s_sleep 1 instead of 4,
 // bits 5-10 delay the first poll sweep of every step by that many s_sleep 1, bit 11 times the
 // batch-group kernels without their prefetch, bit 12 runs the wide-batch kernels at any batch,
-// bit 22 runs the wide forward as two interleaved chains per workgroup (lstm_fwd_il_kernel).
+// bit 22 runs the wide forward as two interleaved chains per workgroup (lstm_fwd_il_kernel),
+// bit 23 stamps the forward pollers' publish acknowledgement, bit 24 makes the wide kernels
+// cycle through all NSLOT exchange slots instead of 2 (A/B: 2 slots keep the BPTT's partial
+// tiles in L2 -- PMC 5.34 -> 3.45 GB per launch at c3, 1.53 -> 1.46 ms standalone).
 extern "C" int mlvae_lstm_set_debug_mode(int mode) {
   g_dbg_mode = mode;
   lstm_wide_set_mode(mode);

@@ -92,6 +92,8 @@ template <> struct Elt<PREC_F32> { typedef float T; static constexpr int GE = 2;
 template <> struct Elt<PREC_BF16> { typedef short T; static constexpr int GE = 4; };
 
 __device__ __forceinline__ unsigned step_tag(int s) { return (unsigned)(((s >> 2) + 1) & 1); }
+// the same over 2^lg slots (the wide kernels)
+__device__ __forceinline__ unsigned step_tag_lg(int s, int lg) { return (unsigned)(((s >> lg) + 1) & 1); }
 
 // Granule packing: value 0 carries the tag in its least significant bit.
 __device__ __forceinline__ unsigned long long pack_bf16(float v0, float v1, float v2, float v3,

@@ -88,6 +88,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63;
+  // exchange slots in use: 2 (every member of a group is producer and consumer of every other,
+  // so a slot is rewritten only after all its readers have loaded it); bit 24: all NSLOT
+  const int nlg = (a.dbg_mode & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
@@ -260,8 +263,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         } else {
           // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
           // granule carries step s-1's tag; then into the swizzled LDS image
-          const unsigned tag = step_tag(s - 1);
-          const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * H + wave * PL * 32 + 8 * q;
+          const unsigned tag = step_tag_lg(s - 1, nlg);
+          const unsigned ebase = (unsigned)(((s - 1) & nmask) * xslot) + bi * H + wave * PL * 32 + 8 * q;
           u32x4 hv[PL];
           unsigned spins = 0;
           while (true) {
@@ -318,8 +321,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       }
       if (s + 1 < T) {
         // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
-        const unsigned tag = step_tag(s);
-        const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * H + j0;
+        const unsigned tag = step_tag_lg(s, nlg);
+        const size_t row = (size_t)(s & nmask) * xslot + (size_t)bi * H + j0;
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
           // units 4m+1..3 of lane (bi, 0) sit in lanes bi + 16, 32, 48: VALU permlane swaps
@@ -353,7 +356,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         of[u] = c[t]; of[HJ + u] = hvals[t];
       }
       // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
-      // waves 4-5 instead, they held the barrier: 1.38 vs 1.33 ms per forward launch at c3)
+      // waves 4-5 instead, they held the barrier: 1.38 vs 1.33 ms per forward launch at c3;
+      // spread over all four poller waves, one Philox call each: no change, 11.82 vs 11.73 ms
+      // per step)
       if (!IO && a.Ydb && tid < NC8) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
     }
     __syncthreads();
@@ -410,6 +415,9 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
   const int dir = gid / npair, pr = gid % npair;
   const int T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63;
+  // exchange slots in use: 2 (every member of a group is producer and consumer of every other,
+  // so a slot is rewritten only after all its readers have loaded it); bit 24: all NSLOT
+  const int nlg = (a.dbg_mode & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
@@ -571,8 +579,8 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
             if constexpr (TPW == 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
           } else if (ROLE == 0) {
-            const unsigned tag = step_tag(s - 1);
-            const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * H + wave * PL * 32 + 8 * q;
+            const unsigned tag = step_tag_lg(s - 1, nlg);
+            const unsigned ebase = (unsigned)(((s - 1) & nmask) * xslot) + bi * H + wave * PL * 32 + 8 * q;
             u32x4 hv[PL];
             unsigned spins = 0;
             while (true) {
@@ -622,8 +630,8 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
           gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
         }
         if (s + 1 < T) {
-          const unsigned tag = step_tag(s);
-          const size_t row = (size_t)(s & (NSLOT - 1)) * xslot + (size_t)bi * H + j0;
+          const unsigned tag = step_tag_lg(s, nlg);
+          const size_t row = (size_t)(s & nmask) * xslot + (size_t)bi * H + j0;
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
             const unsigned hu = __float_as_uint(hvals[t]);
@@ -700,6 +708,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const int dir = gid / a.NB, grp = gid % a.NB;
   const int T = a.T, j0 = js * HJ;
   const int tid = threadIdx.x, lane = tid & 63;
+  // exchange slots in use: 2 (every member of a group is producer and consumer of every other,
+  // so a slot is rewritten only after all its readers have loaded it); bit 24: all NSLOT
+  const int nlg = (a.dbg_mode & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
@@ -836,8 +847,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     for (int ci = 0; ci < CPG; ++ci) dh[ci] = 0.f;
     u32x4 pv[CPG][NPL];
     if (s > 0) {
-      const unsigned tag = step_tag(s - 1);
-      const size_t sb = (size_t)((s - 1) & (NSLOT - 1)) * xslot + (size_t)js * NJ * HJ * 16;
+      const unsigned tag = step_tag_lg(s - 1, nlg);
+      const size_t sb = (size_t)((s - 1) & nmask) * xslot + (size_t)js * NJ * HJ * 16;
       unsigned spins = 0;
       while (true) {
 #pragma unroll
@@ -946,8 +957,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
           acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf, acc[nt], 0, 0, 0);
         }
       }
-      const unsigned tag = step_tag(s);
-      const size_t sb = (size_t)(s & (NSLOT - 1)) * xslot;
+      const unsigned tag = step_tag_lg(s, nlg);
+      const size_t sb = (size_t)(s & nmask) * xslot;
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         // acc[nt][r]: partial dh of utterance 4q + r, unit n

@@ -31,14 +31,15 @@ def test_two_shards_sum_to_full_batch(monkeypatch):
     total = int(O.length_to_mask(lens.cpu(), T).sum().item())
     monkeypatch.setattr(mdist, "allreduce_count", lambda c, group=None: c.fill_(total))
     grads, losses = [], []
-    for r, sl in enumerate((slice(0, 2), slice(2, B))):
+    for r, sl in enumerate((slice(0, B // 2), slice(B // 2, B))):
         eng = VAEEngine(cfg, params=params)
-        eng.world, eng.global_offset = 2, sl.start
+        eng.world, eng.rank = 2, r   # equal shards: the engine starts rank r's at r * B/2
         eng.bucket_allreduce = False  # no collective here: the shards are summed by hand
         w = eng.forward(x[sl].contiguous(), lens[sl].contiguous(), train=True)
         eng.backward(w)
         torch.cuda.synchronize()
         eng.check_errors()
+        assert eng.global_offset == sl.start
         grads.append(eng.grad.clone())
         losses.append(w.loss.clone())
     gsum = grads[0] + grads[1]

@@ -75,6 +75,10 @@ def main():
     for b, nm in zip(range(1, 5), names):
         dd = d[2:, b] - d[2:, b - 1]
         print(f"{nm:14s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
+    per = d[3:T - 1, 0] - d[2:T - 2, 0]     # step start to step start: the whole period
+    tail = per - (d[2:T - 2, 4] - d[2:T - 2, 0])
+    print(f"{'tail':14s} median {tail.median().item():8.0f} ticks  mean {tail.mean().item():8.0f}")
+    print(f"{'step period':14s} median {per.median().item():8.0f} ticks  mean {per.mean().item():8.0f}")
     if a.mode & (1 << 22):  # interleaved forward: chain 1's stamps sit at slots 8..12
         for b, nm in zip(range(9, 13), names):
             dd = d[2:, b] - d[2:, b - 1]
