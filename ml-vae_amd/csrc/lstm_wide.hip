@@ -355,11 +355,15 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
         of[u] = c[t]; of[HJ + u] = hvals[t];
       }
+      STAMP(6);
       // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
       // waves 4-5 instead, they held the barrier: 1.38 vs 1.33 ms per forward launch at c3;
       // spread over all four poller waves, one Philox call each: no change, 11.82 vs 11.73 ms
-      // per step)
+      // per step).  Tried and reverted as well (same box, c3 12.60-12.73 -> 12.78-12.92 ms):
+      // io waves waiting for their gx LDS-DMA alone by a counted vmcnt (their stores left in
+      // flight across the barrier), and the BPTT's dG stores moved behind the next poll.
       if (!IO && a.Ydb && tid < NC8) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
+      STAMP(7);
     }
     __syncthreads();
     if (IO) io_store(T - 1);
@@ -879,7 +883,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     // s+2's loads issued right behind this step's hand-off -- one program point per step, so
     // the loaded registers need no merge (and no wait for the loads)
     stage_cell(s + 1);
+    STAMP(5);
     load_cell(s + 2);
+    STAMP(6);
     if (s > 0) {
       const bool b2 = pg & 4, b1 = pg & 2, b0 = pg & 1;
 #pragma unroll

@@ -75,6 +75,10 @@ def main():
     for b, nm in zip(range(1, 5), names):
         dd = d[2:, b] - d[2:, b - 1]
         print(f"{nm:14s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
+    # every stamp as an offset from the step start (extra stamps 5..7: see the STAMP sites)
+    offs = [f"{b}:{(d[2:T - 1, b] - d[2:T - 1, 0]).median().item():.0f}" for b in range(1, 8)
+            if (d[2:T - 1, b] != 0).all()]
+    print("offsets from step start (median ticks) " + " ".join(offs))
     per = d[3:T - 1, 0] - d[2:T - 2, 0]     # step start to step start: the whole period
     tail = per - (d[2:T - 2, 4] - d[2:T - 2, 0])
     print(f"{'tail':14s} median {tail.median().item():8.0f} ticks  mean {tail.mean().item():8.0f}")
