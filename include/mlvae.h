@@ -299,8 +299,13 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
  * head gets no gradient, so db3v, db2v and db1[C:] are not written).  Replaces the autograd
  * bias sums of ref:src/modules/fc_block.py:9-16 without re-reading dOUT / dP2 / dP1.
  * saved_bf16: p1, p2m/p2v, dmux/dlvx, dp2m/dp2v and dp1 are written as bf16 (packed rows, the
- * weight-gradient GEMMs' operand precision) instead of fp32; mux / lvx / dy stay fp32. */
+ * weight-gradient GEMMs' operand precision) instead of fp32; mux / lvx / dy stay fp32.
+ * With bias_ws and saved_bf16 in train mode the work runs in split form: P1 and dY as 256^2
+ * GEMMs (bias + LReLU + bf16 epilogue; fp32 dY) around a persistent kernel for the middle stages
+ * (same outputs; mlvae_heads_set_mode(1) or MLVAE_HEADS_FUSED=1 keeps the single fused kernel,
+ * for A/B timing; returns the previous mode). */
 size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C);
+int mlvae_heads_set_mode(int mode);
 int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
                          const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
                          const float* w2m, const float* b2m, const float* w3m, const float* b3m,

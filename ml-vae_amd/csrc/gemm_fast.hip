@@ -46,7 +46,7 @@ struct GFArgs {
   unsigned long long dseed, doff; float dkeep, dscale;  // mask of doff + row*ldc + col
   int splits, kchunk;
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
-  int c16;            // C stored as fp16 (epi bit EPI_OUT_F16)
+  int c16;            // C stored as 16-bit: 1 fp16 (epi bit EPI_OUT_F16), 2 bf16 (EPI_OUT_BF16)
   const float* alpha; // device scalar multiplying A.B (fp8 operand scales), or null
   int abl;            // ablation bits (MLVAE_GEMM_ABL, timing only): 1 no MFMA, 2 no staging loads
   float* ws;
@@ -54,6 +54,7 @@ struct GFArgs {
 
 enum { EPI_NONE = 0, EPI_LRELU = 1, EPI_DLRELU = 2, EPI_DROPOUT = 3 };
 constexpr int EPI_OUT_F16 = 16;  // flag bit of the ABI's epi: C is fp16 (staged epilogue only)
+constexpr int EPI_OUT_BF16 = 32; // flag bit of the ABI's epi: C is bf16 (staged epilogue only)
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(3))) bf16x4* lds_b4_t;
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   // (fp32 output, no beta; split partial slabs too).  c2 skinny projection: 88 -> 56 us.
   const bool bias_vec = ((uintptr_t)g.bias1 % 16) == 0 && ((uintptr_t)g.bias2 % 16) == 0;
   if ((g.N % 4) == 0 && g.beta == 0.f &&
-      (split || (vec && bias_vec && (g.epi == EPI_NONE || g.epi == EPI_DROPOUT)))) {
+      (split || (vec && bias_vec && (g.epi == EPI_NONE || g.epi == EPI_DROPOUT || g.epi == EPI_LRELU)))) {
     constexpr int LSR = TBN + 4;  // staged row stride (floats)
     float* st = reinterpret_cast<float*>(smem);  // [64][LSR] = 66.5 KB of the 128 KB
     float* dst = split ? wsz : Cb;
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
         if (g.bias1) b += *reinterpret_cast<const f32x4*>(g.bias1 + col);
         if (g.bias2) b += *reinterpret_cast<const f32x4*>(g.bias2 + col);
       }
-#pragma unroll
+#pragma unroll 2  // (fully unrolled, the four passes outgrew the unroller: acc went to scratch)
       for (int q = 0; q < 8; ++q) {
         const int lr = q * 8 + (tid >> 6);  // wave w stores staged rows w, w + 8, ...
         const int row = m0 + (lr >> 5) * 128 + (2 * pass + ((lr >> 4) & 1)) * 16 + (lr & 15);
@@ -470,7 +471,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
         }
-        if (!split && g.c16)
+        if (!split && g.epi == EPI_LRELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r]);
+        }
+        if (!split && g.c16 == 2)
+          *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(Cb) + (size_t)row * ldd + col) =
+              u32x2{(unsigned)(unsigned short)f2bf(v[0]) | ((unsigned)(unsigned short)f2bf(v[1]) << 16),
+                    (unsigned)(unsigned short)f2bf(v[2]) | ((unsigned)(unsigned short)f2bf(v[3]) << 16)};
+        else if (!split && g.c16)
           *reinterpret_cast<u32x2*>(reinterpret_cast<unsigned short*>(Cb) + (size_t)row * ldd + col) = f2h4(v);
         else
           *reinterpret_cast<f32x4*>(dst + (size_t)row * ldd + col) = v;
@@ -535,9 +544,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
     const int row = (int)(idx / g.N), col = (int)(idx % g.N);
     if (g.bias1) s += g.bias1[col];
     if (g.bias2) s += g.bias2[col];
-    if (g.c16) {  // beta == 0, epi NONE / DROPOUT (checked on the host)
+    if (g.c16) {  // beta == 0, epi NONE / DROPOUT (fp16) or NONE / LRELU (bf16) (checked on the host)
       if (g.epi == EPI_DROPOUT) s *= dropout_scale(g.dseed, g.doff + (size_t)row * g.ldc + col, g.dkeep, g.dscale);
-      reinterpret_cast<unsigned short*>(Cb)[(size_t)row * g.ldc + col] = f2h(s);
+      if (g.epi == EPI_LRELU) s = lrelu(s);
+      reinterpret_cast<unsigned short*>(Cb)[(size_t)row * g.ldc + col] =
+          g.c16 == 2 ? (unsigned short)f2bf(s) : f2h(s);
       continue;
     }
     float* cp = Cb + (size_t)row * g.ldc + col;
@@ -652,11 +663,13 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     return 1;
   }
   if (M == 0 || N == 0) return 0;
-  const int c16 = (epi & EPI_OUT_F16) ? 1 : 0;
-  epi &= ~EPI_OUT_F16;
-  if (c16 && (beta != 0.f || (epi != EPI_NONE && epi != EPI_DROPOUT) || N % 4 || ldc % 4 ||
+  const int c16 = (epi & EPI_OUT_BF16) ? 2 : ((epi & EPI_OUT_F16) ? 1 : 0);
+  epi &= ~(EPI_OUT_F16 | EPI_OUT_BF16);
+  if (c16 && (beta != 0.f || (c16 == 1 && epi != EPI_NONE && epi != EPI_DROPOUT) ||
+              (c16 == 2 && epi != EPI_NONE && epi != EPI_LRELU) || N % 4 || ldc % 4 ||
               ((uintptr_t)C % 16) || (c_bstride % 8) || ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16))) {
-    mlvae_set_error("mlvae_gemm_bf16: fp16 C needs beta 0, epilogue none/dropout, N and ldc %% 4, aligned C/bias");
+    mlvae_set_error("mlvae_gemm_bf16: 16-bit C needs beta 0, epilogue none/dropout (fp16) or none/lrelu (bf16), "
+                    "N and ldc %% 4, aligned C/bias");
     return 1;
   }
   if (epi < EPI_NONE || epi > EPI_DROPOUT) { mlvae_set_error("mlvae_gemm_bf16: bad epilogue %d", epi); return 1; }

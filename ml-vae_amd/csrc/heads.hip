@@ -24,6 +24,7 @@
 // fp32 parameters (two row-major, two transposed; bf16, padded rows: conflict-free 16-lane
 // ds_read_b128).  Saved tensors for the weight-gradient GEMMs (side stream) are written fp32.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -371,6 +372,242 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Split form (train, bf16 saved intermediates): the two wide products leave the fused kernel,
+// whose per-tile W1 / W1^T streaming (16 + 8 dependent L2 round trips per 64-row tile at one
+// workgroup per CU) made it latency-bound (1.7 TB/s):
+//   1. P1 = lrelu(Y W1^T + b1)  bf16       gemm256 (bias + LReLU + bf16 staged epilogue)
+//   2. heads_mid_kernel: stages 2-6 below over P1 -- persistent workgroups build the four small
+//      weight images once and walk 64-row tiles, the next tile's P1 rows and x prefetched into
+//      registers while the current one computes
+//   3. dY = dP1 W1             fp32       gemm256 (k-contiguous dP1 and W1^T)
+// The partial sums and bias column sums keep the fused kernel's per-tile layout.
+template <int C, int F>
+__global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
+  constexpr int C2 = 2 * C, FK = (F + 31) / 32 * 32;
+  constexpr int LC = C + 8, LF = FK + 8, L2C = C2 + 8;
+  constexpr int NC = C / 16, NF = F / 16, NC2 = C2 / 16;
+  constexpr int O_W2I = 0, O_W2T = O_W2I + 2 * C * LC, O_W3I = O_W2T + 2 * C * LC;
+  constexpr int O_W3T = O_W3I + 2 * F * LC, O_P1 = O_W3T + 2 * C * LF;
+  constexpr int O_P2 = O_P1 + RT * L2C, O_DO = O_P2 + 2 * RT * LC, O_END = O_DO + 2 * RT * LF;
+  static_assert(O_END * 2 <= 160 * 1024, "LDS budget");
+  static_assert(C2 == 128, "P1 row = 16 lanes x 16 bytes");
+  extern __shared__ __attribute__((aligned(16))) short sm[];
+  __shared__ float red[4];
+  constexpr int NBS = nbs<C, F>();
+  __shared__ __attribute__((aligned(16))) float bred[4][NBS];
+  __shared__ float inv_cnt;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int ntiles = (a.N + RT - 1) / RT;
+  const bool lik = a.loss_type == 0;
+  const int nh = lik ? 2 : 1;
+
+  // ---- weight images (bf16) from the fp32 parameters, once per workgroup
+  for (int idx = tid; idx < 2 * C * (C / 4); idx += 256) {
+    const int h = idx / (C * C / 4), rem = idx % (C * C / 4), n = rem / (C / 4), k = (rem % (C / 4)) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(a.W2[h] + n * C + k);
+    st4bf(sm + O_W2I + h * C * LC + n * LC + k, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm[O_W2T + h * C * LC + (k + i) * LC + n] = f2bf(v[i]);
+  }
+  for (int idx = tid; idx < 2 * F * (C / 4); idx += 256) {
+    const int h = idx / (F * C / 4), rem = idx % (F * C / 4), f = rem / (C / 4), k = (rem % (C / 4)) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(a.W3[h] + f * C + k);
+    st4bf(sm + O_W3I + h * F * LC + f * LC + k, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm[O_W3T + h * C * LF + (k + i) * LF + f] = f2bf(v[i]);
+  }
+  if constexpr (FK > F) {  // zero K padding of W3^T and of the dOUT images (never rewritten)
+    for (int idx = tid; idx < 2 * C * (FK - F); idx += 256) {
+      const int h = idx / (C * (FK - F)), rem = idx % (C * (FK - F));
+      sm[O_W3T + h * C * LF + (rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
+    }
+    for (int idx = tid; idx < 2 * RT * (FK - F); idx += 256) {
+      const int h = idx / (RT * (FK - F)), rem = idx % (RT * (FK - F));
+      sm[O_DO + h * RT * LF + (rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
+    }
+  }
+  if (tid == 0) {
+    int c = 0;
+    if (a.count) c = *a.count;
+    else for (int b = 0; b < a.B; ++b) c += valid_frames(a.lens[b], a.T);
+    inv_cnt = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
+  }
+
+  // a lane's share of its wave's 16 P1 rows (row l15 + 16 wave... as 4 x 16-byte chunks: chunk
+  // q + 4 i of row l15) and its x values (row l15, columns 16 j + 4 q), prefetched a tile ahead
+  const unsigned short* P1b = reinterpret_cast<const unsigned short*>(a.P1);
+  u32x4 pn[4];
+  f32x4 xn[NF];
+  auto prefetch = [&](int tile) {
+    const int grow = tile * RT + 16 * wave + l15;
+    const bool rv = tile < ntiles && grow < a.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      pn[i] = rv ? *reinterpret_cast<const u32x4*>(P1b + (size_t)grow * C2 + 8 * (q + 4 * i)) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+      xn[j] = rv ? *reinterpret_cast<const f32x4*>(a.x + (size_t)grow * F + 16 * j + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  prefetch(blockIdx.x);
+  __syncthreads();
+
+  const int lrow = 16 * wave + l15;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int grow = tile * RT + lrow;
+    const bool rv = grow < a.N;
+    // this tile's P1 rows into the wave's P1 image; the next tile's loads go out behind them
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(sm + O_P1 + lrow * L2C + 8 * (q + 4 * i)) = pn[i];
+    f32x4 xv[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) xv[j] = xn[j];
+    prefetch(tile + gridDim.x);
+    // P1 in the result layout (lane: row lrow, columns 16 j + 4 q .. + 3) for lrelu' in stage 6
+    f32x4 p1r[NC2];
+#pragma unroll
+    for (int j = 0; j < NC2; ++j) {
+      const bf16x4 v = *reinterpret_cast<const bf16x4*>(sm + O_P1 + lrow * L2C + 16 * j + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p1r[j][r] = bf2f(v[r]);
+    }
+
+    // ---- stages 2-3 per head: P2 = lrelu(P1_h W2^T + b2), OUT = P2 W3^T + b3
+    f32x4 acc2[2][NC], acc3[2][NF];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc2[h][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < C; kk += 32) {
+        const bf16x8 av = lds8(sm + O_P1 + lrow * L2C + h * C + kk + 8 * q);
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+          acc2[h][j] = mfma(lds8(sm + O_W2I + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc2[h][j]);
+      }
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int col = 16 * j + 4 * q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc2[h][j][r] = lrelu(acc2[h][j][r] + a.b2[h][col + r]);
+        st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc2[h][j]);
+        if (rv) st_saved(a.P2[h], (size_t)grow * C + col, acc2[h][j], 1);
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc3[h][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < C; kk += 32) {
+        const bf16x8 av = lds8(sm + O_P2 + h * RT * LC + lrow * LC + kk + 8 * q);
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+          acc3[h][j] = mfma(lds8(sm + O_W3I + h * F * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc3[h][j]);
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int col = 16 * j + 4 * q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc3[h][j][r] += a.b3[h][col + r];
+        if (rv) *reinterpret_cast<f32x4*>(a.OUT[h] + (size_t)grow * F + col) = acc3[h][j];
+      }
+    }
+
+    // ---- stage 4: reconstruction loss, masked partial sum, gradient wrt (mu, log_var)
+    bool m = false;
+    if (rv) {
+      const int b = grow / a.T, t = grow % a.T;
+      m = t < valid_frames(a.lens[b], a.T);
+    }
+    const float sc = m ? a.rec_scale * inv_cnt : 0.f;
+    float lsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int col = 16 * j + 4 * q;
+      f32x4 gm, gv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mu = acc3[0][j][r], d = xv[j][r] - mu;
+        float rr, gmu, glv = 0.f;
+        if (lik) {
+          const float lv = acc3[1][j][r];
+          const float elv = expf(lv), ev = elv + 1e-5f;
+          rr = 0.5f * (LOG_2PI_H + lv + d * d / ev);
+          gmu = -d / ev;
+          glv = 0.5f * (1.f - d * d * elv / (ev * ev));
+        } else {
+          rr = d * d;
+          gmu = -2.f * d;
+        }
+        if (m) lsum += rr;
+        gm[r] = sc * gmu;
+        gv[r] = sc * glv;
+      }
+      rows16_to_lds(gm, &bred[wave][16 * j], lane);
+      rows16_to_lds(gv, &bred[wave][F + 16 * j], lane);
+      st4bf(sm + O_DO + lrow * LF + col, gm);
+      st4bf(sm + O_DO + RT * LF + lrow * LF + col, gv);
+      if (rv) {
+        st_saved(a.dOUT[0], (size_t)grow * F + col, gm, 1);
+        if (lik) st_saved(a.dOUT[1], (size_t)grow * F + col, gv, 1);
+      }
+    }
+    lsum = wave_sum(lsum);
+    if (lane == 0) red[wave] = lsum;
+
+    // ---- stages 5-6 per head: dP2 = (dOUT W3) * lrelu'(P2), dP1_h = (dP2 W2) * lrelu'(P1_h);
+    // every image a wave reads here is its own rows: no workgroup barrier until the sums
+    for (int h = 0; h < 2; ++h) {
+      f32x4 acc5[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc5[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (h < nh) {
+#pragma unroll
+        for (int kk = 0; kk < FK; kk += 32) {
+          const bf16x8 av = lds8(sm + O_DO + h * RT * LF + lrow * LF + kk + 8 * q);
+#pragma unroll
+          for (int j = 0; j < NC; ++j)
+            acc5[j] = mfma(lds8(sm + O_W3T + h * C * LF + (16 * j + l15) * LF + kk + 8 * q), av, acc5[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int col = 16 * j + 4 * q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc5[j][r] *= lrelu_d(acc2[h][j][r]);
+        rows16_to_lds(acc5[j], &bred[wave][2 * F + h * C + 16 * j], lane);
+        st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc5[j]);
+        if (rv && h < nh) st_saved(a.dP2[h], (size_t)grow * C + col, acc5[j], 1);
+      }
+      f32x4 acc6[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc6[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (h < nh) {
+#pragma unroll
+        for (int kk = 0; kk < C; kk += 32) {
+          const bf16x8 av = lds8(sm + O_P2 + h * RT * LC + lrow * LC + kk + 8 * q);
+#pragma unroll
+          for (int j = 0; j < NC; ++j)
+            acc6[j] = mfma(lds8(sm + O_W2T + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc6[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int col = h * C + 16 * j + 4 * q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc6[j][r] *= lrelu_d(p1r[h * NC + j][r]);
+        rows16_to_lds(acc6[j], &bred[wave][2 * F + 2 * C + h * C + 16 * j], lane);
+        if (rv) st_saved(a.dP1, (size_t)grow * C2 + col, acc6[j], 1);
+      }
+    }
+    __syncthreads();  // every wave's sums of this tile are in bred / red
+    for (int c = tid; c < NBS; c += 256)
+      a.bias_ws[(size_t)tile * NBS + c] = (bred[0][c] + bred[1][c]) + (bred[2][c] + bred[3][c]);
+    if (tid == 0) a.partials[tile] = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();  // bred / red are rewritten by the next tile
+  }
+}
+
 // bias gradients = the per-workgroup column sums summed over workgroups, in two fixed-order
 // stages (deterministic): stage 1 -- block (column block of 32, slice z of RSL) sums its slice's
 // workgroups with 8 row groups into slices[z]; stage 2 sums the RSL slices in order.  One block
@@ -428,6 +665,32 @@ int launch_heads(const HeadArgs& a, hipStream_t st) {
 }
 
 template <int C, int F>
+int launch_mid(const HeadArgs& a, hipStream_t st) {
+  constexpr int FK = (F + 31) / 32 * 32, LC = C + 8, LF = FK + 8, L2C = 2 * C + 8;
+  constexpr size_t lds = (size_t)(2 * C * LC * 2 + 2 * F * LC + 2 * C * LF + RT * L2C + 2 * RT * LC +
+                                  2 * RT * LF) * sizeof(short);
+  auto k = heads_mid_kernel<C, F>;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess) {
+      mlvae_set_error("heads_mid: cannot reserve %zu B LDS", lds);
+      return 2;
+    }
+    attr = true;
+  }
+  // persistent: one workgroup per CU (the LDS holds one), ~8 tiles each at c3
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  const int ntiles = (a.N + RT - 1) / RT;
+  k<<<ntiles < cus ? ntiles : cus, 256, lds, st>>>(a);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int C, int F>
 int launch_bias_reduce(const HeadArgs& a, int n1, float* db3m, float* db3v, float* db2m, float* db2v,
                        float* db1, hipStream_t st) {
   constexpr int NBS = nbs<C, F>();
@@ -441,6 +704,31 @@ int launch_bias_reduce(const HeadArgs& a, int n1, float* db3m, float* db3v, floa
 }
 
 }  // namespace
+
+extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, int batch,
+                               const void* A, int lda, long long a_bstride, const void* B, int ldb,
+                               long long b_bstride, float* C, int ldc, long long c_bstride,
+                               float beta, const float* bias1, const float* bias2, int epi,
+                               const float* aux, int ldaux, int kshift_T, int kshift,
+                               int kshift_bstep, unsigned long long drop_seed,
+                               unsigned long long drop_offset, float drop_p,
+                               float* ws, size_t ws_bytes, void* stream);
+
+// heads path (diagnostics / A/B): 1 = the single fused kernel in train mode too (default: the
+// split form whenever the saved intermediates are bf16 and the bias sums are in-kernel)
+static int g_heads_fused_only = -1;
+extern "C" int mlvae_heads_set_mode(int mode) {
+  const int prev = g_heads_fused_only;
+  g_heads_fused_only = mode;
+  return prev;
+}
+static bool heads_fused_only() {
+  if (g_heads_fused_only < 0) {
+    const char* e = getenv("MLVAE_HEADS_FUSED");
+    g_heads_fused_only = e && atoi(e) != 0 ? 1 : 0;
+  }
+  return g_heads_fused_only == 1;
+}
 
 extern "C" int mlvae_heads_partials_count(int B, int T) { return (B * T + RT - 1) / RT; }
 
@@ -545,7 +833,20 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
     a.bias_ws = bias_ws;
   }
   hipStream_t st = (hipStream_t)stream;
-  int rc = F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
+  int rc;
+  if (train && bias_ws && saved_bf16 && !heads_fused_only()) {
+    // split form: P1 GEMM, the persistent middle stages, dY GEMM (heads_mid_kernel comment)
+    constexpr int EPI_LRELU_BF16 = 1 | 32;  // gemm_fast.hip: EPI_LRELU | EPI_OUT_BF16
+    rc = mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
+                         nullptr, EPI_LRELU_BF16, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
+    if (rc) return rc;
+    rc = F == 80 ? launch_mid<64, 80>(a, st) : launch_mid<64, 64>(a, st);
+    if (rc) return rc;
+    rc = mlvae_gemm_bf16(0, 1, a.N, H2, 2 * C, 1, dp1, 2 * C, 0, w1t_bf16, 2 * C, 0, dy, H2, 0, 0.f, nullptr,
+                         nullptr, 0, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
+  } else {
+    rc = F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
+  }
   if (rc || !bias_ws) return rc;
   // mse: the log_var head gets no gradient (torch leaves its grads None): its bias gradients and
   // the log_var half of the stacked first-layer bias are not written

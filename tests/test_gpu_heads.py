@@ -169,4 +169,7 @@ def test_heads_fused_bias_sums(loss_type, B, T, F, H2):
     for k in ("p1", "p2m", "dmux", "dp2m", "dp1") + (("p2v", "dlvx", "dp2v") if lik else ()):
         assert torch.equal(ob[k], o[k].to(torch.bfloat16)), k
     assert torch.equal(dy2, o["dy"]) and torch.equal(mux2, o["mux"])
-    assert torch.equal(b1b[:C], first[:C])
+    # saved_bf16 + bias sums runs the split form (P1 / dY GEMMs around heads_mid_kernel): every
+    # output above is bit-identical; its bias sums agree to fp32 rounding (1 ulp seen in tiles
+    # with masked frames)
+    assert rel_err(b1b[:C], first[:C]) < 1e-6
