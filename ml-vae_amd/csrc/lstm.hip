@@ -27,6 +27,7 @@
 // The backward pass all-gathers the pre-activation gate gradients dG_t the same way and forms
 // dh_{t-1} = dG_t W_hh for its own hidden slice from a resident W_hh^T column slice.
 #include "common.h"
+#include <stdlib.h>
 #include <type_traits>
 
 #include "lstm_common.h"
@@ -821,7 +822,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
 }
 
 unsigned long long* g_dbg = nullptr;
-int g_dbg_mode = 0;
+// debug / A-B bits of the recurrence kernels (mlvae_lstm_set_debug_mode); MLVAE_LSTM_DBG sets
+// the initial value so a whole bench run can be timed under one variant
+int g_dbg_mode = [] {
+  const char* e = getenv("MLVAE_LSTM_DBG");
+  return e ? (int)strtol(e, nullptr, 0) : 0;
+}();
 
 struct Plan {
   int NB, NJ, HJ, Kp, K4p;   // NJ/HJ of the launch being planned (fwd or bwd)

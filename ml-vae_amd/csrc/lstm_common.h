@@ -87,6 +87,35 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
       a.dbg[(size_t)s * 16 + (slot) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// LDS-buffered stamps (wide kernels): thread 0 of workgroup 0 records s_memtime at the phase
+// points of steps [STW0, STW0 + STWN) in LDS and writes them to dbg[s*16 + phase] once, after
+// the step loop -- no global store inside the loop, so no vmcnt wait ever queues behind one
+constexpr int STW0 = 64, STWN = 32;
+#define LSTAMP_DECL                                                            \
+  __shared__ unsigned long long stamp_lds[STWN * 16];                          \
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                            \
+    for (int i_ = 0; i_ < STWN * 16; ++i_) stamp_lds[i_] = 0
+#define LSTAMP(ph)                                                             \
+  do {                                                                         \
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 &&                        \
+        (unsigned)(s - STW0) < (unsigned)STWN)                                 \
+      stamp_lds[(s - STW0) * 16 + (ph)] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+// per-wave stamp (lane 0 of every wave of workgroup 0) into slot 8 + wave
+#define LWSTAMP()                                                              \
+  do {                                                                         \
+    if (a.dbg && blockIdx.x == 0 && (threadIdx.x & 63) == 0 &&                 \
+        (unsigned)(s - STW0) < (unsigned)STWN)                                 \
+      stamp_lds[(s - STW0) * 16 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define LSTAMP_FLUSH()                                                         \
+  do {                                                                         \
+    __syncthreads();                                                           \
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                          \
+      for (int i_ = 0; i_ < STWN * 16; ++i_)                                   \
+        a.dbg[(size_t)STW0 * 16 + i_] = stamp_lds[i_];                         \
+  } while (0)
+
 template <int PREC> struct Elt;
 template <> struct Elt<PREC_F32> { typedef float T; static constexpr int GE = 2; };   // per granule
 template <> struct Elt<PREC_BF16> { typedef short T; static constexpr int GE = 4; };

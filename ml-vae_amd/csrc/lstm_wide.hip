@@ -73,6 +73,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int QPT = NQ / 256;               // quads per io thread
   static_assert(NQ % 256 == 0, "io split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  LSTAMP_DECL;
   char* himg = smem;                                        // [2][16][ROWB], swizzled slots
   unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2][16][GXU] fp16
   char* outr = reinterpret_cast<char*>(gxr + 2 * 16 * GXU);                 // [2][16][OUB]
@@ -135,18 +136,21 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const bool io = wave >= 4;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
+  const auto rgx = make_rsrc(G16 + (size_t)grp * BG * T * 8 * H, 0xffffffffu);
   auto io_load = [&](int s_) {  // input projection of step s_ into gx ring slot s_ & 1
     if (s_ >= T || (s_ > 0 && (a.dbg_mode & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
     constexpr int UPW = 16 / 4;  // utterances per io wave
+    // one descriptor over the group's 16 utterances (per-utterance descriptors spilled SGPRs
+    // into the io waves' MFMA phase); the host keeps 16 T 8H halfs under 4 GB
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
       const int u = (wave - 4) * UPW + i, b = grp * BG + u;
       if (b >= a.B) continue;
       // lane l < HJ/2 -> gate l / (HJ/8), units 8 (l % (HJ/8)) .. + 7
-      const auto rs = make_rsrc(G16 + (size_t)b * T * 8 * H, (unsigned)((size_t)T * 8 * H * 2));
       const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
-      const unsigned off = (unsigned)(((size_t)t_ * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
+      const unsigned off = (unsigned)((((size_t)u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
+      const auto rs = rgx;
       unsigned short* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
       // nt: read-once stream, kept from displacing the hand-off lines in L2
       if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
@@ -226,6 +230,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // The step loop, instantiated once per role (IO: waves 4-7 move the step's HBM traffic;
   // else waves 0-3 poll the hand-off): each instance keeps only its own role's state live,
   // and both pass the same barriers.
+  const bool late_bits = a.Ydb && !(a.dbg_mode & (1 << 27));
   auto run = [&](auto io_tag) {
     constexpr bool IO = decltype(io_tag)::value;
     if (IO) {
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) c[t] = 0.f;
     for (int s = 0; s < T; ++s) {
-      STAMP(0);
+      LSTAMP(0);
       f32x4 acc[TPW];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -270,6 +275,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           while (true) {
 #pragma unroll
             for (int i = 0; i < PL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
+            // step s-1's dropout keep bits, drawn while the first poll's loads are in flight
+            // (drawn before them, at the end of step s-1, they delayed the poll's issue; with the
+            // io-first MFMAs: c3 12.06 -> 11.92, c2 4.95 -> 4.72 ms/step).  A/B bit 27: the old place
+            if (late_bits && spins == 0 && tid < NC8) dbl[((s - 1) & 1) * NC8 + tid] = drop_bits(s - 1, tid);
             bool ok = true;
 #pragma unroll
             for (int i = 0; i < PL; ++i) ok &= tags_ok(hv[i], tag, true, true);
@@ -283,17 +292,24 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
             else __builtin_amdgcn_s_sleep(6);
           }
-          STAMP(1);
+          LSTAMP(1);
 #pragma unroll
           for (int i = 0; i < PL; ++i)
             *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
         }
+        LWSTAMP();
         __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
-        STAMP(2);
+        LSTAMP(2);
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
         if (IO) io_load(s + 1);
         read_gx();
+        // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
+        // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
+        // waves' cells following both MFMA streams (same box, alternating: c3 12.06 -> 11.99,
+        // c2 4.95 -> 4.79 ms/step).  A/B bits: 25 off; 26 the pollers first instead (no gain)
+        const bool first = IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
+        if (first) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) {
           const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
@@ -304,7 +320,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag, acc[t], 0, 0, 0);
           }
         }
-        STAMP(3);
+        if (first) __builtin_amdgcn_s_setprio(0);
+        LSTAMP(3);
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
       char* ob = outr + (s & 1) * 16 * OUB + bi * OUB;
@@ -337,10 +354,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
                     pack_bf16(hvals[t], h1, h2, h3, tag), same_xcd);
         }
       }
-      STAMP(4);
+      LSTAMP(4);
       if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(5);
+        LSTAMP(5);
       }
       // Behind the publish, off the hand-off's path: the io waves store step s-1's saved
       // activations (right after the barrier they delayed the io waves' own publish: 4.2 vs
@@ -355,21 +372,22 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
         of[u] = c[t]; of[HJ + u] = hvals[t];
       }
-      STAMP(6);
+      LSTAMP(6);
       // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
       // waves 4-5 instead, they held the barrier: 1.38 vs 1.33 ms per forward launch at c3;
       // spread over all four poller waves, one Philox call each: no change, 11.82 vs 11.73 ms
       // per step).  Tried and reverted as well (same box, c3 12.60-12.73 -> 12.78-12.92 ms):
       // io waves waiting for their gx LDS-DMA alone by a counted vmcnt (their stores left in
       // flight across the barrier), and the BPTT's dG stores moved behind the next poll.
-      if (!IO && a.Ydb && tid < NC8) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
-      STAMP(7);
+      if (!IO && a.Ydb && tid < NC8 && (!late_bits || s + 1 == T)) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
+      LSTAMP(7);
     }
     __syncthreads();
     if (IO) io_store(T - 1);
   };
   if (io) run(std::true_type{});
   else run(std::false_type{});
+  LSTAMP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -695,6 +713,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int CPG = 2 * HJ / 64;            // (unit, utterance-half) combos per 8-lane group
   static_assert(NPL >= 1 && CPG >= 1 && NPL * CPG == 2, "two 16-byte partial loads per lane");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  LSTAMP_DECL;
   char* aimg = smem;  // [2][16][4HJ] bf16 own dG, gate-major k = g*HJ + u, swizzled slots
   bf16x8* wlds = reinterpret_cast<bf16x8*>(smem + 2 * AIMG);  // [wave][NTW][KLB][lane]
   // cell inputs of a step, staged: [2][16 utt][ gates fp16 4*HJ (+16 B) | c_{t-1} HJ | dy HJ (fp32, +32 B) ]
@@ -834,7 +853,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const float g8s = (F8 && a.dG8) ? *a.g8scale : 0.f;       // fp8 mode: this step's dG scale
 
   auto step = [&](int s) -> bool {
-    STAMP(0);
+    LSTAMP(0);
     // this step's cell inputs (staged in LDS last step) into registers before the poll, so
     // the LDS latency hides behind the hand-off wait
     float xi[CPG], xf[CPG], xgg[CPG], xo[CPG], xcp[CPG], xdy[CPG];
@@ -878,14 +897,15 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         else __builtin_amdgcn_s_sleep(1);
       }
     }
-    STAMP(1);
+    LSTAMP(1);
+    LWSTAMP();
     // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
     // s+2's loads issued right behind this step's hand-off -- one program point per step, so
     // the loaded registers need no merge (and no wait for the loads)
     stage_cell(s + 1);
-    STAMP(5);
+    LSTAMP(5);
     load_cell(s + 2);
-    STAMP(6);
+    LSTAMP(6);
     if (s > 0) {
       const bool b2 = pg & 4, b1 = pg & 2, b0 = pg & 1;
 #pragma unroll
@@ -918,7 +938,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         dh[ci] = keep + dpp_f<0xB1>(send);
       }
     }
-    STAMP(2);
+    LSTAMP(2);
     // cell BPTT -> dG of (utterance cu, unit uc), into the A-image of this step
     char* ab = aimg + (s & 1) * AIMG;
 #pragma unroll
@@ -947,7 +967,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
     }
     __syncthreads();  // double-buffered A-image: one barrier per step
-    STAMP(3);
+    LSTAMP(3);
     if (abort_flag) return false;
     if (s + 1 < T) {
       f32x4 acc[NTW];
@@ -975,7 +995,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
                 pack_bf16(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], tag), same_xcd);
       }
     }
-    STAMP(4);
+    LSTAMP(4);
     // dG of this step for the weight-gradient GEMMs: 16-byte rows out of the A-image
     // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|)
     if (!(a.dbg_mode & 1)) {
@@ -1009,6 +1029,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   };
   for (int s = 0; s < T; ++s)
     if (!step(s)) break;
+  LSTAMP_FLUSH();
   if constexpr (F8) {  // this launch's max |dG| (the next step's fp8 scale): one atomic per wave
     float m = g8max;
 #pragma unroll
@@ -1176,6 +1197,8 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   unsigned long long* dbg, int dbg_mode, const WideFp8& f8) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return -1;
+  // the kernels address a batch group's rows through one buffer descriptor (32-bit offsets)
+  if ((size_t)BG * T * 8 * H * 2 > 0xffffffffull || (size_t)BG * T * 2 * H * 4 > 0xffffffffull) return -1;
   if (!xbuf || xbytes < p.xbytes || !err) {
     mlvae_set_error("lstm_wide: exchange workspace too small (need %zu B)", p.xbytes);
     return 1;

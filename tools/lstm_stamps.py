@@ -3,9 +3,11 @@ stamps s_memtime at the kernel's STAMP(0..4) points; ticks are shader cycles).
 
     python tools/lstm_stamps.py [--B 256] [--T 500] [--bwd] [--mode N]
 
-Phases (batch-group and wide kernels alike):
-  fwd: 0 step start | 1 poll done | 2 barrier / reduce | 3 MFMA done | 4 cell + publish done
-  bwd: 0 step start | 1 poll done | 2 reduce done | 3 barrier | 4 MFMA + publish done
+Phases (wide kernels; stamps of steps 64..95 buffered in LDS, lstm_common.h LSTAMP):
+  fwd: 0 step start | 1 poll done | 2 barrier | 3 MFMA issued | 4 cell + publish | 6 out ring |
+       7 drop bits (5: publish ack, debug bit 23)
+  bwd: 0 step start | 1 poll done | 5 cell inputs staged | 6 prefetch issued | 2 reduce done |
+       3 barrier | 4 MFMA + publish
 """
 import argparse
 import ctypes
@@ -70,32 +72,27 @@ def main():
     lib().mlvae_lstm_set_debug(None)
     lib().mlvae_lstm_set_debug_mode(0)
     d = dbg.view(T, 16).cpu().double()
-    names = (["poll", "reduce", "barrier", "mfma+publish"] if a.bwd else
-             ["poll", "barrier", "mfma", "cell+publish"])
-    for b, nm in zip(range(1, 5), names):
-        dd = d[2:, b] - d[2:, b - 1]
-        print(f"{nm:14s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
-    # every stamp as an offset from the step start (extra stamps 5..7: see the STAMP sites)
-    offs = [f"{b}:{(d[2:T - 1, b] - d[2:T - 1, 0]).median().item():.0f}" for b in range(1, 8)
-            if (d[2:T - 1, b] != 0).all()]
-    print("offsets from step start (median ticks) " + " ".join(offs))
-    per = d[3:T - 1, 0] - d[2:T - 2, 0]     # step start to step start: the whole period
-    tail = per - (d[2:T - 2, 4] - d[2:T - 2, 0])
-    print(f"{'tail':14s} median {tail.median().item():8.0f} ticks  mean {tail.mean().item():8.0f}")
-    print(f"{'step period':14s} median {per.median().item():8.0f} ticks  mean {per.mean().item():8.0f}")
-    if a.mode & (1 << 22):  # interleaved forward: chain 1's stamps sit at slots 8..12
-        for b, nm in zip(range(9, 13), names):
-            dd = d[2:, b] - d[2:, b - 1]
-            print(f"c1 {nm:11s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
-        print(f"{'c0 end->c1':14s} median {(d[2:, 8] - d[2:, 4]).median().item():8.0f}")
-    if a.mode & (1 << 23):  # publish -> own stores acknowledged (slot 5)
-        dd = d[2:, 5] - d[2:, 4]
-        print(f"{'publish ack':14s} median {dd.median().item():8.0f} ticks  mean {dd.mean().item():8.0f}")
-    nxt = d[3:, 0] - d[2:-1, 4]
-    print(f"{'tail->next':14s} median {nxt.median().item():8.0f}")
-    tot = d[3:, 0] - d[2:-1, 0]
-    print(f"{'step total':14s} median {tot.median().item():8.0f} ticks")
-
+    # the wide kernels stamp steps [STW0, STW0 + STWN) into LDS (lstm_common.h LSTAMP)
+    w0, wn = 64, 32
+    w = d[w0:w0 + wn]
+    names = ({1: "poll done", 5: "cell inputs staged", 6: "prefetch issued", 2: "reduce done",
+              3: "barrier", 4: "MFMA + publish"} if a.bwd else
+             {1: "poll done", 2: "barrier", 3: "MFMA issued", 4: "cell + publish", 5: "publish ack",
+              6: "out ring", 7: "drop bits"})
+    order = sorted((b for b in names if (w[:, b] != 0).all()),
+                   key=lambda b: (w[:, b] - w[:, 0]).median().item())
+    prev = 0.0
+    for b in order:
+        off = (w[:, b] - w[:, 0]).median().item()
+        print(f"{names[b]:20s} at {off:7.0f} ticks from the step start  (+{off - prev:6.0f})")
+        prev = off
+    wv = [(w[:, 8 + k] - w[:, 0]).median().item() for k in range(8) if (w[:, 8 + k] != 0).all()]
+    if wv:
+        print("per-wave poll done   " + " ".join(f"w{k}:{v:.0f}" for k, v in enumerate(wv)))
+    per = w[1:, 0] - w[:-1, 0]
+    print(f"{'step period':20s} median {per.median().item():7.0f} ticks  mean {per.mean().item():7.0f}")
+    last = order[-1] if order else 0
+    print(f"{'tail (last -> next)':20s} median {(w[1:, 0] - w[:-1, last]).median().item():7.0f}")
 
 if __name__ == "__main__":
     main()
