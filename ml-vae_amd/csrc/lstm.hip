@@ -821,6 +821,103 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// fp32 BPTT past the persistent kernels' register budget (the gather form holds a quarter of
+// the 4H-wide dG operand per wave in registers: H <= 512 in fp32).  The parity mode has no
+// such limit in nn.LSTM (ref:src/modules/decoder.py:14-15), so larger H run one launch per
+// step: the launch boundary is the hand-off.  Block = (64 units, 16 utterances, direction),
+// 256 threads = 64 units x 4 k-quarters; dG of the previously processed step is staged through
+// LDS in 256-wide k chunks and multiplied by coalesced W_hh rows.  dG overwrites the gates in
+// place (as the persistent kernels do); dc, the cell gradient carried between steps, lives in
+// the caller's workspace.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lstm_bwd_step_f32(int B, int T, int H, int ndir, int s,
+                                                         const float* W0, const float* W1, float* G,
+                                                         const float* Cs, const float* Y, float* dcbuf,
+                                                         unsigned short* dGb) {
+  __shared__ float dgp[16][257];
+  __shared__ float red[4][16][65];
+  const int dir = blockIdx.z, b0 = blockIdx.y * 16, j0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, jl = tid & 63, kq = tid >> 6;
+  const int j = j0 + jl, K4 = 4 * H;
+  const float* W = dir ? W1 : W0;
+  const int t = dir ? s : T - 1 - s;
+  const int tq = dir ? t - 1 : t + 1;  // the step processed before this one
+  const size_t gld = (size_t)K4 * ndir, yld = (size_t)H * ndir;
+  float acc[16];
+#pragma unroll
+  for (int bl = 0; bl < 16; ++bl) acc[bl] = 0.f;
+  if (s > 0) {
+    for (int k0 = 0; k0 < K4; k0 += 256) {
+      for (int e = tid; e < 16 * 256; e += 256) {
+        const int bl = e >> 8, kk = e & 255, b = b0 + bl;
+        dgp[bl][kk] = (b < B && k0 + kk < K4) ? G[((size_t)b * T + tq) * gld + (size_t)dir * K4 + k0 + kk] : 0.f;
+      }
+      __syncthreads();
+      if (j < H) {
+        const int kend = min(64, K4 - k0 - kq * 64);
+        for (int kk = 0; kk < kend; ++kk) {
+          const float w = W[(size_t)(k0 + kq * 64 + kk) * H + j];
+#pragma unroll
+          for (int bl = 0; bl < 16; ++bl) acc[bl] += dgp[bl][kq * 64 + kk] * w;
+        }
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int bl = 0; bl < 16; ++bl) red[kq][bl][jl] = acc[bl];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int idx = tid + 256 * r, bl = idx >> 6, ju = idx & 63;
+    const int b = b0 + bl, jj = j0 + ju;
+    if (b >= B || jj >= H) continue;
+    const float dhrec = red[0][bl][ju] + red[1][bl][ju] + red[2][bl][ju] + red[3][bl][ju];
+    const size_t n = (size_t)b * T + t;
+    float* gp = G + n * gld + (size_t)dir * K4 + jj;
+    const float gi = gp[0], gf = gp[H], gg = gp[2 * H], go = gp[3 * H];
+    const float cc = Cs[n * yld + (size_t)dir * H + jj];
+    const int tp = dir ? t + 1 : t - 1;  // the cell's previous step in forward time
+    const float cp = (tp >= 0 && tp < T) ? Cs[((size_t)b * T + tp) * yld + (size_t)dir * H + jj] : 0.f;
+    float* dcp = dcbuf + ((size_t)dir * B + b) * H + jj;
+    const float dcv = s > 0 ? *dcp : 0.f;
+    const float dh = Y[n * yld + (size_t)dir * H + jj] + dhrec;
+    const float tc = tanhf(cc);
+    const float d_o = dh * tc;
+    const float dcs = dcv + dh * go * (1.f - tc * tc);
+    *dcp = dcs * gf;
+    const float dgi = dcs * gg * gi * (1.f - gi), dgf = dcs * cp * gf * (1.f - gf);
+    const float dgg = dcs * gi * (1.f - gg * gg), dgo = d_o * go * (1.f - go);
+    gp[0] = dgi; gp[H] = dgf; gp[2 * H] = dgg; gp[3 * H] = dgo;
+    if (dGb) {
+      unsigned short* gb = dGb + n * gld + (size_t)dir * K4 + jj;
+      gb[0] = (unsigned short)f2bf(dgi); gb[H] = (unsigned short)f2bf(dgf);
+      gb[2 * H] = (unsigned short)f2bf(dgg); gb[3 * H] = (unsigned short)f2bf(dgo);
+    }
+  }
+}
+
+// fp32 gather-form BPTT holds 4H / (4 x 16) operand loads per wave: more than 32 -> stepwise
+bool use_stepwise_bwd(int H, int prec) { return prec == PREC_F32 && H > 512; }
+
+int run_bwd_stepwise(int B, int T, int H, int ndir, const float* W0, const float* W1, float* G,
+                     const float* Cs, const float* Y, void* xbuf, size_t xbytes, unsigned short* dgb,
+                     hipStream_t st) {
+  const size_t need = (size_t)ndir * B * H * sizeof(float);
+  if (!xbuf || xbytes < need) {
+    mlvae_set_error("lstm: exchange workspace too small (need %zu B)", need);
+    return 1;
+  }
+  float* dc = static_cast<float*>(xbuf);
+  const dim3 grid((H + 63) / 64, (B + 15) / 16, ndir);
+  for (int s = 0; s < T; ++s) {
+    lstm_bwd_step_f32<<<grid, 256, 0, st>>>(B, T, H, ndir, s, W0, W1, G, Cs, Y, dc, dgb);
+    MLVAE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 unsigned long long* g_dbg = nullptr;
 // debug / A-B bits of the recurrence kernels (mlvae_lstm_set_debug_mode); MLVAE_LSTM_DBG sets
 // the initial value so a whole bench run can be timed under one variant
@@ -985,6 +1082,7 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     mlvae_set_error("lstm: fused dropout / bias-gradient outputs, Y = NULL only on the wide-batch path");
     return 1;
   }
+  if (!fwd && use_stepwise_bwd(H, prec)) return run_bwd_stepwise(B, T, H, ndir, W0, W1, G, Cs, Y, xbuf, xbytes, dgb, st);
   const int bmax = max_batch_per_launch(H, fwd, prec);
   if (bmax < BG) { mlvae_set_error("lstm: H=%d too large for one resident launch", H); return 1; }
   Plan full = make_plan(bmax < B ? bmax : B, H, prec, fwd);
@@ -1045,6 +1143,8 @@ extern "C" int mlvae_lstm_workspace_size(int B, int H, int prec, size_t* xbytes)
   Plan pf = make_plan(bf < B ? bf : B, H, prec, true);
   Plan pb = make_plan(bb < B ? bb : B, H, prec, false);
   *xbytes = pf.xbytes_fwd > pb.xbytes_bwd ? pf.xbytes_fwd : pb.xbytes_bwd;
+  if (use_stepwise_bwd(H, prec) && (size_t)2 * B * H * sizeof(float) > *xbytes)
+    *xbytes = (size_t)2 * B * H * sizeof(float);  // the stepwise BPTT's dc state
   if (prec == PREC_BF16) {  // the wide-batch kernels' exchange (used past one launch's batch)
     const size_t wf = lstm_wide_xbytes(B, H, true), wb = lstm_wide_xbytes(B, H, false);
     if (wf > *xbytes) *xbytes = wf;
