@@ -272,9 +272,18 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           const unsigned ebase = (unsigned)(((s - 1) & nmask) * xslot) + bi * H + wave * PL * 32 + 8 * q;
           u32x4 hv[PL];
           unsigned spins = 0;
+          // When the grid fills the chip, retries re-load only the chunks whose tags were stale,
+          // with a shorter back-off (s_sleep 2 instead of 6): less L2 poll traffic per retry and
+          // a finer retry period (same box, alternating: c3 12.15 -> 11.77 and 12.19 -> 11.98
+          // ms/step; at c2's 128 workgroups full sweeps with s_sleep 6 stay 1 % faster).  A/B
+          // bit 28: full re-loads with s_sleep 6 at every size; bit 30: s_sleep 1
+          const bool partial = (int)gridDim.x >= 256 && !(a.dbg_mode & (1 << 28));
+#pragma unroll
+          for (int i = 0; i < PL; ++i) hv[i] = u32x4{tag ^ 1u, 0u, tag ^ 1u, 0u};  // stale: first sweep loads all
           while (true) {
 #pragma unroll
-            for (int i = 0; i < PL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
+            for (int i = 0; i < PL; ++i)
+              if (!partial || !tags_ok(hv[i], tag, true, true)) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
             // step s-1's dropout keep bits, drawn while the first poll's loads are in flight
             // (drawn before them, at the end of step s-1, they delayed the poll's issue; with the
             // io-first MFMAs: c3 12.06 -> 11.92, c2 4.95 -> 4.72 ms/step).  A/B bit 27: the old place
@@ -289,7 +298,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             }
             // a longer back-off thins the L2 poll traffic (3.27 -> 3.20 us/step at B = 256);
             // bit 18: the previous s_sleep(2)
-            if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
+            if (partial && (a.dbg_mode & (1 << 30))) __builtin_amdgcn_s_sleep(1);
+            else if (partial || (a.dbg_mode & 262144)) __builtin_amdgcn_s_sleep(2);
             else __builtin_amdgcn_s_sleep(6);
           }
           LSTAMP(1);
@@ -873,6 +883,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       const unsigned tag = step_tag_lg(s - 1, nlg);
       const size_t sb = (size_t)((s - 1) & nmask) * xslot + (size_t)js * NJ * HJ * 16;
       unsigned spins = 0;
+      // (re-loading only the stale partial tiles measured no faster here: full sweeps)
       while (true) {
 #pragma unroll
         for (int ci = 0; ci < CPG; ++ci)
