@@ -915,7 +915,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     // the loaded registers need no merge (and no wait for the loads)
     stage_cell(s + 1);
     LSTAMP(5);
-    load_cell(s + 2);
+    // At full-chip grids the prefetch is issued after the barrier, so no wave's HBM loads sit in
+    // the CU's memory queue ahead of a later wave's poll loads (same box: c3 12.11 -> 11.99
+    // ms/step; at c2's 128 workgroups right after the poll stays 2 % faster).  A/B bit 16:
+    // right after the poll at every size.  (The io waves' stores issued before their MFMAs
+    // instead of behind their publish, in the forward: c3 12.11 -> 12.48, c2 4.97 -> 5.62.)
+    const bool late_pf = (int)gridDim.x >= 256 && !(a.dbg_mode & (1 << 16));
+    if (!late_pf) load_cell(s + 2);
     LSTAMP(6);
     if (s > 0) {
       const bool b2 = pg & 4, b1 = pg & 2, b0 = pg & 1;
@@ -978,6 +984,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
     }
     __syncthreads();  // double-buffered A-image: one barrier per step
+    if (late_pf) load_cell(s + 2);
     LSTAMP(3);
     if (abort_flag) return false;
     if (s + 1 < T) {
