@@ -32,3 +32,14 @@ def test_abi_version_and_error_channel():
     rc = l.mlvae_gemm(7, 0, 0, 4, 4, 4, 1.0, None, 4, None, 4, 0.0, 1, 4, None, None, 0, None, 0,
                       0, 0, None, 0, None)
     assert rc == 1 and "prec" in _lib.last_error()
+
+
+def test_lstm_workspace_covers_the_stepwise_fp32_bptt():
+    """fp32 past H = 512: the stepwise BPTT keeps the cell gradient [2, B, H] in the workspace
+    (host-side sizing only, no GPU call)."""
+    import ctypes
+    from mlvae_hip._lib import lib
+    for B, H in ((5, 1024), (64, 2048)):
+        xb = ctypes.c_size_t()
+        assert lib().mlvae_lstm_workspace_size(B, H, 0, ctypes.byref(xb)) == 0
+        assert xb.value >= 2 * B * H * 4
