@@ -152,6 +152,13 @@ int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, con
                        void* gates, int gates_fp16, const float* cells, const float* dy,
                        void* dg_bf16, float* dbias_rows, void* xbuf, size_t xbytes, int* err,
                        void* stream);
+/* bwd_ex3: bwd_ex2 with dy given as bf16 [B*T, 2H] when dy_bf16 = 1 (wide path only: gates_fp16 = 1;
+ *   not with the fp8 BPTT) -- the fused engine's heads and dgrad GEMMs write dY in bf16, halving
+ *   its bytes in their epilogues and in the BPTT's cell-input stream.  dy_bf16 = 0: bwd_ex2. */
+int mlvae_lstm_bwd_ex3(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                       void* gates, int gates_fp16, const float* cells, const void* dy, int dy_bf16,
+                       void* dg_bf16, float* dbias_rows, void* xbuf, size_t xbytes, int* err,
+                       void* stream);
 /* fp8 mode (BASELINE.json configs[4]) of the wide-batch recurrences (gates_fp16 shapes, bf16):
  *   fwd: as mlvae_lstm_fwd_ex2 without the fp32 h, plus y_drop_fp8 = e4m3(dropout(h) * x8_scale):
  *        the next layer's fp8 input-projection operand, written by the recurrence itself
@@ -303,7 +310,8 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
  * With bias_ws and saved_bf16 in train mode the work runs in split form: P1 and dY as 256^2
  * GEMMs (bias + LReLU + bf16 epilogue; fp32 dY) around a persistent kernel for the middle stages
  * (same outputs; mlvae_heads_set_mode(1) or MLVAE_HEADS_FUSED=1 keeps the single fused kernel,
- * for A/B timing; returns the previous mode). */
+ * for A/B timing; returns the previous mode).  saved_bf16 bit 1 (value 3): the split form writes
+ * dY as bf16 [N, 2H] (mlvae_lstm_bwd_ex3's dy_bf16 input); an error without the split form. */
 size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C);
 int mlvae_heads_set_mode(int mode);
 int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,

@@ -544,7 +544,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
     const int row = (int)(idx / g.N), col = (int)(idx % g.N);
     if (g.bias1) s += g.bias1[col];
     if (g.bias2) s += g.bias2[col];
-    if (g.c16) {  // beta == 0, epi NONE / DROPOUT (fp16) or NONE / LRELU (bf16) (checked on the host)
+    if (g.c16) {  // beta == 0, epi NONE / DROPOUT (fp16) or NONE / LRELU / DROPOUT (bf16) (checked on the host)
       if (g.epi == EPI_DROPOUT) s *= dropout_scale(g.dseed, g.doff + (size_t)row * g.ldc + col, g.dkeep, g.dscale);
       if (g.epi == EPI_LRELU) s = lrelu(s);
       reinterpret_cast<unsigned short*>(Cb)[(size_t)row * g.ldc + col] =
@@ -666,9 +666,9 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   const int c16 = (epi & EPI_OUT_BF16) ? 2 : ((epi & EPI_OUT_F16) ? 1 : 0);
   epi &= ~(EPI_OUT_F16 | EPI_OUT_BF16);
   if (c16 && (beta != 0.f || (c16 == 1 && epi != EPI_NONE && epi != EPI_DROPOUT) ||
-              (c16 == 2 && epi != EPI_NONE && epi != EPI_LRELU) || N % 4 || ldc % 4 ||
+              (c16 == 2 && epi != EPI_NONE && epi != EPI_LRELU && epi != EPI_DROPOUT) || N % 4 || ldc % 4 ||
               ((uintptr_t)C % 16) || (c_bstride % 8) || ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16))) {
-    mlvae_set_error("mlvae_gemm_bf16: 16-bit C needs beta 0, epilogue none/dropout (fp16) or none/lrelu (bf16), "
+    mlvae_set_error("mlvae_gemm_bf16: 16-bit C needs beta 0, epilogue none/dropout (fp16) or none/lrelu/dropout (bf16), "
                     "N and ldc %% 4, aligned C/bias");
     return 1;
   }

@@ -820,7 +820,8 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
   a.P1 = p1; a.P2[0] = p2m; a.P2[1] = p2v; a.OUT[0] = mux; a.OUT[1] = lvx;
   a.dOUT[0] = dmux; a.dOUT[1] = dlvx; a.dP2[0] = dp2m; a.dP2[1] = dp2v; a.dP1 = dp1; a.dY = dy;
   a.partials = partials;
-  a.sbf = saved_bf16 ? 1 : 0;
+  a.sbf = (saved_bf16 & 1) ? 1 : 0;
+  const bool dy_bf16 = (saved_bf16 & 2) != 0;  // split form: dY written as bf16 [N, H2]
   a.bias_ws = nullptr;
   if (bias_ws) {  // the five bias gradients from in-kernel column sums (train only)
     const bool mse = loss_type == 1;
@@ -834,7 +835,12 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
   }
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  if (train && bias_ws && saved_bf16 && !heads_fused_only()) {
+  const bool split = train && bias_ws && (saved_bf16 & 1) && !heads_fused_only();
+  if (dy_bf16 && !split) {
+    mlvae_set_error("heads: bf16 dY (saved_bf16 bit 1) needs the split form (train, bias_ws, saved_bf16 bit 0)");
+    return 1;
+  }
+  if (split) {
     // split form: P1 GEMM, the persistent middle stages, dY GEMM (heads_mid_kernel comment)
     constexpr int EPI_LRELU_BF16 = 1 | 32;  // gemm_fast.hip: EPI_LRELU | EPI_OUT_BF16
     rc = mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
@@ -843,7 +849,8 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
     rc = F == 80 ? launch_mid<64, 80>(a, st) : launch_mid<64, 64>(a, st);
     if (rc) return rc;
     rc = mlvae_gemm_bf16(0, 1, a.N, H2, 2 * C, 1, dp1, 2 * C, 0, w1t_bf16, 2 * C, 0, dy, H2, 0, 0.f, nullptr,
-                         nullptr, 0, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
+                         nullptr, dy_bf16 ? 32 : 0 /* EPI_OUT_BF16 */, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f,
+                         nullptr, 0, stream);
   } else {
     rc = F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
   }

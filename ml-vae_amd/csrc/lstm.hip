@@ -1055,6 +1055,7 @@ struct WideExtra {  // outputs only the wide kernels write
   unsigned long long seed = 0, off = 0;
   float p = 0.f;
   WideFp8 f8;                     // fp8 mode: e4m3 dropout(h) / dG copies, dG amax
+  const unsigned short* dyb = nullptr;  // backward: dY as bf16 (Y unused)
 };
 
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
@@ -1076,8 +1077,9 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     if (!fwd && !dgb) { mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 (NULL)"); return 1; }
     if (ex.ydb && !(ex.p >= 0.f && ex.p < 1.f)) { mlvae_set_error("lstm: dropout p=%g", ex.p); return 1; }
     return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.dbias, ex.ydb,
-                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode, ex.f8);
+                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode, ex.f8, ex.dyb);
   }
+  if (ex.dyb) { mlvae_set_error("lstm: bf16 dY only on the wide-batch path (fp16 gates)"); return 1; }
   if (ex.ydb || ex.dbias || !Y) {
     mlvae_set_error("lstm: fused dropout / bias-gradient outputs, Y = NULL only on the wide-batch path");
     return 1;
@@ -1095,7 +1097,7 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
   for (int b0 = 0; b0 < B; b0 += bmax) {
     const int bc = B - b0 < bmax ? B - b0 : bmax;
     Plan p = make_plan(bc, H, prec, fwd);
-    LstmArgs a;
+    LstmArgs a{};
     a.B = bc; a.T = T; a.H = H; a.NB = p.NB; a.NJ = p.NJ; a.HJ = p.HJ; a.Kp = p.Kp; a.K4p = p.K4p;
     a.W0 = W0; a.W1 = W1;
     const size_t gld = (size_t)4 * H * ndir, yld = (size_t)H * ndir;  // row strides
@@ -1229,6 +1231,25 @@ extern "C" int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_
   return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
              const_cast<float*>(cells), const_cast<float*>(dy), xbuf, xbytes, err,
              (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), gates_fp16, ex);
+}
+
+// The wide-batch BPTT with dY as bf16 [B*T, 2H] (dy_bf16 = 1; the fused engine's heads and dgrad
+// write it so): half the dY bytes of mlvae_lstm_bwd_ex2.  dy_bf16 = 0 is mlvae_lstm_bwd_ex2.
+extern "C" int mlvae_lstm_bwd_ex3(int prec, int B, int T, int H, const float* w_hh_fwd,
+                                  const float* w_hh_rev, void* gates, int gates_fp16,
+                                  const float* cells, const void* dy, int dy_bf16, void* dg_bf16,
+                                  float* dbias_rows, void* xbuf, size_t xbytes, int* err,
+                                  void* stream) {
+  if (dy_bf16 && !gates_fp16) {
+    mlvae_set_error("lstm_bwd_ex3: bf16 dY needs the wide-batch path (fp16 gates)");
+    return 1;
+  }
+  WideExtra ex;
+  ex.dbias = dbias_rows;
+  if (dy_bf16) ex.dyb = static_cast<const unsigned short*>(dy);
+  return run(false, prec, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
+             const_cast<float*>(cells), dy_bf16 ? nullptr : static_cast<float*>(const_cast<void*>(dy)), xbuf,
+             xbytes, err, (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), gates_fp16, ex);
 }
 
 // Unidirectional layer (nn.LSTM(bidirectional=False)): gates [B*T, 4H] fp32 (in: x W_ih^T + b;

@@ -48,6 +48,7 @@ struct LstmArgs {
   unsigned char* dG8;
   const float* g8scale;
   unsigned* g8amax;
+  const unsigned short* dYb;  // wide BPTT, optional: dY as bf16 [B*T, 2H] instead of Y (fp32)
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -163,7 +164,8 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
-                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8 = WideFp8());
+                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8 = WideFp8(),
+                  const unsigned short* dyb = nullptr);
 // debug-mode bits the wide plans read (bit 21: one workgroup per CU, no two-per-CU plan)
 void lstm_wide_set_mode(int mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply

@@ -706,7 +706,9 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------------------
 // F8: the fp8 mode's e4m3 dG copy + amax (a separate instantiation: the bf16 path's registers
 // stay as they are)
-template <int TPW, int NKC, int OCC, bool F8 = false>  // HJ = 32 * TPW, H = 32 * NKC; OCC as fwd
+// DYB: dY (the layer output's gradient) arrives as bf16 (a.dYb) instead of fp32 (a.Y): half the
+// bytes in the cell-input stream (and in the producers' epilogues)
+template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false>  // HJ = 32 * TPW, H = 32 * NKC
 __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = 32 * TPW;
   constexpr int H = NKC * 32;
@@ -729,7 +731,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   // cell inputs of a step, staged: [2][16 utt][ gates fp16 4*HJ (+16 B) | c_{t-1} HJ | dy HJ (fp32, +32 B) ]
   constexpr int CG_B = 4 * HJ * 2 + 16;       // gate row bytes (padded: 8 utterances -> 32 banks)
   constexpr int CF_B = HJ * 4 + 32;           // c / dy row bytes (padded likewise)
-  constexpr int CUTT = CG_B + 2 * CF_B;       // bytes per utterance
+  // dy row bytes: bf16 rows padded so a row of the staged block is an odd multiple of 4 dwords
+  // past a bank period (HJ 32: 528 B, HJ 64: 976 B) -- 8 utterances' reads of one unit hit 8
+  // distinct banks (16 B of padding left HJ 32 at 512 B per row: 8-way conflicts, c2 +6 %)
+  constexpr int CD_B = DYB ? HJ * 2 + 32 : CF_B;
+  static_assert(((CG_B + CF_B + CD_B) / 4) % 8 == 4 || ((CG_B + CF_B + CD_B) / 4) % 64 == 20,
+                "conflict-free staged rows");
+  constexpr int CUTT = CG_B + CF_B + CD_B;    // bytes per utterance
   char* cst = smem + 2 * AIMG + (size_t)8 * NTW * KLB * 64 * 16;  // [2][16][CUTT]
   __shared__ int abort_flag;
 
@@ -793,22 +801,30 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   // per wave instruction instead of each lane's scattered words -- into registers, two steps
   // ahead; staged to LDS one step ahead (cst slot s_ & 1).  Chunks: 16 x 4 x HJ/8 gate chunks
   // (8 fp16 units), 16 x HJ/4 c chunks, 16 x HJ/4 dy chunks (4 fp32 units).
-  constexpr int NGC = 16 * 4 * HJ / 8, NFC = 16 * HJ / 4, NCH = NGC + 2 * NFC;
-  constexpr int CPT = NCH / 512;              // chunks per thread
-  static_assert(NCH % 512 == 0, "whole chunks per thread");
+  // dy chunks: fp32 4 units or bf16 8 units; chunks past NCH (bf16 dy) are dummies -- loaded from a
+  // valid address (unconditional loads, below) and never staged
+  constexpr int NGC = 16 * 4 * HJ / 8, NFC = 16 * HJ / 4, NDC = DYB ? 16 * HJ / 8 : NFC;
+  constexpr int NCH = NGC + NFC + NDC;
+  constexpr int CPT = (NCH + 511) / 512;      // chunks per thread
+  static_assert(DYB || NCH % 512 == 0, "whole chunks per thread");
+  static_assert(NGC % 64 == 0 && NFC % 64 == 0 && NDC % 64 == 0, "chunk kinds change at whole waves");
   const size_t gbase = (size_t)grp * BG * T;  // first row (utterance grp*16, t = 0) of the group
   const auto rG = make_rsrc(reinterpret_cast<const unsigned short*>(a.G) + gbase * 8 * H, 0xffffffffu);
   const auto rC = make_rsrc(a.Cs + gbase * 2 * H, 0xffffffffu);
-  const auto rY = make_rsrc(a.Y + gbase * 2 * H, 0xffffffffu);
+  const auto rY = DYB ? make_rsrc(a.dYb + gbase * 2 * H, 0xffffffffu) : make_rsrc(a.Y + gbase * 2 * H, 0xffffffffu);
   u32x4 creg[CPT];
   auto chunk_lds = [&](int c) -> int {  // LDS byte offset of chunk c within a slot
     if (c < NGC) {
       const int u = c / (4 * HJ / 8), k = c % (4 * HJ / 8);
       return u * CUTT + k * 16;
     }
-    const int f = c - NGC, which = f / NFC, r = f % NFC;
-    const int u = r / (HJ / 4), k = r % (HJ / 4);
-    return u * CUTT + CG_B + which * CF_B + k * 16;
+    const int f = c - NGC;
+    if (f < NFC) {
+      const int u = f / (HJ / 4), k = f % (HJ / 4);
+      return u * CUTT + CG_B + k * 16;
+    }
+    const int r = f - NFC, upr = DYB ? HJ / 8 : HJ / 4;  // dy chunks per utterance row
+    return (r / upr) * CUTT + CG_B + CF_B + (r % upr) * 16;
   };
   // Unconditional loads (steps past the end and padded utterances read a clamped valid row and
   // are never consumed): a conditional load would make the compiler merge the register values
@@ -822,15 +838,18 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     const int tpc = tp_ < 0 ? 0 : (tp_ >= T ? T - 1 : tp_);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int cw = wave * 64 + 512 * i;  // first chunk of this wave (uniform)
+      const int cw0 = wave * 64 + 512 * i;  // first chunk of this wave (uniform)
+      const int cw = cw0 < NCH ? cw0 : 0;   // dummy chunks (bf16 dy) re-load chunk 0's row
       const int c = cw + lane;
       const bool isg = cw < NGC, ydy = cw - NGC >= NFC;  // uniform: gates, c, dy chunks
       const int r = c - NGC - (ydy ? NFC : 0);
       const int ug = c / (4 * HJ / 8), k = c % (4 * HJ / 8), g = k / (HJ / 8), ugu = (k % (HJ / 8)) * 8;
-      const int uf = r / (HJ / 4), ufu = (r % (HJ / 4)) * 4;
+      const int upr = (ydy && DYB) ? HJ / 8 : HJ / 4, epr = (ydy && DYB) ? 8 : 4;  // chunks / units
+      const int uf = r / upr, ufu = (r % upr) * epr;
       const int u = min(isg ? ug : uf, ulast);
       const unsigned og = ((unsigned)(u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + ugu) * 2u;
-      const unsigned of = ((unsigned)(u * T + (ydy ? t_ : tpc)) * 2 * H + dir * H + j0 + ufu) * 4u;
+      const unsigned of = ((unsigned)(u * T + (ydy ? t_ : tpc)) * 2 * H + dir * H + j0 + ufu) *
+                          ((ydy && DYB) ? 2u : 4u);
       creg[i] = __builtin_bit_cast(
           u32x4, __builtin_amdgcn_raw_buffer_load_b128(isg ? rG : (ydy ? rY : rC), isg ? og : of, 0, NT_AUX));
     }
@@ -839,7 +858,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     char* dst = cst + (s_ & 1) * 16 * CUTT;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      *reinterpret_cast<u32x4*>(dst + chunk_lds(wave * 64 + 512 * i + lane)) = creg[i];
+      if (wave * 64 + 512 * i < NCH)  // (uniform) dummies are not staged
+        *reinterpret_cast<u32x4*>(dst + chunk_lds(wave * 64 + 512 * i + lane)) = creg[i];
     }
   };
   float dc[CPG], cc[CPG], bsum[CPG][4];
@@ -873,7 +893,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       const unsigned short* xg = reinterpret_cast<const unsigned short*>(cu_row) + uc[ci];
       xi[ci] = h2f(xg[0]); xf[ci] = h2f(xg[HJ]); xgg[ci] = h2f(xg[2 * HJ]); xo[ci] = h2f(xg[3 * HJ]);
       xcp[ci] = reinterpret_cast<const float*>(cu_row + CG_B)[uc[ci]];
-      xdy[ci] = reinterpret_cast<const float*>(cu_row + CG_B + CF_B)[uc[ci]];
+      if constexpr (DYB)
+        xdy[ci] = __uint_as_float((unsigned)reinterpret_cast<const unsigned short*>(cu_row + CG_B + CF_B)[uc[ci]] << 16);
+      else
+        xdy[ci] = reinterpret_cast<const float*>(cu_row + CG_B + CF_B)[uc[ci]];
     }
     float dh[CPG];
 #pragma unroll
@@ -1170,7 +1193,9 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC>
-               : (a.g8amax ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true> : lstm_bwd_wide_kernel<TPW, NKC, OCC, false>);
+               : (a.g8amax ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true>
+                           : (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true>
+                                    : lstm_bwd_wide_kernel<TPW, NKC, OCC, false>));
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
     mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
     return 2;
@@ -1212,7 +1237,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
-                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8) {
+                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8, const unsigned short* dyb) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return -1;
   // the kernels address a batch group's rows through one buffer descriptor (32-bit offsets)
@@ -1228,6 +1253,11 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;
   a.dbias = dbias; a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
   a.Y8 = f8.y8; a.x8scale = f8.x8scale; a.dG8 = f8.dg8; a.g8scale = f8.g8scale; a.g8amax = f8.g8amax;
+  a.dYb = fwd ? nullptr : dyb;
+  if (a.dYb && a.g8amax) {
+    mlvae_set_error("lstm_wide: bf16 dY with the fp8 BPTT is not supported (fp8 mode keeps fp32 dY)");
+    return 1;
+  }
   if (a.Y8 && (!ydb || p.il)) {
     mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one (one-group forward)");
     return 1;

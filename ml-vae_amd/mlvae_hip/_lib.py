@@ -58,6 +58,7 @@ _SIGS = {
     "mlvae_lstm_gates_fp16": [I, I, I],
     "mlvae_lstm_fwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_bwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, P, SZ, P, P],
+    "mlvae_lstm_bwd_ex3": [I, I, I, I, P, P, P, I, P, P, I, P, P, P, SZ, P, P],
     "mlvae_elbo_partials_count": [I, I, I],
     "mlvae_heads_partials_count": [I, I],
     "mlvae_heads_supported": [I, I, I],

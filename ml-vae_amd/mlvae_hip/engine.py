@@ -31,6 +31,7 @@ PREC = {"fp32": 0, "bf16": 1}
 LOSS = {"likelihood": 0, "mse": 1}
 EPI_NONE, EPI_LRELU, EPI_DLRELU, EPI_DROPOUT = 0, 1, 2, 3
 EPI_OUT_F16 = 16  # flag: mlvae_gemm_bf16 stores C as fp16
+EPI_OUT_BF16 = 32  # flag: mlvae_gemm_bf16 stores C as bf16
 G8_MARGIN = 2.0   # fp8 mode: headroom of the delayed dG scale over the previous step's amax
 
 
@@ -349,6 +350,11 @@ class VAEEngine:
         # fused heads: in-kernel bias sums + bf16 saved intermediates (MLVAE_HEADS_BSUM=0: the
         # colsum passes over fp32 intermediates, for same-box A/B)
         self.heads_bias_sums = os.environ.get("MLVAE_HEADS_BSUM", "1") != "0"
+        # dY (the layer outputs' gradients) in bf16 where its producers can write it: the heads'
+        # split form and the bf16 dgrad, into the wide-batch BPTT (mlvae_lstm_bwd_ex3); the fp8
+        # mode keeps fp32 dY (its dgrad epilogue writes fp32).  MLVAE_DY_BF16=0: fp32 (A/B)
+        self.dy_bf16 = (cfg.prec == "bf16" and not cfg.fp8 and os.environ.get("MLVAE_DY_BF16", "1") != "0"
+                        and os.environ.get("MLVAE_HEADS_FUSED", "0") in ("", "0"))
         self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
                      if self.fused_heads else None)
         # bf16 mode: the encoder (+ reparameterisation + KL) runs as two fused kernels
@@ -538,13 +544,15 @@ class VAEEngine:
 
     def _fast(self, w, ta, tb, M, N, K, A_bf, lda, B_bf, ldb, C, ldc, batch=1, a_bs=0, b_bs=0,
               c_bs=0, bias1=None, bias2=None, kshift_T=0, kshift=0, kstep=0, drop_seed=None,
-              out_f16=False):
+              out_f16=False, out_bf16=False):
         """bf16 256² LDS-DMA GEMM (mlvae_gemm_bf16) over bf16 operands: the step's big products.
-        out_f16: C is fp16 (the wide recurrence's gate buffer)."""
+        out_f16: C is fp16 (the wide recurrence's gate buffer); out_bf16: C is bf16 (dY)."""
         ws = w.gws_side if self._on_side else w.gws
         epi, p = (EPI_DROPOUT, self.cfg.dropout) if drop_seed is not None else (EPI_NONE, 0.0)
         if out_f16:
             epi |= EPI_OUT_F16
+        if out_bf16:
+            epi |= EPI_OUT_BF16
         check(lib().mlvae_gemm_bf16(ta, tb, M, N, K, batch, A_bf, lda, a_bs, B_bf, ldb, b_bs, C, ldc,
                                     c_bs, 0.0, bias1, bias2, epi, None, 0, kshift_T, kshift, kstep,
                                     drop_seed or 0, self._drop_off, p, _p(ws), w.gws_bytes,
@@ -786,6 +794,9 @@ class VAEEngine:
             # (P1, P2, dOUT, dP2, dP1) are saved as bf16 -- their operand precision -- in the
             # fp32 buffers' memory (packed rows)
             w.heads_bias = bool(train) and w.heads_bws is not None and self.heads_bias_sums
+            # bf16 dY from the heads' split form, read by the wide BPTT (per-layer flags)
+            w.dy_bf16 = {li: False for li in range(cfg.L)}
+            w.dy_bf16[cfg.L - 1] = bool(self.dy_bf16 and w.heads_bias and w.g16)
             bias_args = (_p(w.heads_bws), w.heads_bws.numel() * 4, hg("mean_fc.blocks.4.bias"),
                          hg("log_var_fc.blocks.4.bias"), hg("mean_fc.blocks.2.bias"),
                          hg("log_var_fc.blocks.2.bias"), hg("mean_fc.blocks.0.bias")) \
@@ -802,7 +813,8 @@ class VAEEngine:
                   _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
                   _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
                   _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
-                  _p(w.ph), *bias_args, 1 if w.heads_bias else 0, s), "heads_fused")
+                  _p(w.ph), *bias_args, (3 if w.dy_bf16[cfg.L - 1] else 1) if w.heads_bias else 0, s),
+                  "heads_fused")
             check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w
@@ -972,9 +984,10 @@ class VAEEngine:
                                                am + 4 * par, _p(w.xbuf), w.xbuf.numel(), _p(self.err), s),
                           "lstm_bwd_fp8")
                 else:
-                    check(l.mlvae_lstm_bwd_ex2(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                    dyb = bool(getattr(w, "dy_bf16", {}).get(li, False))
+                    check(l.mlvae_lstm_bwd_ex3(PREC[cfg.prec], B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                               int(w.g16), _p(w.Cs[li]), _p(w.dY[li]),
+                                               int(w.g16), _p(w.Cs[li]), _p(w.dY[li]), int(dyb),
                                                _pb(dGb) if dGb is not None else None,
                                                _p(rows) if rows is not None else None,
                                                _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_bwd")
@@ -1062,11 +1075,15 @@ class VAEEngine:
                           "gemm_fp8_ex")
                 fused = epi8 == EPI_DROPOUT
             elif dG_bf is not None and li in self.wih_t and din >= 256:
-                # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy
+                # dX = dG W_ih as an NT product over the k-contiguous W_ih^T copy; dY of the layer
+                # below in bf16 when the wide BPTT reads it (the dropout backward fused)
+                fused = drop and mask_ptr is None
+                dyb = bool(self.dy_bf16 and w.g16 and (fused or not drop) and getattr(w, "dy_bf16", None) is not None)
+                if dyb:
+                    w.dy_bf16[li - 1] = True
                 with self._timed(f"dgrad_l{li}"):
                     self._fast(w, 0, 1, N, din, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[li]), 8 * H,
-                               _p(dx), din, drop_seed=seed if (drop and mask_ptr is None) else None)
-                fused = drop and mask_ptr is None
+                               _p(dx), din, drop_seed=seed if fused else None, out_bf16=dyb)
             else:
                 fused = self._mm(w, 0, 0, N, din, 8 * H, pg(dG), 8 * H,
                                  self._ptr(f"decoder.rnn.weight_ih_l{li}"), din, _p(dx), din,
