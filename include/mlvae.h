@@ -173,6 +173,11 @@ int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* 
                        const float* cells, const float* dy, void* dg_bf16, float* dbias_rows,
                        void* dg_fp8, const float* dg8_scale, unsigned* dg_amax, void* xbuf,
                        size_t xbytes, int* err, void* stream);
+/* mlvae_lstm_bwd_fp8 with dy as bf16 [B*T, 2H] when dy_bf16 = 1 (as mlvae_lstm_bwd_ex3). */
+int mlvae_lstm_bwd_fp8_ex(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
+                          const float* cells, const void* dy, int dy_bf16, void* dg_bf16,
+                          float* dbias_rows, void* dg_fp8, const float* dg8_scale, unsigned* dg_amax,
+                          void* xbuf, size_t xbytes, int* err, void* stream);
 /* Workgroups (one per CU, co-resident) of the recurrence launch for this shape as the engine
  * runs it (fp16 gates where mlvae_lstm_gates_fp16): the wide kernels fill the chip. */
 int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd);
@@ -227,9 +232,10 @@ int mlvae_viterbi_md(int B, int T, int N, int L, const float* logits, int ldl, c
  *   cast_fp8:  dst = e4m3(clamp(src * scale, +-448)), RNE; scale = *scale_p if non-null. */
 int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
                    const float* alpha, const float* bias1, const float* bias2, int epi, void* stream);
-/* As mlvae_gemm_fp8 with epi = EPI_DROPOUT allowed (fp32 C): C *= the inter-layer dropout mask of
- * element drop_offset + row * ldc + col -- the fp8 layer-1 dgrad with the dropout backward fused
- * (ref:src/modules/decoder.py:14-15: the dropout between the LSTM layers). */
+/* As mlvae_gemm_fp8 with epi = EPI_DROPOUT allowed (fp32 or, with the EPI_OUT_BF16 flag 32, bf16
+ * C): C *= the inter-layer dropout mask of element drop_offset + row * ldc + col -- the fp8
+ * layer-1 dgrad with the dropout backward fused (ref:src/modules/decoder.py:14-15: the dropout
+ * between the LSTM layers); bf16 C is the wide BPTT's dY input (mlvae_lstm_bwd_ex3). */
 int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C,
                       int ldc, const float* alpha, const float* bias1, const float* bias2, int epi,
                       unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,

@@ -765,7 +765,8 @@ extern "C" int mlvae_gemm_fp8(int M, int N, int K, const void* A, int lda, const
 }
 
 // epi: EPI_NONE or EPI_DROPOUT (the inter-layer dropout's backward: C *= mask of element
-// drop_offset + row * ldc + col, the Philox mask of the forward), optionally | EPI_OUT_F16
+// drop_offset + row * ldc + col, the Philox mask of the forward), optionally | EPI_OUT_F16 (with
+// NONE) or | EPI_OUT_BF16
 extern "C" int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B, int ldb, void* C,
                                  int ldc, const float* alpha, const float* bias1, const float* bias2, int epi,
                                  unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
@@ -775,11 +776,13 @@ extern "C" int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, co
     return 1;
   }
   if (M == 0 || N == 0) return 0;
-  const int c16 = (epi & EPI_OUT_F16) ? 1 : 0;
-  epi &= ~EPI_OUT_F16;
+  const int c16 = (epi & EPI_OUT_BF16) ? 2 : ((epi & EPI_OUT_F16) ? 1 : 0);
+  epi &= ~(EPI_OUT_F16 | EPI_OUT_BF16);
   if ((epi != EPI_NONE && epi != EPI_DROPOUT) || N % 4 || ldc % 4 || ((uintptr_t)C % 16) ||
-      ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16) || (epi == EPI_DROPOUT && (c16 || !(drop_p >= 0.f && drop_p < 1.f)))) {
-    mlvae_set_error("mlvae_gemm_fp8: epilogue none (+ fp16 C) or dropout (fp32 C), N and ldc %% 4, aligned C / bias");
+      ((uintptr_t)bias1 % 16) || ((uintptr_t)bias2 % 16) ||
+      (epi == EPI_DROPOUT && (c16 == 1 || !(drop_p >= 0.f && drop_p < 1.f)))) {
+    mlvae_set_error("mlvae_gemm_fp8: epilogue none (+ fp16 / bf16 C) or dropout (fp32 / bf16 C), N and ldc %% 4, "
+                    "aligned C / bias");
     return 1;
   }
   if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || (lda % 16) || (ldb % 16) || (K % 16)) {

@@ -1203,10 +1203,11 @@ extern "C" int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, co
   return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, nullptr,
              xbuf, xbytes, err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
 }
-extern "C" int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
-                                  void* gates, const float* cells, const float* dy, void* dg_bf16,
-                                  float* dbias_rows, void* dg_fp8, const float* dg8_scale,
-                                  unsigned* dg_amax, void* xbuf, size_t xbytes, int* err, void* stream) {
+extern "C" int mlvae_lstm_bwd_fp8_ex(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                     void* gates, const float* cells, const void* dy, int dy_bf16,
+                                     void* dg_bf16, float* dbias_rows, void* dg_fp8,
+                                     const float* dg8_scale, unsigned* dg_amax, void* xbuf,
+                                     size_t xbytes, int* err, void* stream) {
   if (!use_wide(B, H, PREC_BF16) || !dg_amax || (dg_fp8 && !dg8_scale)) {
     mlvae_set_error("lstm_bwd_fp8: wide-batch shapes; the amax word, and a scale with the fp8 copy");
     return 1;
@@ -1216,9 +1217,17 @@ extern "C" int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, co
   ex.f8.dg8 = static_cast<unsigned char*>(dg_fp8);
   ex.f8.g8scale = dg8_scale;
   ex.f8.g8amax = dg_amax;
+  if (dy_bf16) ex.dyb = static_cast<const unsigned short*>(dy);
   return run(false, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates),
-             const_cast<float*>(cells), const_cast<float*>(dy), xbuf, xbytes, err,
-             (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), 1, ex);
+             const_cast<float*>(cells), dy_bf16 ? nullptr : static_cast<float*>(const_cast<void*>(dy)), xbuf,
+             xbytes, err, (hipStream_t)stream, nullptr, static_cast<unsigned short*>(dg_bf16), 1, ex);
+}
+extern "C" int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                  void* gates, const float* cells, const float* dy, void* dg_bf16,
+                                  float* dbias_rows, void* dg_fp8, const float* dg8_scale,
+                                  unsigned* dg_amax, void* xbuf, size_t xbytes, int* err, void* stream) {
+  return mlvae_lstm_bwd_fp8_ex(B, T, H, w_hh_fwd, w_hh_rev, gates, cells, dy, 0, dg_bf16, dbias_rows, dg_fp8,
+                               dg8_scale, dg_amax, xbuf, xbytes, err, stream);
 }
 
 extern "C" int mlvae_lstm_bwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd,

@@ -1193,7 +1193,8 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC>
-               : (a.g8amax ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true>
+               : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
+                                    : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, false>));
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
@@ -1254,10 +1255,6 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.dbias = dbias; a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
   a.Y8 = f8.y8; a.x8scale = f8.x8scale; a.dG8 = f8.dg8; a.g8scale = f8.g8scale; a.g8amax = f8.g8amax;
   a.dYb = fwd ? nullptr : dyb;
-  if (a.dYb && a.g8amax) {
-    mlvae_set_error("lstm_wide: bf16 dY with the fp8 BPTT is not supported (fp8 mode keeps fp32 dY)");
-    return 1;
-  }
   if (a.Y8 && (!ydb || p.il)) {
     mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one (one-group forward)");
     return 1;

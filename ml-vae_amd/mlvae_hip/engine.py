@@ -351,9 +351,10 @@ class VAEEngine:
         # colsum passes over fp32 intermediates, for same-box A/B)
         self.heads_bias_sums = os.environ.get("MLVAE_HEADS_BSUM", "1") != "0"
         # dY (the layer outputs' gradients) in bf16 where its producers can write it: the heads'
-        # split form and the bf16 dgrad, into the wide-batch BPTT (mlvae_lstm_bwd_ex3); the fp8
-        # mode keeps fp32 dY (its dgrad epilogue writes fp32).  MLVAE_DY_BF16=0: fp32 (A/B)
-        self.dy_bf16 = (cfg.prec == "bf16" and not cfg.fp8 and os.environ.get("MLVAE_DY_BF16", "1") != "0"
+        # split form and the bf16 dgrad, into the wide-batch BPTT (mlvae_lstm_bwd_ex3 /
+        # _fp8_ex); the fp8 dgrad's epilogue writes fp32, so that layer's dY stays fp32.
+        # MLVAE_DY_BF16=0: fp32 everywhere (A/B)
+        self.dy_bf16 = (cfg.prec == "bf16" and os.environ.get("MLVAE_DY_BF16", "1") != "0"
                         and os.environ.get("MLVAE_HEADS_FUSED", "0") in ("", "0"))
         self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
                      if self.fused_heads else None)
@@ -976,9 +977,10 @@ class VAEEngine:
                     am = self.g8_amax[li].data_ptr()
                     check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), am + 4 * par, _p(self.w8s[li]), G8_MARGIN,
                                                     _p(self.g8[li]), s), "fp8_delayed_scale")
-                    check(l.mlvae_lstm_bwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                    dyb = bool(getattr(w, "dy_bf16", {}).get(li, False))
+                    check(l.mlvae_lstm_bwd_fp8_ex(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                               _p(w.Cs[li]), _p(w.dY[li]), _pb(dGb),
+                                               _p(w.Cs[li]), _p(w.dY[li]), int(dyb), _pb(dGb),
                                                _p(rows) if rows is not None else None,
                                                w.dG8.data_ptr() if f8_dgrad else None, _p(self.g8[li]),
                                                am + 4 * par, _p(w.xbuf), w.xbuf.numel(), _p(self.err), s),
@@ -1068,9 +1070,15 @@ class VAEEngine:
                 # configs[4]: dX = dG W_ih on e4m3 operands (dG from the BPTT, W_ih^T cast with the
                 # forward's scale), alpha = 1 / (q_dG q_W), the dropout backward in the epilogue
                 epi8 = EPI_DROPOUT if (drop and mask_ptr is None) else EPI_NONE
+                # dY of the layer below in bf16 when the wide BPTT reads it (as the bf16 dgrad)
+                dyb = bool(self.dy_bf16 and w.g16 and (epi8 == EPI_DROPOUT or not drop)
+                           and getattr(w, "dy_bf16", None) is not None)
+                if dyb:
+                    w.dy_bf16[li - 1] = True
                 with self._timed(f"dgrad_l{li}"):
                     check(l.mlvae_gemm_fp8_ex(N, din, 8 * H, w.dG8.data_ptr(), 8 * H, self.w8t[li].data_ptr(),
-                                              8 * H, _p(dx), din, _p(self.g8[li], 1), None, None, epi8,
+                                              8 * H, _p(dx), din, _p(self.g8[li], 1), None, None,
+                                              epi8 | (EPI_OUT_BF16 if dyb else 0),
                                               (seed or 0) if epi8 else 0, self._drop_off, cfg.dropout, s),
                           "gemm_fp8_ex")
                 fused = epi8 == EPI_DROPOUT
