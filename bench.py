@@ -68,11 +68,12 @@ def macs_per_frame(F, E, Z, H, L, C):
     return enc + lstm + heads
 
 
-def lstm_launch_bytes(B, T, H, gate_bytes=4, dg_bytes=4):
+def lstm_launch_bytes(B, T, H, gate_bytes=4, dg_bytes=4, dy_bytes=4):
     """Algorithmic HBM bytes of one BPTT launch (both directions) per frame: read the saved gates
-    [8H] (gate_bytes: 2 = the wide path's fp16 gate buffer, 4 = fp32), read c_{t-1} [2H] and dY
-    [2H] (fp32), write dG [8H] (dg_bytes: 2 = bf16 in bf16 mode)."""
-    return B * T * (8 * H * gate_bytes + 2 * H * 4 + 2 * H * 4 + 8 * H * dg_bytes)
+    [8H] (gate_bytes: 2 = the wide path's fp16 gate buffer, 4 = fp32), read c_{t-1} [2H] (fp32)
+    and dY [2H] (dy_bytes: 2 = bf16, the engine's bf16 step), write dG [8H] (dg_bytes: 2 = bf16
+    in bf16 mode)."""
+    return B * T * (8 * H * gate_bytes + 2 * H * 4 + 2 * H * dy_bytes + 8 * H * dg_bytes)
 
 
 def lstm_launch_flops(B, T, H):
@@ -92,12 +93,12 @@ def encoder_bwd_bytes(N, F, E, Z):
     return N * (4 * Z + 4 * 2 * Z + 4 * Z + 2 * 2 * E + 4 * F)
 
 
-def heads_bytes(N, F, C, H):
-    """heads_kernel (train, the engine's fused mode): reads h (2H bf16) and x (F fp32); writes
-    mu_x, log_var_x (F each, fp32), dY (2H fp32) and, as bf16 (the weight-gradient GEMMs' operand
-    precision), P1 (2C), P2m, P2v (C each), d mu_x, d log_var_x (F each), dP2m, dP2v (C each),
-    dP1 (2C)."""
-    return N * (2 * 2 * H + 4 * F + 4 * 2 * F + 4 * 2 * H + 2 * (2 * C + 2 * C + 2 * F + 2 * C + 2 * C))
+def heads_bytes(N, F, C, H, dy_bytes=4):
+    """The heads (train, the engine's fused mode): reads h (2H bf16) and x (F fp32); writes
+    mu_x, log_var_x (F each, fp32), dY (2H; dy_bytes 2 = bf16, the engine's bf16 step) and, as
+    bf16 (the weight-gradient GEMMs' operand precision), P1 (2C), P2m, P2v (C each), d mu_x,
+    d log_var_x (F each), dP2m, dP2v (C each), dP1 (2C)."""
+    return N * (2 * 2 * H + 4 * F + 4 * 2 * F + dy_bytes * 2 * H + 2 * (2 * C + 2 * C + 2 * F + 2 * C + 2 * C))
 
 
 def conv_fwd_bytes(N, F, E):
@@ -268,8 +269,9 @@ def timed_run(eng, x, lens, steps, warmup, world, timers=None, norm=None):
     return dt, loss
 
 
-def secondary(kern, B, T, cfg_name):
-    """Per-kernel rooflines of the timed secondary launches (HIP events, main stream)."""
+def secondary(kern, B, T, cfg_name, dy_bytes=4):
+    """Per-kernel rooflines of the timed secondary launches (HIP events, main stream); dy_bytes:
+    the width of dY the engine's heads write (2 = bf16)."""
     F, E, Z, H, L, C, _, _, _ = CONFIGS[cfg_name]
     N = B * T
     out = {}
@@ -291,7 +293,7 @@ def secondary(kern, B, T, cfg_name):
                               ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), "encoder_bwd"),
                               ("conv_fwd", conv_fwd_bytes(N, F, E), "conv_fwd"),
                               ("conv_bwd", conv_bwd_bytes(N, F, E), "conv_bwd"),
-                              ("heads", heads_bytes(N, F, C, H), "heads")):
+                              ("heads", heads_bytes(N, F, C, H, dy_bytes), "heads")):
         if name in kern:
             gbs = nbytes / (kern[name] * 1e-3) / 1e9
             out[name] = {"bound": "hbm", "avg_launch_ms": kern[name], "achieved": gbs,
@@ -318,6 +320,7 @@ def extra_runs(args, device):
         from brain.features import InputNormalization
         dt, loss = timed_run(eng, x, lens, steps, warm, 1, timers if cname in ("c4", "c5", "c5bf16") else None,
                              InputNormalization())
+        dyb = 2 if getattr(eng, "dy_bf16", False) else 4
         lv = loss.tolist()
         out[key] = {"global_batch": B, "seq_len": T, "dtype": prec, "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
@@ -326,13 +329,13 @@ def extra_runs(args, device):
             kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
             if cname in ENC_CONV:
                 out[key]["encoder"] = f"Conv1d K={ENC_CONV[cname]} [{F},{E},{E}]"
-                out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname).items()
+                out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname, dyb).items()
                                        if k.startswith("conv")}
                 # PMC HBM bytes per launch of each conv kernel (profiles/pmc_traffic.json[c4])
                 out[key]["pmc_bytes_per_launch"] = {k: pmc_traffic(f"{cname}/{k}") for k in
                                                     ("conv_fwd_layer", "conv_dgrad", "conv_wgrad")}
             else:
-                sec = secondary(kern, B, T, cname)
+                sec = secondary(kern, B, T, cname, dyb)
                 if cname in FP8:  # against the fp8 (block-scaled) MFMA peak
                     what = {"proj_l1": "layer-1 input projection on fp8 e4m3 operands (incl. the W_ih "
                                        "scale + casts; the input arrives as e4m3 from the recurrence)",
@@ -405,6 +408,7 @@ def main():
     lv = loss.tolist()
     kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
     launches = {k: len(v) for k, v in timers.items()}
+    dyb = 2 if getattr(eng, "dy_bf16", False) else 4   # dY width the engine's bf16 step used
     del eng
     torch.cuda.empty_cache()
     if rank == 0:
@@ -412,7 +416,8 @@ def main():
         dur_s = kern[dom] * 1e-3
         from mlvae_hip._lib import lib
         g16 = bool(lib().mlvae_lstm_gates_fp16(B, H, 1 if args.prec == "bf16" else 0))
-        nbytes = lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if args.prec == "bf16" else 4)
+        nbytes = lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if args.prec == "bf16" else 4,
+                                   dyb if g16 else 4)
         achieved = nbytes / dur_s / 1e9
         step_us = kern[dom] * 1e3 / T
         enc_desc = f"Conv1d(K={ENC_CONV[args.config]})" if args.config in ENC_CONV else "VanillaVAE"
@@ -450,7 +455,7 @@ def main():
                          MFMA_PEAK_TFLOPS[args.prec],
                          "step_latency_us": step_us, "handoff_floor_us": HANDOFF_FLOOR_US,
                          "latency_frac": HANDOFF_FLOOR_US / step_us},
-            "kernels": secondary(kern, B, T, args.config) if args.prec == "bf16" else {},
+            "kernels": secondary(kern, B, T, args.config, dyb) if args.prec == "bf16" else {},
             "kernel_ms": kern,
         }
         if world == 1 and not args.no_extra:
