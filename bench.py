@@ -16,10 +16,12 @@ worker processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their e
 before it touches the GPU, waits for them and exits with their worst status.
 
 Rank 0 prints ONE JSON line.  Besides the contract fields it carries
-  roofline          the dominant kernel (the persistent BiLSTM BPTT recurrence): HIP-event time
-                    of its launches on their stream, algorithmic bytes per launch, PMC traffic
-                    from the committed rocprofv3 passes (profiles/pmc_traffic.json) or null, and
-                    its per-step latency against the inter-CU hand-off floor
+  roofline          the dominant kernel -- whichever persistent BiLSTM recurrence (forward or
+                    BPTT) took the most measured time per step: HIP-event time of its launches
+                    on their stream, algorithmic bytes per launch, PMC traffic from the
+                    committed rocprofv3 passes (profiles/pmc_traffic.json, source named) or
+                    null, and its per-step latency against the inter-CU hand-off floor
+  recurrences       the same fields for both recurrences
   kernels           secondary rooflines: the two big GEMMs against the bf16 MFMA peak, the fused
                     encoder (+reparameterisation + KL) and decoder-heads (+NLL) kernels against HBM
   cpu_baseline      the CPU oracle (oracle/vae_cpu.py, pinned to reference fixtures) timed on this
@@ -74,6 +76,17 @@ def lstm_launch_bytes(B, T, H, gate_bytes=4, dg_bytes=4, dy_bytes=4):
     and dY [2H] (dy_bytes: 2 = bf16, the engine's bf16 step), write dG [8H] (dg_bytes: 2 = bf16
     in bf16 mode)."""
     return B * T * (8 * H * gate_bytes + 2 * H * 4 + 2 * H * dy_bytes + 8 * H * dg_bytes)
+
+
+def lstm_fwd_launch_bytes(B, T, H, L, gate_bytes=2, h_bytes=2, drop=True, fp8=False):
+    """Algorithmic HBM bytes of one forward-recurrence launch (both directions), averaged over
+    the L layers' launches (the HIP-event timer averages them too).  Per frame: read the input
+    projection [8H] (gate_bytes: 2 = fp16 on the wide path), write the activated gates [8H]
+    (same width), c [2H] fp32 and h [2H] (h_bytes: 2 = the bf16 GEMM operand); layers below the
+    top also write dropout(h) [2H] bf16 (drop) and, in fp8 mode, its e4m3 copy [2H]."""
+    per = [8 * H * gate_bytes * 2 + 2 * H * 4 + 2 * H * h_bytes +
+           ((2 * H * 2 + (2 * H if fp8 else 0)) if (drop and l < L - 1) else 0) for l in range(L)]
+    return B * T * sum(per) / L
 
 
 def lstm_launch_flops(B, T, H):
@@ -152,17 +165,43 @@ def cpu_baseline(cfg_name, budget_s=15.0):
                       f"dropout 0.15, clip+Adam) in {dt:.1f} s on {torch.get_num_threads()} host threads"}
 
 
+def _pmc_table():
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def pmc_traffic(key):
     """HBM bytes per launch of kernel "<config>/<kernel>" from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, written by tools/gpu_pmc.sh + tools/pmc_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     cfg, _, kern = key.partition("/")
     try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(cfg, {}).get(kern, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError, AttributeError):
+        return _pmc_table().get(cfg, {}).get(kern, {}).get("hbm_bytes_per_launch")
+    except AttributeError:
         return None
+
+
+def pmc_source(cfg):
+    """Which rocprofv3 PMC passes the config's traffic numbers came from."""
+    src = _pmc_table().get(cfg, {}).get("_source")
+    return {"file": "profiles/pmc_traffic.json", "config": cfg, **(src or {})}
+
+
+def recurrence_roofline(name, what, nbytes, flops, ms, launches, T, cfg_name, prec):
+    """HBM roofline (algorithmic bytes / HIP-event launch time) + per-step latency of one
+    persistent recurrence kernel."""
+    dur_s = ms * 1e-3
+    achieved = nbytes / dur_s / 1e9
+    step_us = ms * 1e3 / T
+    return {"kernel": name, "what": what, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": pmc_traffic(f"{cfg_name}/{name}"), "traffic_source": pmc_source(cfg_name),
+            "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": ms, "launches": launches,
+            "mfma_frac": flops / dur_s / 1e12 / MFMA_PEAK_TFLOPS[prec],
+            "step_latency_us": step_us, "handoff_floor_us": HANDOFF_FLOOR_US,
+            "latency_frac": HANDOFF_FLOOR_US / step_us}
 
 
 def _free_port():
@@ -322,7 +361,9 @@ def extra_runs(args, device):
                              InputNormalization())
         dyb = 2 if getattr(eng, "dy_bf16", False) else 4
         lv = loss.tolist()
-        out[key] = {"global_batch": B, "seq_len": T, "dtype": prec, "steps": steps,
+        out[key] = {"global_batch": B, "seq_len": T,
+                    "dtype": "fp8-e4m3 layer-1 projection/dgrad, bf16 elsewhere" if cname in FP8 else prec,
+                    "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
                     "loss": lv[2]}
         if timers:
@@ -334,6 +375,7 @@ def extra_runs(args, device):
                 # PMC HBM bytes per launch of each conv kernel (profiles/pmc_traffic.json[c4])
                 out[key]["pmc_bytes_per_launch"] = {k: pmc_traffic(f"{cname}/{k}") for k in
                                                     ("conv_fwd_layer", "conv_dgrad", "conv_wgrad")}
+                out[key]["pmc_source"] = pmc_source(cname)
             else:
                 sec = secondary(kern, B, T, cname, dyb)
                 if cname in FP8:  # against the fp8 (block-scaled) MFMA peak
@@ -412,14 +454,23 @@ def main():
     del eng
     torch.cuda.empty_cache()
     if rank == 0:
-        dom = "lstm_bwd"
-        dur_s = kern[dom] * 1e-3
         from mlvae_hip._lib import lib
-        g16 = bool(lib().mlvae_lstm_gates_fp16(B, H, 1 if args.prec == "bf16" else 0))
-        nbytes = lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if args.prec == "bf16" else 4,
-                                   dyb if g16 else 4)
-        achieved = nbytes / dur_s / 1e9
-        step_us = kern[dom] * 1e3 / T
+        g16 = bool(lib().mlvae_lstm_gates_fp16_t(B, T, H, 1 if args.prec == "bf16" else 0))
+        bf = args.prec == "bf16"
+        recs = {
+            "lstm_fwd": recurrence_roofline(
+                "lstm_fwd", "persistent BiLSTM forward recurrence, both directions, one launch per layer",
+                lstm_fwd_launch_bytes(B, T, H, L, 2 if g16 else 4, 2 if bf else 4, True,
+                                      args.config in FP8 and bf),
+                lstm_launch_flops(B, T, H), kern["lstm_fwd"], launches["lstm_fwd"], T, args.config, args.prec),
+            "lstm_bwd": recurrence_roofline(
+                "lstm_bwd", "persistent BiLSTM BPTT recurrence, both directions, one launch per layer",
+                lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if bf else 4, dyb if g16 else 4),
+                lstm_launch_flops(B, T, H), kern["lstm_bwd"], launches["lstm_bwd"], T, args.config, args.prec),
+        }
+        # the bench line's roofline names the kernel with the most measured time per step (both
+        # recurrences run once per layer per step)
+        dom = max(recs, key=lambda k: kern[k] * launches[k])
         enc_desc = f"Conv1d(K={ENC_CONV[args.config]})" if args.config in ENC_CONV else "VanillaVAE"
         out = {
             "metric": METRIC,
@@ -444,17 +495,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "elbo": {"kld_loss": lv[0], "recon_loss": lv[1], "loss": lv[2]},
             "train_tflops": value * 6 * macs_per_frame(F, E, Z, H, L, C) / 1e12,
-            "roofline": {"kernel": "lstm_bwd (persistent BiLSTM BPTT recurrence, both directions, "
-                                   "all batch chunks of one layer)",
-                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(f"{args.config}/lstm_bwd"),
-                         "algorithmic_bytes_per_launch": nbytes,
-                         "avg_launch_ms": kern[dom], "launches": launches[dom],
-                         "mfma_frac": lstm_launch_flops(B, T, H) / dur_s / 1e12 /
-                         MFMA_PEAK_TFLOPS[args.prec],
-                         "step_latency_us": step_us, "handoff_floor_us": HANDOFF_FLOOR_US,
-                         "latency_frac": HANDOFF_FLOOR_US / step_us},
+            "roofline": recs[dom],
+            "recurrences": recs,
             "kernels": secondary(kern, B, T, args.config, dyb) if args.prec == "bf16" else {},
             "kernel_ms": kern,
         }

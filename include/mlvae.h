@@ -143,6 +143,9 @@ int mlvae_lstm1_bwd(int prec, int B, int T, int H, const float* w_hh, float* gat
  *   dG over each batch group's 16 utterances and all T steps: dbias_rows [ceil(B/16)][8H], whose
  *   column sums are the layer's b_ih / b_hh gradients (ref:src/modules/decoder.py:14-15). */
 int mlvae_lstm_gates_fp16(int B, int H, int prec);
+/* The same for sequence length T: also 0 where T exceeds the wide kernels' 32-bit batch-group
+ * addressing (16 T 8H fp16 gates >= 4 GB); the engine picks its gate buffer with it. */
+int mlvae_lstm_gates_fp16_t(int B, int T, int H, int prec);
 int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                        void* gates, int gates_fp16, float* cells, float* y, void* y_bf16,
                        void* y_drop_bf16, unsigned long long drop_seed,

@@ -101,11 +101,13 @@ class Checkpointer:
             out.append((d, meta))
         return out
 
-    def find_checkpoints(self, max_key=None, min_key=None, max_num_checkpoints=None):
-        """Checkpoints ranked best first (SpeechBrain find_checkpoints)."""
+    def find_checkpoints(self, max_key=None, min_key=None, max_num_checkpoints=None, predicate=None):
+        """Checkpoints ranked best first (SpeechBrain find_checkpoints); predicate(meta) filters."""
         if max_key is not None and min_key is not None:
             raise ValueError("give max_key or min_key, not both")
         ckpts = self.list_checkpoints()
+        if predicate is not None:
+            ckpts = [c for c in ckpts if predicate(c[1]["meta"])]
         if max_key is not None:
             ckpts = [c for c in ckpts if max_key in c[1]["meta"]]
             ckpts.sort(key=lambda c: c[1]["meta"][max_key], reverse=True)
@@ -121,19 +123,23 @@ class Checkpointer:
         return ckpts[0][0] if ckpts else None
 
     def save_and_keep_only(self, meta=None, end_of_epoch=True, max_keys=None, min_keys=None,
-                           num_to_keep=1):
+                           num_to_keep=1, ckpt_predicate=None):
+        """Save, then delete the checkpoints that are neither among the num_to_keep most recent
+        nor the best by a max/min key.  ckpt_predicate(meta dict) limits both the ranking and
+        the deletion to the checkpoints it accepts (SpeechBrain: the intra-epoch checkpoints
+        replace only each other)."""
         d = self.save_checkpoint(meta, end_of_epoch=end_of_epoch)
         keep = {d}
-        for c, _ in self.find_checkpoints(max_num_checkpoints=num_to_keep):
+        for c, _ in self.find_checkpoints(max_num_checkpoints=num_to_keep, predicate=ckpt_predicate):
             keep.add(c)
         for k in max_keys or []:
-            for c, _ in self.find_checkpoints(max_key=k, max_num_checkpoints=num_to_keep):
+            for c, _ in self.find_checkpoints(max_key=k, max_num_checkpoints=num_to_keep, predicate=ckpt_predicate):
                 keep.add(c)
         for k in min_keys or []:
-            for c, _ in self.find_checkpoints(min_key=k, max_num_checkpoints=num_to_keep):
+            for c, _ in self.find_checkpoints(min_key=k, max_num_checkpoints=num_to_keep, predicate=ckpt_predicate):
                 keep.add(c)
-        for c, _ in self.list_checkpoints():
-            if c not in keep:
+        for c, m in self.list_checkpoints():
+            if c not in keep and (ckpt_predicate is None or ckpt_predicate(m["meta"])):
                 shutil.rmtree(c, ignore_errors=True)
         return d
 

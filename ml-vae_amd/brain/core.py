@@ -1,11 +1,15 @@
 """Brain: the epoch/batch loop around compute_forward / compute_objectives."""
 import enum
 import logging
+import time
 from types import SimpleNamespace
 
 import torch
 
 logger = logging.getLogger(__name__)
+
+
+INTRA_EPOCH_CKPT_FLAG = "brain_intra_epoch_ckpt"   # SpeechBrain's meta key of intra-epoch saves
 
 
 class Stage(enum.Enum):
@@ -147,12 +151,20 @@ class Brain:
             self.nonfinite_count = 0
             self.step = 0
             acc = None
+            last_ckpt = time.time()
             for batch in train_set:
                 self.step += 1
                 loss = self.fit_batch(batch)
                 acc = self.update_average(loss, acc)
                 if self.debug and self.step == self.debug_batches:
                     break
+                # --ckpt_interval_minutes: an intra-epoch checkpoint on the host timer (SpeechBrain
+                # Brain.fit); rank 0 writes it, replacing only the previous intra-epoch one
+                if (self.checkpointer is not None and self.ckpt_interval_minutes > 0
+                        and time.time() - last_ckpt >= self.ckpt_interval_minutes * 60.0):
+                    if self.rank == 0:
+                        self._save_intra_epoch_ckpt()
+                    last_ckpt = time.time()
             self.avg_train_loss = self._stage_loss(acc)
             self.on_stage_end(Stage.TRAIN, self.avg_train_loss, epoch)
             self.avg_train_loss = 0.0
@@ -172,6 +184,11 @@ class Brain:
                     self.on_stage_end(Stage.VALID, self._stage_loss(acc), epoch)
             if self.debug and epoch == self.debug_epochs:
                 break
+
+    def _save_intra_epoch_ckpt(self):
+        self.checkpointer.save_and_keep_only(
+            end_of_epoch=False, num_to_keep=1, meta={INTRA_EPOCH_CKPT_FLAG: True},
+            ckpt_predicate=lambda meta: INTRA_EPOCH_CKPT_FLAG in meta)
 
     def evaluate(self, test_set, max_key=None, min_key=None, progressbar=None,
                  test_loader_kwargs=None):

@@ -1169,6 +1169,10 @@ extern "C" int mlvae_lstm_launch_workgroups(int B, int H, int prec, int fwd) {
 // gate buffer is fp16 [B*T, 8H]: the caller then passes fp16 gates to the _ex2 entry points.
 // fp32 gates (every other entry point) always run the batch-group kernels, batch-chunked.
 extern "C" int mlvae_lstm_gates_fp16(int B, int H, int prec) { return use_wide(B, H, prec) ? 1 : 0; }
+// the same for a sequence length T: 0 also where T exceeds the wide kernels' addressing
+extern "C" int mlvae_lstm_gates_fp16_t(int B, int T, int H, int prec) {
+  return use_wide(B, H, prec) && lstm_wide_t_ok(T, H) ? 1 : 0;
+}
 
 extern "C" int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_hh_fwd,
                                   const float* w_hh_rev, void* gates, int gates_fp16, float* cells,

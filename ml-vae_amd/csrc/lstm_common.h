@@ -170,5 +170,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
 void lstm_wide_set_mode(int mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply
 size_t lstm_wide_xbytes(int B, int H, bool fwd);
+// the wide kernels address one batch group's rows through 32-bit buffer offsets: T bound
+bool lstm_wide_t_ok(int T, int H);
 // workgroups of the wide launch at (B, H), or 0 when it does not apply
 int lstm_wide_workgroups(int B, int H, bool fwd);

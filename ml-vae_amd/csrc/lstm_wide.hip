@@ -1223,6 +1223,10 @@ int launch_il(const LstmArgs& a, const WidePlan& p, hipStream_t s) {
 
 void lstm_wide_set_mode(int mode) { g_wide_mode = mode; }
 
+bool lstm_wide_t_ok(int T, int H) {
+  return (size_t)BG * T * 8 * H * 2 <= 0xffffffffull && (size_t)BG * T * 2 * H * 4 <= 0xffffffffull;
+}
+
 int lstm_wide_workgroups(int B, int H, bool fwd) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return 0;
@@ -1242,7 +1246,11 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return -1;
   // the kernels address a batch group's rows through one buffer descriptor (32-bit offsets)
-  if ((size_t)BG * T * 8 * H * 2 > 0xffffffffull || (size_t)BG * T * 2 * H * 4 > 0xffffffffull) return -1;
+  if (!lstm_wide_t_ok(T, H)) {
+    mlvae_set_error("lstm_wide: T=%d too long for the wide kernels' 32-bit batch-group addressing at H=%d "
+                    "(mlvae_lstm_gates_fp16_t(B, T, H, prec) = 0: pass fp32 gates)", T, H);
+    return 1;
+  }
   if (!xbuf || xbytes < p.xbytes || !err) {
     mlvae_set_error("lstm_wide: exchange workspace too small (need %zu B)", p.xbytes);
     return 1;

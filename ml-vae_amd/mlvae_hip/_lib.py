@@ -56,6 +56,7 @@ _SIGS = {
     "mlvae_lstm1_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm1_bwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_gates_fp16": [I, I, I],
+    "mlvae_lstm_gates_fp16_t": [I, I, I, I],
     "mlvae_lstm_fwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_bwd_ex2": [I, I, I, I, P, P, P, I, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_ex3": [I, I, I, I, P, P, P, I, P, P, I, P, P, P, SZ, P, P],

@@ -52,6 +52,14 @@ def allreduce_loss(loss3, group=None):
     dist.all_reduce(loss3, op=dist.ReduceOp.SUM, group=group)
 
 
+def allreduce_err(err, group=None):
+    """MAX of the recurrence timeout words over ranks (int32 [1]), before the fused Adam reads
+    it: a timeout on any rank leaves that rank's share of the summed gradient undefined, so
+    every rank must skip the update together or the replicas' weights diverge."""
+    dist.all_reduce(err, op=dist.ReduceOp.MAX, group=group)
+    return err
+
+
 def allreduce_count(count, group=None):
     """Global number of valid frames (int tensor [1])."""
     dist.all_reduce(count, op=dist.ReduceOp.SUM, group=group)

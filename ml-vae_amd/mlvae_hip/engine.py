@@ -217,7 +217,7 @@ class _Work:
         self.eps = empty(N, Z, **f)
         # gate buffer [N, 8H]: fp32, or fp16 where the recurrence runs the wide-batch kernels
         # (halves the projection's write and the recurrences' reads; include/mlvae.h)
-        self.g16 = bool(lib().mlvae_lstm_gates_fp16(B, H, PREC[cfg.prec]))
+        self.g16 = bool(lib().mlvae_lstm_gates_fp16_t(B, T, H, PREC[cfg.prec]))
         self.G = [empty(N, 8 * H, dtype=torch.float16 if self.g16 else torch.float32) for _ in range(L)]
         # wide BPTT: per batch group rows of the bias gradients (summed over groups by colsum)
         self.NBG = (B + 15) // 16
@@ -960,7 +960,8 @@ class VAEEngine:
             self._mm(w, 0, 0, N, 2 * H, K1, _p(w.dP1), 2 * C, self._ptr("decoder.mean_fc.blocks.0.weight"),
                      2 * H, _p(w.dY[cfg.L - 1]), 2 * H, B_bf=wb("decoder.mean_fc.blocks.0.weight"))
         # ---- BiLSTM layers, top to bottom
-        for li in range(cfg.L - 1, -1, -1):
+        ran_f8 = False   # an fp8 BPTT recorded this step's amax (a batch too small for the wide
+        for li in range(cfg.L - 1, -1, -1):   # kernels runs none: the amax parity must not flip)
             xin, xin_bf, din, ldx = w.layer_in[li]
             Gl = w.G[li]
             dGb = w.dGb[li] if w.bf else None
@@ -973,6 +974,7 @@ class VAEEngine:
                 # the layer-0 biases come with dW_ih_l0 from skinny_tn when the encoder is fused
                 rows = w.dbias_rows[li] if (w.g16 and not (li == 0 and w.enc_fused)) else None
                 if f8:
+                    ran_f8 = True
                     par = self.g8_par   # this step's amax word; the other holds the last step's
                     am = self.g8_amax[li].data_ptr()
                     check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), am + 4 * par, _p(self.w8s[li]), G8_MARGIN,
@@ -1109,7 +1111,7 @@ class VAEEngine:
             if li == cfg.L - 1 and self.world > 1 and self.bucket_allreduce and not full:
                 self._flush_side(pending)  # the bucket waits on the side stream: issue it all
                 self._start_suffix_allreduce()
-        if getattr(self, "g8", None):
+        if ran_f8:
             self.g8_ready = True   # this step's BPTT recorded the amax the next step scales by
             self.g8_par ^= 1
         # ---- encoder
@@ -1207,6 +1209,9 @@ class VAEEngine:
         else:
             mdist.allreduce_grad_bucket(self.grad, self.process_group)
         mdist.allreduce_loss(w.loss, self.process_group)
+        # the skip-on-timeout decision is global: a rank whose recurrence timed out contributed
+        # an undefined share to the summed gradient, so every rank skips that update
+        mdist.allreduce_err(self.err, self.process_group)
 
     def _main(self):
         """Context: run on the high-priority main stream, ordered after (and before) the

@@ -400,15 +400,24 @@ class LSTMFn(torch.autograd.Function):
                 t_last = 0 if d else T - 1
                 hn[li * ndir + d] = Y_[:, t_last, d * H:(d + 1) * H]
                 cn[li * ndir + d] = Cv[:, t_last, d * H:(d + 1) * H]
-        ctx.mark_non_differentiable(hn, cn)
+        # h_n is differentiable (its gradient joins the layer output's at the last step); c_n's
+        # gradient would need an initial cell gradient the BPTT kernels do not take: refused
+        # loudly in backward.  Unused outputs arrive as None (no materialised zero tensors).
+        ctx.set_materialize_grads(False)
+        ctx.out_shape = h.shape
         return h, hn, cn
 
     @staticmethod
-    def backward(ctx, dy, _dhn=None, _dcn=None):
+    def backward(ctx, dy, dhn=None, dcn=None):
         H, L, ndir = ctx.H, ctx.L, ctx.ndir
         nw, GL = 4 * ndir, 4 * H * ndir
         t = ctx.saved_tensors
         inputs, saved, weights = t[:L], t[L:4 * L], t[4 * L:]
+        if dcn is not None and bool(dcn.ne(0).any()):
+            raise NotImplementedError("gradient through c_n of the HIP LSTM is not supported "
+                                      "(the BPTT starts from a zero cell gradient)")
+        if dy is None:
+            dy = torch.zeros(ctx.out_shape, device=t[0].device, dtype=torch.float32)
         dy = _need(dy, "lstm grad").clone()
         B, T = dy.shape[0], dy.shape[1]
         N = B * T
@@ -421,6 +430,9 @@ class LSTMFn(torch.autograd.Function):
             w = weights[nw * li:nw * li + nw]
             xin = inputs[li]
             din = xin.shape[-1]
+            if dhn is not None:  # h_n[li, d] is Y_li at t = T-1 (forward) / t = 0 (reverse)
+                for d in range(ndir):
+                    dy[:, 0 if d else T - 1, d * H:(d + 1) * H] += dhn[li * ndir + d]
             if ndir == 2:
                 check(l.mlvae_lstm_bwd(_prec(), B, T, H, _p(w[1]), _p(w[5]), _p(G), _p(Cs), _p(dy),
                                        _p(xbuf), xbuf.numel() * 4, _p(err), _stream()), "lstm_bwd")

@@ -203,7 +203,10 @@ class MDModel(Brain):
         batch = batch.to(self.device)
         feats, lens = batch["feat"]
         norm = getattr(self.hparams, "normalizer", None)
-        if isinstance(norm, InputNormalization) and lib().mlvae_norm_supported(feats.shape[-1]):
+        # the device normaliser applies (x - mean) / std: a module with mean_norm or std_norm
+        # off runs its own forward instead
+        if isinstance(norm, InputNormalization) and norm.mean_norm and norm.std_norm \
+                and lib().mlvae_norm_supported(feats.shape[-1]):
             return feats.contiguous(), lens, norm
         if norm is not None:
             feats = norm(feats, lens, epoch=self.hparams.epoch_counter.current)

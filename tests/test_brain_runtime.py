@@ -78,6 +78,47 @@ def test_mid_epoch_checkpoint_replays_the_epoch(tmp_path):
     assert ec.current == 3
 
 
+def test_ckpt_interval_minutes_saves_intra_epoch_checkpoints(tmp_path, monkeypatch):
+    """--ckpt_interval_minutes (SpeechBrain Brain.fit): an end_of_epoch=False checkpoint on the
+    host timer during TRAIN, each replacing the previous intra-epoch one only; the end-of-epoch
+    save_and_keep_only (min_keys) then removes it and keeps the best epoch checkpoint."""
+    import brain.core as core
+    from brain import Checkpointer, EpochCounter
+    from brain.core import INTRA_EPOCH_CKPT_FLAG, Brain, Stage
+
+    clock = [1000.0]
+    monkeypatch.setattr(core.time, "time", lambda: clock[0])
+
+    class Toy(Brain):
+        def compute_forward(self, batch, stage):
+            return self.modules["lin"](batch)
+
+        def compute_objectives(self, out, batch, stage):
+            clock[0] += 40.0                     # every batch takes 40 "seconds"
+            return out.pow(2).mean()
+
+        def fit_batch(self, batch):               # CPU: no HIP clip
+            loss = self.compute_objectives(self.compute_forward(batch, Stage.TRAIN), batch, Stage.TRAIN)
+            return loss.detach()
+
+        def on_stage_end(self, stage, loss, epoch=None):
+            if stage == Stage.TRAIN:
+                ck = self.checkpointer.list_checkpoints()
+                self.seen = [(m["end_of_epoch"], INTRA_EPOCH_CKPT_FLAG in m["meta"]) for _, m in ck]
+                clock[0] += 1.0
+                self.checkpointer.save_and_keep_only(meta={"loss": loss}, min_keys=["loss"])
+
+    lin = torch.nn.Linear(4, 2)
+    ec = EpochCounter(1)
+    ck = Checkpointer(tmp_path, {"lin": lin, "epoch_counter": ec})
+    b = Toy(modules={"lin": lin}, opt_class=lambda p: torch.optim.SGD(p, lr=0.1),
+            run_opts={"device": "cpu", "ckpt_interval_minutes": 1.0}, checkpointer=ck)
+    b.fit(ec, [torch.randn(3, 4) for _ in range(6)])
+    assert b.seen == [(False, True)]             # one intra-epoch checkpoint survived the epoch
+    left = ck.list_checkpoints()
+    assert len(left) == 1 and left[0][1]["end_of_epoch"] and "loss" in left[0][1]["meta"]
+
+
 def test_optimizer_state_dict_is_torch_adam_layout():
     """EngineOptimizer's state_dict must load into torch.optim.Adam (and back)."""
     from mlvae_hip.engine import ParamLayout, VAEConfig

@@ -69,3 +69,41 @@ def test_rnn_dropin_module_forward_and_state_dict():
     from mlvae_hip import ops
     tol = 1e-5 if ops.get_precision() == "fp32" else 1e-2
     assert norm_rel(o, ro) < tol and norm_rel(h, rh) < tol and norm_rel(c, rc) < tol
+
+
+def test_rnn_dropin_gradient_through_h_n_and_c_n():
+    """h_n backpropagates as in nn.LSTM (its gradient joins each layer's output
+    gradient at the last step, bidirectional included); a gradient through c_n is refused
+    loudly instead of being dropped."""
+    need_gpu()
+    from mlvae_hip import ops
+    torch.manual_seed(6)
+    ref = torch.nn.LSTM(24, 32, num_layers=2, batch_first=True, bidirectional=True).double()
+    mine = torch.nn.LSTM(24, 32, num_layers=2, batch_first=True, bidirectional=True)
+    mine.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    mine = mine.cuda().eval()
+    x = torch.randn(3, 11, 24)
+    cot_o, cot_h = torch.randn(3, 11, 64), torch.randn(4, 3, 32)
+    prev = ops.get_precision()
+    ops.set_precision("fp32")
+    try:
+        xd = x.cuda().requires_grad_(True)
+        o, hn, cn = ops.LSTMFn.apply(xd, 32, 2, 2, 0.0, 0, *[p for p in mine.parameters()])
+        ((o * cot_o.cuda()).sum() + (hn * cot_h.cuda()).sum()).backward()
+        xr = x.double().requires_grad_(True)
+        ro, (rh, _) = ref(xr)
+        ((ro * cot_o.double()).sum() + (rh * cot_h.double()).sum()).backward()
+        assert norm_rel(xd.grad, xr.grad) < 1e-5
+        for (k, a), (_, b) in zip(mine.named_parameters(), ref.named_parameters()):
+            assert norm_rel(a.grad, b.grad) < 1e-5, k
+        # only h_n used: the output's gradient arrives as None
+        xd2 = x.cuda().requires_grad_(True)
+        _, hn2, _ = ops.LSTMFn.apply(xd2, 32, 2, 2, 0.0, 0, *[p for p in mine.parameters()])
+        hn2.sum().backward()
+        assert torch.isfinite(xd2.grad).all()
+        xd3 = x.cuda().requires_grad_(True)
+        _, _, cn3 = ops.LSTMFn.apply(xd3, 32, 2, 2, 0.0, 0, *[p for p in mine.parameters()])
+        with pytest.raises(NotImplementedError, match="c_n"):
+            cn3.sum().backward()
+    finally:
+        ops.set_precision(prev)

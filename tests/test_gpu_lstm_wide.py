@@ -114,6 +114,9 @@ def test_gate_buffer_format_is_checked():
     assert l.mlvae_lstm_gates_fp16(8, H, 1) == 1
     assert l.mlvae_lstm_gates_fp16(256, H, 0) == 0     # fp32 parity mode
     assert l.mlvae_lstm_gates_fp16(256, 128, 1) == 0   # wide kernels are built for H = 512
+    # T-aware form: a batch group's 16 T 8H fp16 gates must stay under 4 GB (32-bit offsets)
+    assert l.mlvae_lstm_gates_fp16_t(256, 2000, H, 1) == 1
+    assert l.mlvae_lstm_gates_fp16_t(256, 40000, H, 1) == 0
     B, T, H2 = 8, 4, 128                               # a batch-group shape refuses fp16 gates
     N = B * T
     G = torch.zeros(N, 8 * H2, device="cuda", dtype=torch.float16)

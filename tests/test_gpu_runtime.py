@@ -172,6 +172,57 @@ def _dp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _err_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from mlvae_hip import dist as mdist
+    from mlvae_hip.engine import VAEConfig, VAEEngine
+    from oracle import vae_cpu as O
+    cfg = VAEConfig(F=16, E=16, Z=8, H=32, L=2, C=16, dropout=0.0, prec="fp32")
+    eng = VAEEngine(cfg, params=O.init_params(16, 16, 8, 32, 2, 16, seed=5), seed=3)
+    B, T = 2, 10
+    mdist.attach(eng, rank=rank, world=world, batch_per_rank=B)
+    g = torch.Generator().manual_seed(2)
+    xg = torch.randn(B * world, T, 16, generator=g)
+    sl = slice(rank * B, (rank + 1) * B)
+    eng.train_step(xg[sl].cuda(), torch.ones(B).cuda())   # a good step: both replicas move
+    torch.cuda.synchronize()
+    before = eng.flat.cpu()
+    if rank == 1:
+        eng.err.fill_(1)                                   # rank 1's recurrence timed out
+    for _ in range(2):
+        eng.train_step(xg[sl].cuda(), torch.ones(B).cuda())
+    torch.cuda.synchronize()
+    q.put((rank, before, eng.flat.cpu(), int(eng.err.item()), int(eng.err_skips.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_a_timeout_on_one_rank_skips_the_update_on_every_rank():
+    """the fused Adam's skip-on-timeout decision must be global.  Rank 1's err word
+    is set after one good step; both ranks then skip every update (the word is MAX-reduced with
+    the gradients), so the replicas keep identical weights instead of diverging."""
+    need_gpu()
+    import torch.multiprocessing as mp
+    from test_dist_gloo import _free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_err_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, before, after, err, skips in res:
+        assert err == 1 and skips == 2, (rank, err, skips)
+        assert torch.equal(before, after), rank
+    assert torch.equal(res[0][2], res[1][2])
+
+
 def test_two_gloo_ranks_through_the_engine_equal_one_engine_on_the_global_batch():
     """SURVEY.md 8(e)(i)-(iii) with a real collective: two ranks (gloo on CUDA tensors, one GPU)
     each train their shard with the bucketed all-reduce live (suffix bucket on the comm stream

@@ -12,6 +12,7 @@ taken as 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B streaming stores.  hbm_byt
 import collections
 import csv
 import json
+import os
 import sys
 
 
@@ -53,9 +54,13 @@ def main(fetch_csv, write_csv, out, config):
             allres = json.load(fh)
     except (OSError, ValueError):
         allres = {}
+    # where the numbers came from (bench.py cites it next to every "traffic" it reports)
+    tag = os.environ.get("PMC_TAG", "")
+    res["_source"] = {"fetch_csv": os.path.basename(fetch_csv), "write_csv": os.path.basename(write_csv),
+                      "tag": tag, "committed_as": f"profiles/pmc_{tag or config}_{{fetch,write}}.csv"}
     allres[config] = res
     json.dump(allres, open(out, "w"), indent=1)
-    for k, v in list(res.items())[:10]:
+    for k, v in [kv for kv in res.items() if not kv[0].startswith('_')][:10]:
         print(f"{k:40s} launches {v['launches']:3d}  read {v['read_bytes_corrected'] / 1e6:9.1f} MB  "
               f"write {v['write_size_bytes'] / 1e6:9.1f} MB")
 
