@@ -56,7 +56,11 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // forward
 // ---------------------------------------------------------------------------------------
 // OCC = minimum waves per SIMD (2: one 512-thread workgroup per CU)
-template <int TPW, int NKC, int OCC>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
+// IOV: where the io waves store step s-1's saved activations (A/B variants, picked on the host
+// by debug bits): 0 right behind their own publish of step s; 1 behind every wave's publish of
+// step s (bit 17); 2 gathered LDS -> registers before barrier s and stored right after it, so
+// the stores drain during the MFMA / cell phase, away from the publish and the poll (bit 19)
+template <int TPW, int NKC, int OCC, int IOV = 0>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -80,6 +84,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUB);  // [wave][TPW][KLF][lane]
   unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);  // [2][NC8] keep bits
   __shared__ int abort_flag;
+  // LDS arrival counters (A/B variants): waves that published / wrote their out ring, per step
+  __shared__ unsigned pubcnt, outcnt;
 
   // group slots padded to a multiple of 8 (idle slots exit at once): members gid + k * gstride
   // then share one XCD under round-robin dispatch at every batch size (B = 32: 4 groups)
@@ -121,7 +127,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   __shared__ int placement;
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement) &&
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
-  if (tid == 0) abort_flag = 0;
+  if (tid == 0) { abort_flag = 0; pubcnt = 0; outcnt = 0; }
+  constexpr bool st_after_pub = IOV == 1;
+  constexpr bool st_early = IOV == 2;  // (the host picks it only without the fp32 h output)
 
   const size_t xslot = (size_t)BG * H;  // elements per exchange slot
   short* xb = reinterpret_cast<short*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
@@ -227,6 +235,80 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       }
     }
   };
+  // bit 19: step s_'s saved activations held in registers between the gather (before barrier
+  // s_ + 1) and the stores (right after it); dropout applied at issue time (the pollers draw the
+  // keep bits of step s_ inside the poll of step s_ + 1)
+  constexpr int NG8R = (16 * 4 * HJ / 8 + 255) / 256;  // gate chunks per io thread
+  struct Held { u32x4 gv[NG8R]; f32x4 cv, h0, h1; };
+  auto io_gather = [&](int s_, Held& hd) {
+    const char* src = outr + (s_ & 1) * 16 * OUB;
+    constexpr int NG8 = 16 * 4 * HJ / 8;
+#pragma unroll
+    for (int k = 0; k < NG8R; ++k) {
+      const int ci = iot + 256 * k;
+      if (ci < NG8) {
+        const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
+        hd.gv[k] = *reinterpret_cast<const u32x4*>(src + (row >> 2) * OUB + ((row & 3) * HJ + uu) * 2);
+      }
+    }
+    constexpr int NQ2 = 16 * HJ / 4;
+    if (iot < NQ2) {
+      const int u = iot / (HJ / 4), uu = (iot % (HJ / 4)) * 4;
+      hd.cv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + uu);
+    }
+    const int ci8 = iot >= NC8 ? iot - NC8 : iot;
+    if (iot < 2 * NC8) {
+      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8;
+      const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
+      hd.h0 = *reinterpret_cast<const f32x4*>(hf + uu);
+      hd.h1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
+    }
+  };
+  auto io_issue = [&](int s_, Held& hd) {
+    if (a.dbg_mode & 1) return;
+    const int t_ = dir ? T - 1 - s_ : s_;
+    constexpr int NG8 = 16 * 4 * HJ / 8;
+#pragma unroll
+    for (int k = 0; k < NG8R; ++k) {
+      const int ci = iot + 256 * k;
+      const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
+      const int u = row >> 2, g = row & 3, b = grp * BG + u;
+      if (ci < NG8 && b < a.B)
+        *reinterpret_cast<u32x4*>(G16 + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) = hd.gv[k];
+    }
+    constexpr int NQ2 = 16 * HJ / 4;
+    {
+      const int u = iot / (HJ / 4), uu = (iot % (HJ / 4)) * 4, b = grp * BG + u;
+      if (iot < NQ2 && b < a.B)
+        *reinterpret_cast<f32x4*>(a.Cs + ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu) = hd.cv;
+    }
+    const bool drop8 = iot >= NC8;
+    const int ci8 = drop8 ? iot - NC8 : iot;
+    if (ci8 < NC8 && (drop8 ? a.Ydb != nullptr : a.Yb != nullptr)) {
+      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8, b = grp * BG + u;
+      if (b < a.B) {
+        f32x4 v0 = hd.h0, v1 = hd.h1;
+        const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
+        if (drop8) {
+          const unsigned bits = dbl[(s_ & 1) * NC8 + ci8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v0[e] = (bits >> e) & 1 ? v0[e] * a.dscale : 0.f;
+            v1[e] = (bits >> (4 + e)) & 1 ? v1[e] * a.dscale : 0.f;
+          }
+        }
+        *reinterpret_cast<bf16x8*>((drop8 ? a.Ydb : a.Yb) + o) =
+            bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
+                   f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+        if (drop8 && a.Y8) {
+          const float xs = a.x8scale;
+          *reinterpret_cast<u32x2*>(a.Y8 + o) =
+              u32x2{pack4_fp8(v0[0] * xs, v0[1] * xs, v0[2] * xs, v0[3] * xs),
+                    pack4_fp8(v1[0] * xs, v1[1] * xs, v1[2] * xs, v1[3] * xs)};
+        }
+      }
+    }
+  };
   // The step loop, instantiated once per role (IO: waves 4-7 move the step's HBM traffic;
   // else waves 0-3 poll the hand-off): each instance keeps only its own role's state live,
   // and both pass the same barriers.
@@ -242,6 +324,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     float c[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) c[t] = 0.f;
+    Held held;
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
       f32x4 acc[TPW];
@@ -265,6 +348,11 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (IO) {
           if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
+          if (st_early) {  // every wave's out ring of step s-1 is written: gather it
+            while (__hip_atomic_load(&outcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8u * s)
+              __builtin_amdgcn_s_sleep(1);
+            io_gather(s - 1, held);
+          }
         } else {
           // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
           // granule carries step s-1's tag; then into the swizzled LDS image
@@ -313,6 +401,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
         if (IO) io_load(s + 1);
+        if (IO && st_early) io_issue(s - 1, held);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
         // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
@@ -365,22 +454,38 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         }
       }
       LSTAMP(4);
+      if (st_after_pub && lane == 0)
+        __hip_atomic_fetch_add(&pubcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         LSTAMP(5);
       }
+      auto write_out = [&]() {  // step s's gates (fp16), c and h into the out ring
+        unsigned short* og = reinterpret_cast<unsigned short*>(ob);
+        float* of = reinterpret_cast<float*>(ob + 8 * HJ);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const int u = 4 * (wave * TPW + t) + q;
+          og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
+          og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
+          of[u] = c[t]; of[HJ + u] = hvals[t];
+        }
+        if (st_early) {  // the io waves gather it before barrier s+1
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_fetch_add(&outcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      };
       // Behind the publish, off the hand-off's path: the io waves store step s-1's saved
       // activations (right after the barrier they delayed the io waves' own publish: 4.2 vs
       // 3.7 us/step at B = 256); every wave puts step s's into the out ring (gates as fp16).
-      if (IO && s > 0) io_store(s - 1);
-      unsigned short* og = reinterpret_cast<unsigned short*>(ob);
-      float* of = reinterpret_cast<float*>(ob + 8 * HJ);
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const int u = 4 * (wave * TPW + t) + q;
-        og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
-        og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
-        of[u] = c[t]; of[HJ + u] = hvals[t];
+      if (IO && st_after_pub) {  // bit 17: the stores queue behind every wave's publish
+        write_out();
+        while (__hip_atomic_load(&pubcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8u * (s + 1))
+          __builtin_amdgcn_s_sleep(1);
+        if (s > 0) io_store(s - 1);
+      } else {
+        if (IO && s > 0 && !st_early) io_store(s - 1);
+        write_out();
       }
       LSTAMP(6);
       // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
@@ -1192,7 +1297,10 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC>
+  const int iov = a.Y ? 0 : (a.dbg_mode & (1 << 19)) ? 2 : (a.dbg_mode & (1 << 17)) ? 1 : 0;
+  auto kf = iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2>
+          : iov == 1 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0>;
+  auto k = fwd ? kf
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true>
