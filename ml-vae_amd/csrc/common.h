@@ -131,18 +131,32 @@ __device__ __forceinline__ void philox4(unsigned long long seed, unsigned long l
 }
 
 // Inter-layer LSTM dropout mask of flat element i (train mode, ref:src/modules/decoder.py:14):
-// keep iff u < 1-p with u = 24-bit uniform from word (i & 3) of Philox(seed, i >> 2); kept
-// elements are scaled by 1/(1-p) (nn.Dropout).  The forward (dropout kernel / recurrence store
-// path) and the backward (dgrad GEMM epilogue) evaluate the same function: no stored mask.
-__device__ __forceinline__ float dropout_word_scale(unsigned w, float keep, float scale) {
-  return ((w >> 8) * (1.f / 16777216.f)) < keep ? scale : 0.f;
+// keep iff u < 1-p, u = the 16-bit uniform in bits [16 (i & 3), +16) of
+//     r(q) = mix64(drop_key(seed) + q * 0x9E3779B97F4A7C15),  q = i >> 2
+// (SplitMix64: the generator's output function over a Weyl sequence; 8 32-bit multiplies per
+// four elements against Philox-4x32-10's 40, which sat on the forward recurrence's poll path and
+// in the dgrad epilogue); kept elements are scaled by 1/(1-p) (nn.Dropout).  The forward (dropout
+// kernel / recurrence store path) and the backward (dgrad GEMM epilogue) evaluate the same
+// function: no stored mask.  tests/philox_np.py dropout_mask restates it.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ unsigned long long drop_key(unsigned long long seed) {
+  return mix64(seed ^ 0x6A09E667F3BCC909ull);
+}
+// the 64 random bits of element quad q under key k = drop_key(seed)
+__device__ __forceinline__ unsigned long long drop_quad(unsigned long long k, unsigned long long q) {
+  return mix64(k + q * 0x9E3779B97F4A7C15ull);
+}
+// element e (0..3) of a quad: scale if kept, else 0
+__device__ __forceinline__ float drop_elem_scale(unsigned long long r, int e, float keep, float scale) {
+  return ((float)((unsigned)(r >> (16 * e)) & 0xffffu) * (1.f / 65536.f)) < keep ? scale : 0.f;
 }
 __device__ __forceinline__ float dropout_scale(unsigned long long seed, unsigned long long i,
                                                float keep, float scale) {
-  unsigned r[4];
-  philox4(seed, i >> 2, r);
-  const unsigned w = (i & 2) ? ((i & 1) ? r[3] : r[2]) : ((i & 1) ? r[1] : r[0]);
-  return dropout_word_scale(w, keep, scale);
+  return drop_elem_scale(drop_quad(drop_key(seed), i >> 2), (int)(i & 3), keep, scale);
 }
 
 // ---- fp8 e4m3 (OCP, gfx950's native format): saturating pack of four floats, round to nearest

@@ -428,6 +428,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   }
   // epilogue: lane holds C[m0 + wm*128 + i*16 + (lane&15)][n0 + wn*64 + j*16 + 4*(lane>>4) + r]
   const bool split = g.splits > 1;
+  const unsigned long long dkey = drop_key(g.dseed);
   float* Cb = g.c16 ? reinterpret_cast<float*>(reinterpret_cast<unsigned short*>(g.C) + bz * g.c_bs)
                     : g.C + bz * g.c_bs;
   float* wsz = split ? g.ws + ((size_t)bz * g.splits + kz) * (size_t)g.M * g.N : nullptr;
@@ -465,11 +466,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
         const int row = m0 + (lr >> 5) * 128 + (2 * pass + ((lr >> 4) & 1)) * 16 + (lr & 15);
         if (row >= g.M || col >= g.N) continue;
         f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * LSR + 4 * c4) + b;
-        if (!split && g.epi == EPI_DROPOUT) {  // one Philox call per 4 aligned columns
-          unsigned w4[4];
-          philox4(g.dseed, (g.doff + (size_t)row * g.ldc + col) >> 2, w4);
+        if (!split && g.epi == EPI_DROPOUT) {  // one mask quad per 4 aligned columns
+          const unsigned long long rq = drop_quad(dkey, (g.doff + (size_t)row * g.ldc + col) >> 2);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
+          for (int r = 0; r < 4; ++r) v[r] *= drop_elem_scale(rq, r, g.dkeep, g.dscale);
         }
         if (!split && g.epi == EPI_LRELU) {
 #pragma unroll
@@ -514,13 +514,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       if (vec && col + 3 < g.N && g.beta == 0.f && g.epi == EPI_NONE) {
         *reinterpret_cast<f32x4*>(cp) = acc[i][j] + b;
       } else if (vec && col + 3 < g.N && g.beta == 0.f && g.epi == EPI_DROPOUT) {
-        // the 4 columns are one aligned Philox counter (row*ldc + col is a multiple of 4):
-        // one call gives all four mask words, as dropout_scale() does element by element
-        unsigned w4[4];
-        philox4(g.dseed, (g.doff + (size_t)row * g.ldc + col) >> 2, w4);
+        // the 4 columns are one aligned mask quad (row*ldc + col is a multiple of 4): one
+        // hash gives all four, as dropout_scale() does element by element
+        const unsigned long long rq = drop_quad(dkey, (g.doff + (size_t)row * g.ldc + col) >> 2);
         f32x4 v = acc[i][j] + b;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] *= dropout_word_scale(w4[r], g.dkeep, g.dscale);
+        for (int r = 0; r < 4; ++r) v[r] *= drop_elem_scale(rq, r, g.dkeep, g.dscale);
         *reinterpret_cast<f32x4*>(cp) = v;
       } else {
 #pragma unroll

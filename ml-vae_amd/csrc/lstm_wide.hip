@@ -164,20 +164,19 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
     }
   };
-  // Philox keep bits (bit e = element e) of h chunk c8 (8 units) at step s_: one call per 4
-  // aligned elements, as dropout_scale in common.h
+  // dropout keep bits (bit e = element e) of h chunk c8 (8 units) at step s_: one mask quad per
+  // 4 aligned elements, as dropout_scale in common.h
   auto drop_bits = [&](int s_, int c8) -> unsigned {
     const int u = c8 / (HJ / 8), uu = (c8 % (HJ / 8)) * 8;
     const int t_ = dir ? T - 1 - s_ : s_;
     const size_t o = ((size_t)(grp * BG + u) * T + t_) * 2 * H + dir * H + j0 + uu;
-    unsigned w0[4], w1[4];
-    philox4(a.dseed, (a.doff + o) >> 2, w0);
-    philox4(a.dseed, (a.doff + o + 4) >> 2, w1);
+    const unsigned long long k = drop_key(a.dseed);
+    const unsigned long long r0 = drop_quad(k, (a.doff + o) >> 2), r1 = drop_quad(k, (a.doff + o + 4) >> 2);
     unsigned bits = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      bits |= (dropout_word_scale(w0[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
-      bits |= (dropout_word_scale(w1[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
+      bits |= (drop_elem_scale(r0, e, a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
+      bits |= (drop_elem_scale(r1, e, a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
     }
     return bits;
   };
@@ -611,14 +610,13 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
     const int u = c8 / (HJ / 8), uu = (c8 % (HJ / 8)) * 8;
     const int t_ = dir ? T - 1 - s_ : s_;
     const size_t o = ((size_t)((2 * pr + c) * BG + u) * T + t_) * 2 * H + dir * H + j0 + uu;
-    unsigned w0[4], w1[4];
-    philox4(a.dseed, (a.doff + o) >> 2, w0);
-    philox4(a.dseed, (a.doff + o + 4) >> 2, w1);
+    const unsigned long long k = drop_key(a.dseed);
+    const unsigned long long r0 = drop_quad(k, (a.doff + o) >> 2), r1 = drop_quad(k, (a.doff + o + 4) >> 2);
     unsigned bits = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      bits |= (dropout_word_scale(w0[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
-      bits |= (dropout_word_scale(w1[e], a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
+      bits |= (drop_elem_scale(r0, e, a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
+      bits |= (drop_elem_scale(r1, e, a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
     }
     return bits;
   };

@@ -206,7 +206,7 @@ static int colsum_chunks(int N, int C) {
 }
 
 // ---------------------------------------------------------------- dropout
-// one thread per 4 consecutive elements: one Philox call gives all four mask words
+// one thread per 4 consecutive elements: one mask quad (common.h drop_quad) gives all four
 __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __restrict__ x,
                                                       float* __restrict__ y,
                                                       unsigned short* __restrict__ ybf,
@@ -215,14 +215,15 @@ __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __r
                                                       unsigned long long qoff, float p, bool vec) {
   const float keep = 1.f - p, scale = 1.f / keep;
   const size_t nq = (n + 3) / 4;
+  const unsigned long long dk = drop_key(seed);
   for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (size_t)gridDim.x * 256) {
-    unsigned r[4] = {0u, 0u, 0u, 0u};
-    if (!mask) philox4(seed, qoff + q, r);  // element offset 4*qoff: the shard's first row
+    unsigned long long r = 0;
+    if (!mask) r = drop_quad(dk, qoff + q);  // element offset 4*qoff: the shard's first row
     if (vec && q * 4 + 3 < n) {  // 16-byte load, 16- / 8-byte stores
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + q * 4);
       f32x4 v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = xv[e] * (mask ? mask[q * 4 + e] : dropout_word_scale(r[e], keep, scale));
+      for (int e = 0; e < 4; ++e) v[e] = xv[e] * (mask ? mask[q * 4 + e] : drop_elem_scale(r, e, keep, scale));
       if (y) *reinterpret_cast<f32x4*>(y + q * 4) = v;
       if (ybf) *reinterpret_cast<bf16x4*>(ybf + q * 4) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
       continue;
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(256) void dropout_kernel(size_t n, const float* __r
     for (int e = 0; e < 4; ++e) {
       const size_t i = q * 4 + e;
       if (i >= n) break;
-      const float m = mask ? mask[i] : dropout_word_scale(r[e], keep, scale);
+      const float m = mask ? mask[i] : drop_elem_scale(r, e, keep, scale);
       const float v = x[i] * m;
       if (y) y[i] = v;
       if (ybf) ybf[i] = (unsigned short)f2bf(v);

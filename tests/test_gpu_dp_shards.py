@@ -69,6 +69,7 @@ def test_bucketed_allreduce_sees_final_gradients(monkeypatch):
     monkeypatch.setattr(mdist, "allreduce_count", lambda c, group=None: c)
     monkeypatch.setattr(mdist, "allreduce_grad_bucket", lambda b, group=None: b.mul_(2.0))
     monkeypatch.setattr(mdist, "allreduce_loss", lambda l, group=None: l.mul_(2.0))
+    monkeypatch.setattr(mdist, "allreduce_err", lambda e, group=None: e)
     eng = VAEEngine(cfg, params=params)
     eng.world = 2
     w = eng.forward(x, lens, eps=eps, train=True)
