@@ -59,7 +59,8 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // IOV: where the io waves store step s-1's saved activations (A/B variants, picked on the host
 // by debug bits): 0 right behind their own publish of step s; 1 behind every wave's publish of
 // step s (bit 17); 2 gathered LDS -> registers before barrier s and stored right after it, so
-// the stores drain during the MFMA / cell phase, away from the publish and the poll (bit 19)
+// the stores drain during the MFMA / cell phase, away from the publish and the poll (bit 19);
+// 3 as 2 without the step barrier: LDS flags per quarter of the h image (bit 29, below)
 template <int TPW, int NKC, int OCC, int IOV = 0>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
@@ -129,7 +130,17 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) { abort_flag = 0; pubcnt = 0; outcnt = 0; }
   constexpr bool st_after_pub = IOV == 1;
-  constexpr bool st_early = IOV == 2;  // (the host picks it only without the fp32 h output)
+  constexpr bool st_early = IOV >= 2;  // (the host picks it only without the fp32 h output)
+  // IOV 3: no step barrier.  Each poller flags its quarter of the h image in LDS (qflag = step)
+  // and each io wave its gx DMA (gflag); every wave then runs its MFMAs quarter by quarter in a
+  // fixed order as the flags appear, so the MFMAs over the quarters that landed first overlap
+  // the wait for the last one (the fixed order keeps the sums bit-identical to IOV 0-2).  The
+  // image slot of step s is rewritten at step s+2 only after every wave has read it: a poller's
+  // data for step s+2 exists only once every member -- this workgroup's every wave included --
+  // published h_{s+1}, i.e. finished its MFMAs of step s+1 (and so of step s).
+  constexpr bool QF = IOV == 3;
+  __shared__ int qflag[4], gflag[4];
+  if (tid < 4) { qflag[tid] = 0; gflag[tid] = 0; }  // (visible after run()'s first barrier)
 
   const size_t xslot = (size_t)BG * H;  // elements per exchange slot
   short* xb = reinterpret_cast<short*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
@@ -347,6 +358,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (IO) {
           if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
+          if (QF && lane == 0) __hip_atomic_store(&gflag[wave - 4], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (st_early) {  // every wave's out ring of step s-1 is written: gather it
             while (__hip_atomic_load(&outcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8u * s)
               __builtin_amdgcn_s_sleep(1);
@@ -393,14 +405,26 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
 #pragma unroll
           for (int i = 0; i < PL; ++i)
             *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
+          if (QF) {  // (on a timeout too: abort_flag is set, nobody waits forever)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&qflag[wave], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
         }
         LWSTAMP();
-        __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
+        auto wait_flag = [&](int* f) {
+          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != s) __builtin_amdgcn_s_sleep(0);
+        };
+        if constexpr (QF) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) wait_flag(&gflag[k]);  // gx ring slot s & 1 landed
+        } else {
+          __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
+          if (abort_flag) break;
+          // gx of step s+1 right behind the barrier (it lands before barrier s+1)
+          if (IO) io_load(s + 1);
+          if (IO && st_early) io_issue(s - 1, held);
+        }
         LSTAMP(2);
-        if (abort_flag) break;
-        // gx of step s+1 right behind the barrier (it lands before barrier s+1)
-        if (IO) io_load(s + 1);
-        if (IO && st_early) io_issue(s - 1, held);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
         // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
@@ -410,6 +434,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (first) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) {
+          if (QF && kc % (NKC / 4) == 0) {
+            wait_flag(&qflag[kc / (NKC / 4)]);  // this quarter of h_{t-1} is in the image
+            if (IO && kc / (NKC / 4) == 3) {    // every poll of step s is done: the io traffic
+              io_load(s + 1);
+              io_issue(s - 1, held);
+            }
+          }
           const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
@@ -419,6 +450,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           }
         }
         if (first) __builtin_amdgcn_s_setprio(0);
+        if (QF && abort_flag) break;
         LSTAMP(3);
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
@@ -1295,8 +1327,10 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  const int iov = a.Y ? 0 : (a.dbg_mode & (1 << 19)) ? 2 : (a.dbg_mode & (1 << 17)) ? 1 : 0;
-  auto kf = iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2>
+  const int iov = a.Y ? 0 : (a.dbg_mode & (1 << 29)) ? 3 : (a.dbg_mode & (1 << 19)) ? 2
+                        : (a.dbg_mode & (1 << 17)) ? 1 : 0;
+  auto kf = iov == 3 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 3>
+          : iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2>
           : iov == 1 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0>;
   auto k = fwd ? kf
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
