@@ -58,10 +58,14 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // OCC = minimum waves per SIMD (2: one 512-thread workgroup per CU)
 // IOV: where the io waves store step s-1's saved activations (A/B variants, picked on the host
 // by debug bits): 0 right behind their own publish of step s; 1 behind every wave's publish of
-// step s (bit 17); 2 gathered LDS -> registers before barrier s and stored right after it, so
+// step s (measured no gain, not instantiated); 2 gathered LDS -> registers before barrier s and stored right after it, so
 // the stores drain during the MFMA / cell phase, away from the publish and the poll (bit 19);
 // 3 as 2 without the step barrier: LDS flags per quarter of the h image (bit 29, below)
-template <int TPW, int NKC, int OCC, int IOV = 0>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
+// XL: exchange layout.  0: [slot][utt][H] -- a 128-byte line (64 units of one utterance) is
+// assembled from 16 granule stores of 8 waves; 1 (debug bit 9): [slot][H / 8][utt][8] -- the 8
+// units of one wave (TPW 2: both tiles, one 16-byte store per utterance) for 8 utterances fill a
+// line, written by one store instruction (TPW 1: two waves' 8-byte halves)
+template <int TPW, int NKC, int OCC, int IOV = 0, bool XL = false>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -369,6 +373,11 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           // granule carries step s-1's tag; then into the swizzled LDS image
           const unsigned tag = step_tag_lg(s - 1, nlg);
           const unsigned ebase = (unsigned)(((s - 1) & nmask) * xslot) + bi * H + wave * PL * 32 + 8 * q;
+          // XL: load i = units u = 32 (wave PL + i) + 8 q = chunk u / 8 of utterance bi
+          const unsigned xbase = (unsigned)(((s - 1) & nmask) * xslot) + (((wave * PL * 32 + 8 * q) >> 3) * 16 + bi) * 8;
+          auto poll_off = [&](int i) -> unsigned {
+            return XL ? xbase + (unsigned)i * (32 / 8) * 16 * 8 : ebase + i * 32;
+          };
           u32x4 hv[PL];
           unsigned spins = 0;
           // When the grid fills the chip, retries re-load only the chunks whose tags were stale,
@@ -382,7 +391,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           while (true) {
 #pragma unroll
             for (int i = 0; i < PL; ++i)
-              if (!partial || !tags_ok(hv[i], tag, true, true)) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
+              if (!partial || !tags_ok(hv[i], tag, true, true)) hv[i] = ld_sc1_b128(xr, poll_off(i) * sizeof(short));
             // step s-1's dropout keep bits, drawn while the first poll's loads are in flight
             // (drawn before them, at the end of step s-1, they delayed the poll's issue; with the
             // io-first MFMAs: c3 12.06 -> 11.92, c2 4.95 -> 4.72 ms/step).  A/B bit 27: the old place
@@ -470,6 +479,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
         const unsigned tag = step_tag_lg(s, nlg);
         const size_t row = (size_t)(s & nmask) * xslot + (size_t)bi * H + j0;
+        unsigned long long gr[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
           // units 4m+1..3 of lane (bi, 0) sit in lanes bi + 16, 32, 48: VALU permlane swaps
@@ -479,9 +489,20 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           const unsigned x2 = __builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1];  // row0 <- row2
           const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];  // row0 <- row3
           const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
-          if (q == 0)
-            publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)),
-                    pack_bf16(hvals[t], h1, h2, h3, tag), same_xcd);
+          gr[t] = pack_bf16(hvals[t], h1, h2, h3, tag);
+          if (!XL && q == 0)
+            publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)), gr[t], same_xcd);
+        }
+        if (XL && q == 0) {
+          const int u0 = j0 + 4 * TPW * wave;  // the wave's first unit
+          const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7);
+          if constexpr (TPW == 2) {
+            const u32x4 v = {(unsigned)gr[0], (unsigned)(gr[0] >> 32), (unsigned)gr[1], (unsigned)(gr[1] >> 32)};
+            if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, cell * sizeof(short), 0, 0);
+            else st_sc1_b128(xr, cell * sizeof(short), v);
+          } else {
+            publish(xr, cell * sizeof(short), gr[0], same_xcd);
+          }
         }
       }
       LSTAMP(4);
@@ -1327,11 +1348,12 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  const int iov = a.Y ? 0 : (a.dbg_mode & (1 << 29)) ? 3 : (a.dbg_mode & (1 << 19)) ? 2
-                        : (a.dbg_mode & (1 << 17)) ? 1 : 0;
-  auto kf = iov == 3 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 3>
-          : iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2>
-          : iov == 1 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0>;
+  const int iov = a.Y ? 0 : (a.dbg_mode & (1 << 29)) ? 3 : (a.dbg_mode & (1 << 19)) ? 2 : 0;
+  const bool xl = (a.dbg_mode & (1 << 9)) != 0;
+  auto kf = xl ? (iov == 3 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 3, true>
+                : iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2, true> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0, true>)
+               : (iov == 3 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 3>
+                : iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0>);
   auto k = fwd ? kf
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)

@@ -191,7 +191,8 @@ def test_interleaved_forward_matches_one_group_kernel(B, T):
 def test_io_store_placement_variants_are_bit_identical(B, T):
     """The forward's io waves store step s-1's saved activations behind their own publish (IOV 0),
     behind every wave's publish (debug bit 17), from registers right after barrier s (bit 19), or
-    with per-quarter LDS flags instead of the step barrier (bit 29):
+    with per-quarter LDS flags instead of the step barrier (bit 29), and publish h through the
+    whole-line exchange layout (bit 9):
     only the timing differs, so every output (fp16 gates, c, bf16 h, bf16 dropout(h)) is
     bit-identical to the default placement, including a ragged last batch group."""
     need_gpu()
@@ -200,7 +201,7 @@ def test_io_store_placement_variants_are_bit_identical(B, T):
     W0, W1 = w[0].float().cuda(), w[1].float().cuda()
     seed, doff, p = 0xA0 + B, 16 * 2 * H, 0.15
     outs = []
-    for mode in (0, 1 << 17, 1 << 19, 1 << 29):
+    for mode in (0, 1 << 19, 1 << 29, 1 << 9, (1 << 9) | (1 << 29)):
         lib().mlvae_lstm_set_debug_mode(mode)
         try:
             G = gx.reshape(N, 8 * H).to(torch.float16).cuda().contiguous()

@@ -1,18 +1,25 @@
 """ELBO parity along a training trajectory, and fp32-mode whole-step parity at the benchmarked sizes.
 
 VERDICT r03: at PyTorch-default init the loss is the model-free value 0.5 (log 2 pi + E[x^2])
-whatever the decoder computes, so a one-step ELBO check cannot see a decoder error.  Here the
-fused engine and the CPU oracle (oracle/vae_cpu.py) each train their OWN copy of the c2 model
-(F=80, enc [80,64,64], z=32, BiLSTM 2x512, dec-FC [1024,64,64,80], dropout 0.15) for 160
-fit_batch steps (ref:src/models/md_model.py:77-88: forward, backward, check_gradients clip 5.0,
-Adam 1e-3) over four fixed batches of low-rank, temporally smooth frames that the model can
-learn: the loss leaves the 1.419 init floor and falls below 1.10.  Every step's randomness is
-the engine's own (in-kernel Philox eps read back, dropout masks replayed on the host), the
-oracle threads its own Adam state, and the ELBO of EVERY step is compared:
+whatever the decoder computes, so a one-step ELBO check cannot see a decoder error.  Here the fused
+engine trains the c2 model (F=80, enc [80,64,64], z=32, BiLSTM 2x512, dec-FC [1024,64,64,80],
+dropout 0.15) for 160 fit_batch steps (ref:src/models/md_model.py:77-88: forward, backward,
+check_gradients clip 5.0, Adam 1e-3) over four fixed batches of low-rank, temporally smooth frames
+the model can learn: the loss leaves the 1.419 init floor and falls below 1.10.  Every step's
+randomness is the engine's own (in-kernel eps read back, dropout masks replayed on the host).
 
-  * fp32 mode (the north-star "ELBO within 1e-4 relative" mode): <= 1e-4 at every step;
-  * bf16 mode (bf16 MFMA operands, fp16 gate buffer): <= BF16_TRAJ at every step (measured,
-    DESIGN.md section 2).
+* Teacher-forced: before EVERY step the oracle (oracle/vae_cpu.py) is handed the engine's state
+  (parameters, Adam moments, step count) and takes the same step.  The ELBO of every step -- on a
+  model that has learned, so the decoder's outputs decide it -- and the Adam update are compared:
+  fp32 mode (the north-star "ELBO within 1e-4 relative" mode) <= 1e-4 at every step; bf16 mode
+  <= BF16_ELBO (measured).
+* Free-running: the oracle trains its OWN copy from the same init for 100 steps, threading its own
+  Adam state.  Two fp32 implementations that round differently drift apart through the chaotic
+  training dynamics (Adam moves weights with tiny gradients by ~lr whichever way their sign falls),
+  so the same run is repeated with the oracle's initial weights moved by one fp32 ulp each: the
+  engine-vs-oracle ELBO gap must stay within 1e-4 while the dynamics are still smooth (the first
+  20 steps) and, later, within a small factor of the gap that one ulp of the oracle's own inputs
+  opens -- a kernel error would show up as a gap far above that intrinsic sensitivity.
 
 The per-step curves are printed (DESIGN.md section 2 records them)."""
 import numpy as np
@@ -28,7 +35,8 @@ pytestmark = pytest.mark.gpu
 F, E, Z, H, L, C = 80, 64, 32, 512, 2, 64
 B, T = 8, 100
 STEPS = 160
-BF16_TRAJ = 1e-2
+FREE_STEPS = 100
+BF16_ELBO = 2e-3
 
 
 def _batches(seed=5):
@@ -45,48 +53,103 @@ def _batches(seed=5):
     return out
 
 
-def _trajectory(prec):
+def _engine(prec):
     from mlvae_hip.engine import VAEConfig, VAEEngine
     from oracle import vae_cpu as O
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec=prec)
     params = O.init_params(F, E, Z, H, L, C, seed=7)
-    eng = VAEEngine(cfg, params=params, seed=31)
-    ocfg = dict(L=L, loss_type="likelihood", kld_weight=1e-3)
-    ref, state = params, {}
+    return VAEEngine(cfg, params=params, seed=31), params
+
+
+def _gpu_step(eng, x, lens):
+    """One engine step; returns (its ELBO, the eps it drew, the dropout masks it drew)."""
+    k = eng.rng_step
+    loss = eng.train_step(x.cuda(), lens.cuda())
+    torch.cuda.synchronize()
+    w = eng.work(B, T)
+    eps = w.eps_used.detach().cpu().view(B, T, Z)
+    masks = torch.stack([torch.from_numpy(dropout_mask((eng.seed * 1000003 + k * 131 + li) & ((1 << 63) - 1),
+                                                       B * T * 2 * H, 0.15)).view(B, T, 2 * H)
+                         for li in range(L - 1)])
+    return float(loss[2].item()), eps, masks
+
+
+OCFG = dict(L=L, loss_type="likelihood", kld_weight=1e-3)
+
+
+@pytest.mark.parametrize("prec,bound", [("fp32", 1e-4), ("bf16", BF16_ELBO)])
+def test_elbo_trajectory_teacher_forced_160_steps(prec, bound):
+    need_gpu()
+    from oracle import vae_cpu as O
+    from step_parity import update_errors
+    eng, _ = _engine(prec)
     data = _batches()
-    gpu_l, ref_l, rel = [], [], []
+    rel, ref_l, gpu_l, signs, uerrs = [], [], [], [], []
     for st in range(STEPS):
         x, lens = data[st % 4]
-        k = eng.rng_step
-        loss = eng.train_step(x.cuda(), lens.cuda())
-        torch.cuda.synchronize()
-        w = eng.work(B, T)
-        eps = w.eps_used.detach().cpu().view(B, T, Z)
-        masks = torch.stack([torch.from_numpy(dropout_mask((eng.seed * 1000003 + k * 131 + li) & ((1 << 63) - 1),
-                                                           B * T * 2 * H, 0.15)).view(B, T, 2 * H)
-                             for li in range(L - 1)])
-        ref, rec = O.train_step(ref, state, x, lens, eps, ocfg, masks, impl="aten")
-        a, b = float(loss[2].item()), float(rec["out"]["loss"].item())
-        gpu_l.append(a)
-        ref_l.append(b)
-        rel.append(abs(a - b) / abs(b))
+        before = {k: v.detach().cpu().clone() for k, v in eng.named_parameters().items()}
+        state = {"step": int(eng.step_ctr.item()),
+                 "m": {k: eng.view(k, eng.exp_avg).detach().cpu().clone() for k in before},
+                 "v": {k: eng.view(k, eng.exp_avg_sq).detach().cpu().clone() for k in before}}
+        got, eps, masks = _gpu_step(eng, x, lens)
+        new_ref, rec = O.train_step(before, state, x, lens, eps, OCFG, masks, impl="aten")
+        want = float(rec["out"]["loss"].item())
+        gpu_l.append(got)
+        ref_l.append(want)
+        rel.append(abs(got - want) / abs(want))
+        if st % 20 == 0 or st == STEPS - 1:
+            sg, ue, _ = update_errors(eng, rec, new_ref, before)
+            signs.append(sg)
+            uerrs.append(ue)
     eng.check_errors()
-    drift = max((eng.view(kk).cpu() - v).abs().max().item() for kk, v in ref.items())
-    return np.array(gpu_l), np.array(ref_l), np.array(rel), drift
-
-
-@pytest.mark.parametrize("prec,bound", [("fp32", 1e-4), ("bf16", BF16_TRAJ)])
-def test_elbo_trajectory_160_steps_matches_oracle(prec, bound):
-    need_gpu()
-    gpu_l, ref_l, rel, drift = _trajectory(prec)
+    rel, ref_l = np.array(rel), np.array(ref_l)
     marks = [0, 1, 10, 40, 80, 120, STEPS - 1]
-    print(f"\n[trajectory {prec}] " + " ".join(f"s{i}:{gpu_l[i]:.5f}/{ref_l[i]:.5f}({rel[i]:.1e})" for i in marks)
+    print(f"\n[teacher-forced {prec}] " + " ".join(f"s{i}:{gpu_l[i]:.5f}/{ref_l[i]:.5f}({rel[i]:.1e})" for i in marks)
           + f" | max rel {rel.max():.2e} at step {int(rel.argmax())}, median {np.median(rel):.2e}, "
-          f"min loss {ref_l.min():.4f}, final max |param - oracle| {drift:.2e}")
+          f"final-20 mean loss {ref_l[-20:].mean():.4f}; update sign min {min(signs) * 100:.2f} %, "
+          f"update err max {max(uerrs):.2e}")
     assert ref_l[0] > 1.3 and ref_l[-20:].mean() < 1.10, "the model must leave the init floor"
-    assert np.all(np.isfinite(gpu_l))
     assert rel.max() <= bound, (rel.max(), int(rel.argmax()))
+    if prec == "fp32":
+        assert min(signs) >= 0.999 and max(uerrs) <= 1e-2, (signs, uerrs)
+    else:
+        assert min(signs) >= 0.995 and max(uerrs) <= 0.15, (signs, uerrs)
+
+
+def test_elbo_trajectory_free_running_fp32_against_one_ulp_control():
+    need_gpu()
+    from oracle import vae_cpu as O
+    eng, params = _engine("fp32")
+    # the control: the oracle from weights one fp32 ulp away (every element, random direction),
+    # the size of the rounding differences two fp32 implementations make
+    gs = torch.Generator().manual_seed(3)
+    bumped = {}
+    for k, v in params.items():
+        d = torch.where(torch.rand(v.shape, generator=gs) < 0.5, float("inf"), float("-inf"))
+        bumped[k] = torch.nextafter(v, d)
+    data = _batches()
+    ref, st_ref, ctl, st_ctl = params, {}, bumped, {}
+    g_l, r_l, c_l = [], [], []
+    for st in range(FREE_STEPS):
+        x, lens = data[st % 4]
+        got, eps, masks = _gpu_step(eng, x, lens)
+        ref, rec = O.train_step(ref, st_ref, x, lens, eps, OCFG, masks, impl="aten")
+        ctl, recc = O.train_step(ctl, st_ctl, x, lens, eps, OCFG, masks, impl="aten")
+        g_l.append(got)
+        r_l.append(float(rec["out"]["loss"].item()))
+        c_l.append(float(recc["out"]["loss"].item()))
+    eng.check_errors()
+    g_l, r_l, c_l = map(np.array, (g_l, r_l, c_l))
+    gap = np.abs(g_l - r_l) / np.abs(r_l)
+    ctl_gap = np.abs(c_l - r_l) / np.abs(r_l)
+    print("\n[free-running fp32] step: engine-vs-oracle / 1-ulp-control gap  " +
+          " ".join(f"s{i}:{gap[i]:.1e}/{ctl_gap[i]:.1e}" for i in (0, 10, 20, 40, 60, 80, FREE_STEPS - 1)))
+    assert gap[:20].max() <= 1e-4, gap[:20].max()
+    # later steps: the engine stays as close to the oracle as the oracle is to itself one ulp away
+    late = slice(40, FREE_STEPS)
+    assert np.median(gap[late]) <= 10 * max(np.median(ctl_gap[late]), 1e-6), \
+        (np.median(gap[late]), np.median(ctl_gap[late]))
 
 
 @pytest.mark.parametrize("B_,seed", [(32, 1301), (256, 1303)])
