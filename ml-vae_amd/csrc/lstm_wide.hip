@@ -56,16 +56,12 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // forward
 // ---------------------------------------------------------------------------------------
 // OCC = minimum waves per SIMD (2: one 512-thread workgroup per CU)
-// IOV: where the io waves store step s-1's saved activations (A/B variants, picked on the host
-// by debug bits): 0 right behind their own publish of step s; 1 behind every wave's publish of
-// step s (measured no gain, not instantiated); 2 gathered LDS -> registers before barrier s and stored right after it, so
-// the stores drain during the MFMA / cell phase, away from the publish and the poll (bit 19);
-// 3 as 2 without the step barrier: LDS flags per quarter of the h image (bit 29, below)
-// XL: exchange layout.  0: [slot][utt][H] -- a 128-byte line (64 units of one utterance) is
-// assembled from 16 granule stores of 8 waves; 1 (debug bit 9): [slot][H / 8][utt][8] -- the 8
-// units of one wave (TPW 2: both tiles, one 16-byte store per utterance) for 8 utterances fill a
-// line, written by one store instruction (TPW 1: two waves' 8-byte halves)
-template <int TPW, int NKC, int OCC, int IOV = 0, bool XL = false>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
+// Exchange layout [slot][H / 8][utt][8]: the 8 units of one wave (TPW 2: both tiles, one
+// 16-byte store per utterance; TPW 1: two waves' 8-byte halves) for 8 utterances fill one
+// 128-byte line, written by one store instruction.  (The earlier [slot][utt][H] layout
+// assembled each line from 16 granule stores of 8 waves: same box, B = 256 / 64 / 32 forward
+// 3.45 / 2.24 / 2.21 -> 3.22 / 1.99 / 1.95 us per step, profiles/ab/r04_fwd_variants.txt.)
+template <int TPW, int NKC, int OCC>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -89,8 +85,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUB);  // [wave][TPW][KLF][lane]
   unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);  // [2][NC8] keep bits
   __shared__ int abort_flag;
-  // LDS arrival counters (A/B variants): waves that published / wrote their out ring, per step
-  __shared__ unsigned pubcnt, outcnt;
 
   // group slots padded to a multiple of 8 (idle slots exit at once): members gid + k * gstride
   // then share one XCD under round-robin dispatch at every batch size (B = 32: 4 groups)
@@ -132,19 +126,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   __shared__ int placement;
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement) &&
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
-  if (tid == 0) { abort_flag = 0; pubcnt = 0; outcnt = 0; }
-  constexpr bool st_after_pub = IOV == 1;
-  constexpr bool st_early = IOV >= 2;  // (the host picks it only without the fp32 h output)
-  // IOV 3: no step barrier.  Each poller flags its quarter of the h image in LDS (qflag = step)
-  // and each io wave its gx DMA (gflag); every wave then runs its MFMAs quarter by quarter in a
-  // fixed order as the flags appear, so the MFMAs over the quarters that landed first overlap
-  // the wait for the last one (the fixed order keeps the sums bit-identical to IOV 0-2).  The
-  // image slot of step s is rewritten at step s+2 only after every wave has read it: a poller's
-  // data for step s+2 exists only once every member -- this workgroup's every wave included --
-  // published h_{s+1}, i.e. finished its MFMAs of step s+1 (and so of step s).
-  constexpr bool QF = IOV == 3;
-  __shared__ int qflag[4], gflag[4];
-  if (tid < 4) { qflag[tid] = 0; gflag[tid] = 0; }  // (visible after run()'s first barrier)
+  if (tid == 0) abort_flag = 0;
 
   const size_t xslot = (size_t)BG * H;  // elements per exchange slot
   short* xb = reinterpret_cast<short*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
@@ -160,6 +142,12 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
   const auto rgx = make_rsrc(G16 + (size_t)grp * BG * T * 8 * H, 0xffffffffu);
+  // debug bit 10 (timing probe only, outputs wrong): the saved activations and the gx loads
+  // addressed time-major (row t * B + b) -- one step's rows of all utterances contiguous in HBM
+  const bool tmaj = (a.dbg_mode & 1024) != 0;
+  auto rowof = [&](int b_, int t_) -> size_t { return tmaj ? (size_t)t_ * a.B + b_ : (size_t)b_ * T + t_; };
+  // (the probe's absolute descriptor: range-checked to the gate buffer, at most 4 GB)
+  const auto rgx_abs = make_rsrc(G16, (unsigned)min((size_t)a.B * T * 8 * H * 2, (size_t)0xffffffffu));
   auto io_load = [&](int s_) {  // input projection of step s_ into gx ring slot s_ & 1
     if (s_ >= T || (s_ > 0 && (a.dbg_mode & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
@@ -172,8 +160,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (b >= a.B) continue;
       // lane l < HJ/2 -> gate l / (HJ/8), units 8 (l % (HJ/8)) .. + 7
       const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
-      const unsigned off = (unsigned)((((size_t)u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
-      const auto rs = rgx;
+      const unsigned off = tmaj ? (unsigned)((((size_t)t_ * a.B + b) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2)
+                                : (unsigned)((((size_t)u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
+      const auto rs = tmaj ? rgx_abs : rgx;
       unsigned short* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
       // nt: read-once stream, kept from displacing the hand-off lines in L2
       if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
@@ -205,7 +194,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
       const int u = row >> 2, g = row & 3, b = grp * BG + u;
       if (b >= a.B) continue;
-      *reinterpret_cast<u32x4*>(G16 + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
+      *reinterpret_cast<u32x4*>(G16 + rowof(b, t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
           *reinterpret_cast<const u32x4*>(src + u * OUB + (g * HJ + uu) * 2);
     }
     // c (fp32) and, when asked, h (fp32): 16 x HJ/4 quads
@@ -213,7 +202,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     for (int qi = iot; qi < NQ2; qi += 256) {
       const int u = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4, b = grp * BG + u;
       if (b >= a.B) continue;
-      const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
+      const size_t o = rowof(b, t_) * 2 * H + dir * H + j0 + uu;
       const float* cf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ);
       *reinterpret_cast<f32x4*>(a.Cs + o) = *reinterpret_cast<const f32x4*>(cf + uu);
       if (a.Y) *reinterpret_cast<f32x4*>(a.Y + o) = *reinterpret_cast<const f32x4*>(cf + HJ + uu);
@@ -228,7 +217,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
-        const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
+        const size_t o = rowof(b, t_) * 2 * H + dir * H + j0 + uu;
         if (drop8) {  // keep bits drawn by the pollers at the end of step s_
           const unsigned bits = dbl[(s_ & 1) * NC8 + ci8];
 #pragma unroll
@@ -241,80 +230,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
                    f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
         if (drop8 && a.Y8) {  // fp8 mode: the next layer's e4m3 projection operand, fixed scale
-          const float xs = a.x8scale;
-          *reinterpret_cast<u32x2*>(a.Y8 + o) =
-              u32x2{pack4_fp8(v0[0] * xs, v0[1] * xs, v0[2] * xs, v0[3] * xs),
-                    pack4_fp8(v1[0] * xs, v1[1] * xs, v1[2] * xs, v1[3] * xs)};
-        }
-      }
-    }
-  };
-  // bit 19: step s_'s saved activations held in registers between the gather (before barrier
-  // s_ + 1) and the stores (right after it); dropout applied at issue time (the pollers draw the
-  // keep bits of step s_ inside the poll of step s_ + 1)
-  constexpr int NG8R = (16 * 4 * HJ / 8 + 255) / 256;  // gate chunks per io thread
-  struct Held { u32x4 gv[NG8R]; f32x4 cv, h0, h1; };
-  auto io_gather = [&](int s_, Held& hd) {
-    const char* src = outr + (s_ & 1) * 16 * OUB;
-    constexpr int NG8 = 16 * 4 * HJ / 8;
-#pragma unroll
-    for (int k = 0; k < NG8R; ++k) {
-      const int ci = iot + 256 * k;
-      if (ci < NG8) {
-        const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
-        hd.gv[k] = *reinterpret_cast<const u32x4*>(src + (row >> 2) * OUB + ((row & 3) * HJ + uu) * 2);
-      }
-    }
-    constexpr int NQ2 = 16 * HJ / 4;
-    if (iot < NQ2) {
-      const int u = iot / (HJ / 4), uu = (iot % (HJ / 4)) * 4;
-      hd.cv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + uu);
-    }
-    const int ci8 = iot >= NC8 ? iot - NC8 : iot;
-    if (iot < 2 * NC8) {
-      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8;
-      const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
-      hd.h0 = *reinterpret_cast<const f32x4*>(hf + uu);
-      hd.h1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
-    }
-  };
-  auto io_issue = [&](int s_, Held& hd) {
-    if (a.dbg_mode & 1) return;
-    const int t_ = dir ? T - 1 - s_ : s_;
-    constexpr int NG8 = 16 * 4 * HJ / 8;
-#pragma unroll
-    for (int k = 0; k < NG8R; ++k) {
-      const int ci = iot + 256 * k;
-      const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
-      const int u = row >> 2, g = row & 3, b = grp * BG + u;
-      if (ci < NG8 && b < a.B)
-        *reinterpret_cast<u32x4*>(G16 + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) = hd.gv[k];
-    }
-    constexpr int NQ2 = 16 * HJ / 4;
-    {
-      const int u = iot / (HJ / 4), uu = (iot % (HJ / 4)) * 4, b = grp * BG + u;
-      if (iot < NQ2 && b < a.B)
-        *reinterpret_cast<f32x4*>(a.Cs + ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu) = hd.cv;
-    }
-    const bool drop8 = iot >= NC8;
-    const int ci8 = drop8 ? iot - NC8 : iot;
-    if (ci8 < NC8 && (drop8 ? a.Ydb != nullptr : a.Yb != nullptr)) {
-      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8, b = grp * BG + u;
-      if (b < a.B) {
-        f32x4 v0 = hd.h0, v1 = hd.h1;
-        const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
-        if (drop8) {
-          const unsigned bits = dbl[(s_ & 1) * NC8 + ci8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v0[e] = (bits >> e) & 1 ? v0[e] * a.dscale : 0.f;
-            v1[e] = (bits >> (4 + e)) & 1 ? v1[e] * a.dscale : 0.f;
-          }
-        }
-        *reinterpret_cast<bf16x8*>((drop8 ? a.Ydb : a.Yb) + o) =
-            bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
-                   f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
-        if (drop8 && a.Y8) {
           const float xs = a.x8scale;
           *reinterpret_cast<u32x2*>(a.Y8 + o) =
               u32x2{pack4_fp8(v0[0] * xs, v0[1] * xs, v0[2] * xs, v0[3] * xs),
@@ -338,7 +253,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     float c[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) c[t] = 0.f;
-    Held held;
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
       f32x4 acc[TPW];
@@ -362,22 +276,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (IO) {
           if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
-          if (QF && lane == 0) __hip_atomic_store(&gflag[wave - 4], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (st_early) {  // every wave's out ring of step s-1 is written: gather it
-            while (__hip_atomic_load(&outcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8u * s)
-              __builtin_amdgcn_s_sleep(1);
-            io_gather(s - 1, held);
-          }
         } else {
           // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
           // granule carries step s-1's tag; then into the swizzled LDS image
           const unsigned tag = step_tag_lg(s - 1, nlg);
-          const unsigned ebase = (unsigned)(((s - 1) & nmask) * xslot) + bi * H + wave * PL * 32 + 8 * q;
-          // XL: load i = units u = 32 (wave PL + i) + 8 q = chunk u / 8 of utterance bi
+          // load i: units u = 32 (wave PL + i) + 8 q = chunk u / 8 of utterance bi
           const unsigned xbase = (unsigned)(((s - 1) & nmask) * xslot) + (((wave * PL * 32 + 8 * q) >> 3) * 16 + bi) * 8;
-          auto poll_off = [&](int i) -> unsigned {
-            return XL ? xbase + (unsigned)i * (32 / 8) * 16 * 8 : ebase + i * 32;
-          };
+          auto poll_off = [&](int i) -> unsigned { return xbase + (unsigned)i * (32 / 8) * 16 * 8; };
           u32x4 hv[PL];
           unsigned spins = 0;
           // When the grid fills the chip, retries re-load only the chunks whose tags were stale,
@@ -414,26 +319,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
 #pragma unroll
           for (int i = 0; i < PL; ++i)
             *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
-          if (QF) {  // (on a timeout too: abort_flag is set, nobody waits forever)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(&qflag[wave], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
         }
         LWSTAMP();
-        auto wait_flag = [&](int* f) {
-          while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != s) __builtin_amdgcn_s_sleep(0);
-        };
-        if constexpr (QF) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) wait_flag(&gflag[k]);  // gx ring slot s & 1 landed
-        } else {
-          __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
-          if (abort_flag) break;
-          // gx of step s+1 right behind the barrier (it lands before barrier s+1)
-          if (IO) io_load(s + 1);
-          if (IO && st_early) io_issue(s - 1, held);
-        }
+        __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
         LSTAMP(2);
+        if (abort_flag) break;
+        // gx of step s+1 right behind the barrier (it lands before barrier s+1)
+        if (IO) io_load(s + 1);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
         // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
@@ -443,13 +335,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (first) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kc = 0; kc < NKC; ++kc) {
-          if (QF && kc % (NKC / 4) == 0) {
-            wait_flag(&qflag[kc / (NKC / 4)]);  // this quarter of h_{t-1} is in the image
-            if (IO && kc / (NKC / 4) == 3) {    // every poll of step s is done: the io traffic
-              io_load(s + 1);
-              io_issue(s - 1, held);
-            }
-          }
           const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
@@ -459,7 +344,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           }
         }
         if (first) __builtin_amdgcn_s_setprio(0);
-        if (QF && abort_flag) break;
         LSTAMP(3);
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
@@ -478,7 +362,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (s + 1 < T) {
         // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
         const unsigned tag = step_tag_lg(s, nlg);
-        const size_t row = (size_t)(s & nmask) * xslot + (size_t)bi * H + j0;
         unsigned long long gr[TPW];
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
@@ -490,10 +373,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];  // row0 <- row3
           const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
           gr[t] = pack_bf16(hvals[t], h1, h2, h3, tag);
-          if (!XL && q == 0)
-            publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)), gr[t], same_xcd);
         }
-        if (XL && q == 0) {
+        if (q == 0) {
           const int u0 = j0 + 4 * TPW * wave;  // the wave's first unit
           const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7);
           if constexpr (TPW == 2) {
@@ -506,38 +387,24 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         }
       }
       LSTAMP(4);
-      if (st_after_pub && lane == 0)
-        __hip_atomic_fetch_add(&pubcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         LSTAMP(5);
       }
-      auto write_out = [&]() {  // step s's gates (fp16), c and h into the out ring
-        unsigned short* og = reinterpret_cast<unsigned short*>(ob);
-        float* of = reinterpret_cast<float*>(ob + 8 * HJ);
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const int u = 4 * (wave * TPW + t) + q;
-          og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
-          og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
-          of[u] = c[t]; of[HJ + u] = hvals[t];
-        }
-        if (st_early) {  // the io waves gather it before barrier s+1
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_fetch_add(&outcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      };
       // Behind the publish, off the hand-off's path: the io waves store step s-1's saved
       // activations (right after the barrier they delayed the io waves' own publish: 4.2 vs
-      // 3.7 us/step at B = 256); every wave puts step s's into the out ring (gates as fp16).
-      if (IO && st_after_pub) {  // bit 17: the stores queue behind every wave's publish
-        write_out();
-        while (__hip_atomic_load(&pubcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 8u * (s + 1))
-          __builtin_amdgcn_s_sleep(1);
-        if (s > 0) io_store(s - 1);
-      } else {
-        if (IO && s > 0 && !st_early) io_store(s - 1);
-        write_out();
+      // 3.7 us/step at B = 256; round 4, same box: behind every wave's publish 3.19 vs 3.19,
+      // from registers right after the barrier 3.35 vs 3.19 us/step); every wave puts step s's
+      // into the out ring (gates as fp16).
+      if (IO && s > 0) io_store(s - 1);
+      unsigned short* og = reinterpret_cast<unsigned short*>(ob);
+      float* of = reinterpret_cast<float*>(ob + 8 * HJ);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int u = 4 * (wave * TPW + t) + q;
+        og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
+        og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
+        of[u] = c[t]; of[HJ + u] = hvals[t];
       }
       LSTAMP(6);
       // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
@@ -1348,13 +1215,7 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  const int iov = a.Y ? 0 : (a.dbg_mode & (1 << 29)) ? 3 : (a.dbg_mode & (1 << 19)) ? 2 : 0;
-  const bool xl = (a.dbg_mode & (1 << 9)) != 0;
-  auto kf = xl ? (iov == 3 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 3, true>
-                : iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2, true> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0, true>)
-               : (iov == 3 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 3>
-                : iov == 2 ? lstm_fwd_wide_kernel<TPW, NKC, OCC, 2> : lstm_fwd_wide_kernel<TPW, NKC, OCC, 0>);
-  auto k = fwd ? kf
+  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC>
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true>
