@@ -117,6 +117,29 @@ constexpr int STW0 = 64, STWN = 32;
         a.dbg[(size_t)STW0 * 16 + i_] = stamp_lds[i_];                         \
   } while (0)
 
+// Realtime stamps of EVERY workgroup (debug bit 3; s_memrealtime, the chip-wide 100 MHz clock, so
+// a producer's publish and its consumer's poll completion compare across CUs): per wave w its
+// publish of step s (slot w) and, for the polling waves, the poll completion of step s (slot
+// 8 + w), steps [STW0, STW0 + STWN); written after the step loop to
+// dbg[T * 16 + blockIdx * STWN * 16 + (s - STW0) * 16 + slot].
+#define RTS_DECL                                                               \
+  __shared__ unsigned long long rts_lds[STWN * 16];                            \
+  const bool rts_on = a.dbg && (a.dbg_mode & 8);                               \
+  if (rts_on)                                                                  \
+    for (int i_ = threadIdx.x; i_ < STWN * 16; i_ += blockDim.x) rts_lds[i_] = 0
+#define RTS(slot)                                                              \
+  do {                                                                         \
+    if (rts_on && (threadIdx.x & 63) == 0 && (unsigned)(s - STW0) < (unsigned)STWN) \
+      rts_lds[(s - STW0) * 16 + (slot)] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#define RTS_FLUSH()                                                            \
+  do {                                                                         \
+    __syncthreads();                                                           \
+    if (rts_on)                                                                \
+      for (int i_ = threadIdx.x; i_ < STWN * 16; i_ += blockDim.x)             \
+        a.dbg[(size_t)a.T * 16 + (size_t)blockIdx.x * STWN * 16 + i_] = rts_lds[i_]; \
+  } while (0)
+
 template <int PREC> struct Elt;
 template <> struct Elt<PREC_F32> { typedef float T; static constexpr int GE = 2; };   // per granule
 template <> struct Elt<PREC_BF16> { typedef short T; static constexpr int GE = 4; };

@@ -79,6 +79,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   static_assert(NQ % 256 == 0, "io split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LSTAMP_DECL;
+  RTS_DECL;
   char* himg = smem;                                        // [2][16][ROWB], swizzled slots
   unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2][16][GXU] fp16
   char* outr = reinterpret_cast<char*>(gxr + 2 * 16 * GXU);                 // [2][16][OUB]
@@ -316,6 +317,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             else __builtin_amdgcn_s_sleep(6);
           }
           LSTAMP(1);
+          RTS(8 + wave);
 #pragma unroll
           for (int i = 0; i < PL; ++i)
             *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
@@ -387,6 +389,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         }
       }
       LSTAMP(4);
+      RTS(wave);
       if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         LSTAMP(5);
@@ -422,6 +425,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   if (io) run(std::true_type{});
   else run(std::false_type{});
   LSTAMP_FLUSH();
+  RTS_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -925,10 +929,16 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) dh[ci] = 0.f;
     u32x4 pv[CPG][NPL];
+    // A/B bits: 17 -- the pollers at priority 2 while they poll (a wave still polling gets the
+    // issue slots before its SIMD partner's post-poll VALU work); 19 -- step s+1's cell inputs
+    // staged to LDS while the first poll's loads are in flight instead of after the poll
+    const bool poll_prio = (a.dbg_mode & (1 << 17)) != 0;
+    const bool early_stage = (a.dbg_mode & (1 << 19)) != 0 && s > 0;
     if (s > 0) {
       const unsigned tag = step_tag_lg(s - 1, nlg);
       const size_t sb = (size_t)((s - 1) & nmask) * xslot + (size_t)js * NJ * HJ * 16;
       unsigned spins = 0;
+      if (poll_prio) __builtin_amdgcn_s_setprio(2);
       // (re-loading only the stale partial tiles measured no faster here: full sweeps)
       while (true) {
 #pragma unroll
@@ -939,6 +949,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
             const size_t off = sb + ((size_t)p * HJ + uc[ci]) * 16 + (cu[ci] >> 3) * 8;
             pv[ci][i] = ld_sc1_b128(xr, (unsigned)(off * sizeof(short)));
           }
+        if (early_stage && spins == 0) stage_cell(s + 1);
         bool ok = true;
 #pragma unroll
         for (int ci = 0; ci < CPG; ++ci)
@@ -953,13 +964,14 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
         else __builtin_amdgcn_s_sleep(1);
       }
+      if (poll_prio) __builtin_amdgcn_s_setprio(0);
     }
     LSTAMP(1);
     LWSTAMP();
     // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
     // s+2's loads issued right behind this step's hand-off -- one program point per step, so
     // the loaded registers need no merge (and no wait for the loads)
-    stage_cell(s + 1);
+    if (!early_stage) stage_cell(s + 1);
     LSTAMP(5);
     // At full-chip grids the prefetch is issued after the barrier, so no wave's HBM loads sit in
     // the CU's memory queue ahead of a later wave's poll loads (same box: c3 12.11 -> 11.99
