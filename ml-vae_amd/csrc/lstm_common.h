@@ -88,6 +88,14 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
       a.dbg[(size_t)s * 16 + (slot) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// debug bit 4 (wide forward): wave 4 (an io wave) of workgroup 0 stamps its own phases into
+// slots 8 + k instead of the per-wave poll-completion stamps
+#define IOSTAMP(k)                                                             \
+  do {                                                                         \
+    if (a.dbg && (a.dbg_mode & 16) && blockIdx.x == 0 && threadIdx.x == 256 && \
+        (unsigned)(s - STW0) < (unsigned)STWN)                                 \
+      stamp_lds[(s - STW0) * 16 + 8 + (k)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
 // LDS-buffered stamps (wide kernels): thread 0 of workgroup 0 records s_memtime at the phase
 // points of steps [STW0, STW0 + STWN) in LDS and writes them to dbg[s*16 + phase] once, after
 // the step loop -- no global store inside the loop, so no vmcnt wait ever queues behind one
@@ -105,7 +113,7 @@ constexpr int STW0 = 64, STWN = 32;
 // per-wave stamp (lane 0 of every wave of workgroup 0) into slot 8 + wave
 #define LWSTAMP()                                                              \
   do {                                                                         \
-    if (a.dbg && blockIdx.x == 0 && (threadIdx.x & 63) == 0 &&                 \
+    if (a.dbg && !(a.dbg_mode & 16) && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
   } while (0)

@@ -256,6 +256,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     for (int t = 0; t < TPW; ++t) c[t] = 0.f;
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
+      IOSTAMP(0);
       f32x4 acc[TPW];
 #pragma unroll
       for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -277,6 +278,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (IO) {
           if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
+          IOSTAMP(1);
         } else {
           // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
           // granule carries step s-1's tag; then into the swizzled LDS image
@@ -327,7 +329,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         LSTAMP(2);
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
+        IOSTAMP(2);
         if (IO) io_load(s + 1);
+        IOSTAMP(3);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
         // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
@@ -347,6 +351,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         }
         if (first) __builtin_amdgcn_s_setprio(0);
         LSTAMP(3);
+        IOSTAMP(4);
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
       char* ob = outr + (s & 1) * 16 * OUB + bi * OUB;
@@ -390,6 +395,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       }
       LSTAMP(4);
       RTS(wave);
+      IOSTAMP(5);
       if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         LSTAMP(5);
@@ -400,6 +406,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       // from registers right after the barrier 3.35 vs 3.19 us/step); every wave puts step s's
       // into the out ring (gates as fp16).
       if (IO && s > 0) io_store(s - 1);
+      IOSTAMP(6);
       unsigned short* og = reinterpret_cast<unsigned short*>(ob);
       float* of = reinterpret_cast<float*>(ob + 8 * HJ);
 #pragma unroll
@@ -929,16 +936,16 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) dh[ci] = 0.f;
     u32x4 pv[CPG][NPL];
-    // A/B bits: 17 -- the pollers at priority 2 while they poll (a wave still polling gets the
-    // issue slots before its SIMD partner's post-poll VALU work); 19 -- step s+1's cell inputs
-    // staged to LDS while the first poll's loads are in flight instead of after the poll
-    const bool poll_prio = (a.dbg_mode & (1 << 17)) != 0;
-    const bool early_stage = (a.dbg_mode & (1 << 19)) != 0 && s > 0;
+    // Step s+1's cell inputs are staged to LDS while the first poll's loads are in flight
+    // instead of after the poll (same box, c3: BPTT 1.292 / 1.283 -> 1.269 / 1.260 ms per
+    // launch; bit 19 restores the old place).  (The pollers at priority 2 while they poll, so a
+    // wave still polling gets the issue slots before its SIMD partner's post-poll work: 1.337 /
+    // 1.304, dropped.)
+    const bool early_stage = !(a.dbg_mode & (1 << 19)) && s > 0;
     if (s > 0) {
       const unsigned tag = step_tag_lg(s - 1, nlg);
       const size_t sb = (size_t)((s - 1) & nmask) * xslot + (size_t)js * NJ * HJ * 16;
       unsigned spins = 0;
-      if (poll_prio) __builtin_amdgcn_s_setprio(2);
       // (re-loading only the stale partial tiles measured no faster here: full sweeps)
       while (true) {
 #pragma unroll
@@ -964,7 +971,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
         else __builtin_amdgcn_s_sleep(1);
       }
-      if (poll_prio) __builtin_amdgcn_s_setprio(0);
     }
     LSTAMP(1);
     LWSTAMP();

@@ -86,7 +86,15 @@ def main():
         off = (w[:, b] - w[:, 0]).median().item()
         print(f"{names[b]:20s} at {off:7.0f} ticks from the step start  (+{off - prev:6.0f})")
         prev = off
-    wv = [(w[:, 8 + k] - w[:, 0]).median().item() for k in range(8) if (w[:, 8 + k] != 0).all()]
+    if a.mode & 16 and not a.bwd:  # wave 4 (io) phases (debug bit 4, lstm_common.h IOSTAMP)
+        io_names = ["io step start", "io vmcnt done", "io barrier", "io gx DMA issued", "io MFMA issued",
+                    "io publish", "io stores issued"]
+        for k, nm in enumerate(io_names):
+            if (w[:, 8 + k] != 0).all():
+                print(f"{nm:20s} at {(w[:, 8 + k] - w[:, 0]).median().item():7.0f} ticks from wave 0's step start")
+        wv = []
+    else:
+        wv = [(w[:, 8 + k] - w[:, 0]).median().item() for k in range(8) if (w[:, 8 + k] != 0).all()]
     if wv:
         print("per-wave poll done   " + " ".join(f"w{k}:{v:.0f}" for k, v in enumerate(wv)))
     per = w[1:, 0] - w[:-1, 0]
