@@ -75,7 +75,10 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
   return *scratch == 0;
 }
 
-// Phase stamps (s_memtime) of workgroup 0, thread 0: dbg[s*16 + phase]
+// Phase stamps (s_memtime) of workgroup 0, thread 0: dbg[s*16 + phase].  The LDS-buffered and
+// realtime stamps below compile only into the kernels' DBG instances (template flag), which the
+// host launches only while a stamp buffer is set (mlvae_lstm_set_debug): production instances
+// carry no stamp code (it cost the forward 35 spilled SGPRs).
 #define STAMP(ph)                                                              \
   do {                                                                         \
     if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                          \
@@ -92,7 +95,7 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
 // slots 8 + k instead of the per-wave poll-completion stamps
 #define IOSTAMP(k)                                                             \
   do {                                                                         \
-    if (a.dbg && (a.dbg_mode & 16) && blockIdx.x == 0 && threadIdx.x == 256 && \
+    if (DBG && a.dbg && (a.dbg_mode & 16) && blockIdx.x == 0 && threadIdx.x == 256 && \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + 8 + (k)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
@@ -101,26 +104,26 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
 // the step loop -- no global store inside the loop, so no vmcnt wait ever queues behind one
 constexpr int STW0 = 64, STWN = 32;
 #define LSTAMP_DECL                                                            \
-  __shared__ unsigned long long stamp_lds[STWN * 16];                          \
-  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                            \
+  __shared__ unsigned long long stamp_lds[DBG ? STWN * 16 : 1];                \
+  if (DBG && a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                     \
     for (int i_ = 0; i_ < STWN * 16; ++i_) stamp_lds[i_] = 0
 #define LSTAMP(ph)                                                             \
   do {                                                                         \
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0 &&                        \
+    if (DBG && a.dbg && blockIdx.x == 0 && threadIdx.x == 0 &&                        \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + (ph)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
 // per-wave stamp (lane 0 of every wave of workgroup 0) into slot 8 + wave
 #define LWSTAMP()                                                              \
   do {                                                                         \
-    if (a.dbg && !(a.dbg_mode & 16) && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && \
+    if (DBG && a.dbg && !(a.dbg_mode & 16) && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #define LSTAMP_FLUSH()                                                         \
   do {                                                                         \
-    __syncthreads();                                                           \
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                          \
+    if (DBG) __syncthreads();                                                  \
+    if (DBG && a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                   \
       for (int i_ = 0; i_ < STWN * 16; ++i_)                                   \
         a.dbg[(size_t)STW0 * 16 + i_] = stamp_lds[i_];                         \
   } while (0)
@@ -131,8 +134,8 @@ constexpr int STW0 = 64, STWN = 32;
 // 8 + w), steps [STW0, STW0 + STWN); written after the step loop to
 // dbg[T * 16 + blockIdx * STWN * 16 + (s - STW0) * 16 + slot].
 #define RTS_DECL                                                               \
-  __shared__ unsigned long long rts_lds[STWN * 16];                            \
-  const bool rts_on = a.dbg && (a.dbg_mode & 8);                               \
+  __shared__ unsigned long long rts_lds[DBG ? STWN * 16 : 1];                  \
+  const bool rts_on = DBG && a.dbg && (a.dbg_mode & 8);                        \
   if (rts_on)                                                                  \
     for (int i_ = threadIdx.x; i_ < STWN * 16; i_ += blockDim.x) rts_lds[i_] = 0
 #define RTS(slot)                                                              \
@@ -142,7 +145,7 @@ constexpr int STW0 = 64, STWN = 32;
   } while (0)
 #define RTS_FLUSH()                                                            \
   do {                                                                         \
-    __syncthreads();                                                           \
+    if (DBG) __syncthreads();                                                  \
     if (rts_on)                                                                \
       for (int i_ = threadIdx.x; i_ < STWN * 16; i_ += blockDim.x)             \
         a.dbg[(size_t)a.T * 16 + (size_t)blockIdx.x * STWN * 16 + i_] = rts_lds[i_]; \

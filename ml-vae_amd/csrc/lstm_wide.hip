@@ -32,6 +32,11 @@
 namespace {
 
 constexpr int WW = 8;  // waves per workgroup
+// forward: k-chunks whose A-fragments (W_hh) live in LDS instead of registers.  4 (was 2) frees
+// the VGPRs that let each wave read a quarter of its B-fragments (h) ahead of the MFMAs that
+// consume them (the 2-chunk build read one fragment, waited for it and issued its two MFMAs, so
+// every k-chunk exposed an LDS round trip)
+constexpr int FWD_KLF = 4;
 #ifndef NT_AUX
 #define NT_AUX 2  // cache policy of the read-once activation streams (2 = nt)
 #endif
@@ -61,7 +66,7 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // 128-byte line, written by one store instruction.  (The earlier [slot][utt][H] layout
 // assembled each line from 16 granule stores of 8 waves: same box, B = 256 / 64 / 32 forward
 // 3.45 / 2.24 / 2.21 -> 3.22 / 1.99 / 1.95 us per step, profiles/ab/r04_fwd_variants.txt.)
-template <int TPW, int NKC, int OCC>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
+template <int TPW, int NKC, int OCC, bool DBG = false>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -72,8 +77,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // out ring bytes per utterance: gates fp16 [i f g o][HJ] | c fp32 [HJ] | h fp32 [HJ] | 16 B
   constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;
   constexpr int NC8 = 16 * HJ / 8;            // 8-unit chunks of h per step
-  constexpr int KLF = 2;                      // k-chunks whose A-fragments live in LDS (VGPR budget)
+  constexpr int KLF = FWD_KLF;                // k-chunks whose A-fragments live in LDS (VGPR budget)
   constexpr int KR = NKC - KLF;               // ... and in registers
+  constexpr int HB = 4;                       // B-fragments (h) read ahead per batch
   constexpr int NQ = 16 * 4 * HJ / 4;         // 16-byte quads of gx / gates per step
   constexpr int QPT = NQ / 256;               // quads per io thread
   static_assert(NQ % 256 == 0, "io split");
@@ -330,7 +336,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
         IOSTAMP(2);
-        if (IO) io_load(s + 1);
+        // gx of step s+1: right behind the barrier, or (bit 17) behind the io wave's publish of
+        // step s, off its barrier -> publish path (the DMA issue stalled ~1,000 ticks there)
+        const bool late_dma = (a.dbg_mode & (1 << 17)) != 0;
+        if (IO && !late_dma) io_load(s + 1);
         IOSTAMP(3);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
@@ -340,13 +349,21 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         const bool first = IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
         if (first) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int kc = 0; kc < NKC; ++kc) {
-          const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
+        for (int k0 = 0; k0 < NKC; k0 += HB) {
+          bf16x8 hfrag[HB];
 #pragma unroll
-          for (int t = 0; t < TPW; ++t) {
-            const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
-                                      : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag, acc[t], 0, 0, 0);
+          for (int i = 0; i < HB; ++i)
+            hfrag[i] = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
+          __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
+#pragma unroll
+          for (int i = 0; i < HB; ++i) {
+            const int kc = k0 + i;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+              const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
+                                        : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag[i], acc[t], 0, 0, 0);
+            }
           }
         }
         if (first) __builtin_amdgcn_s_setprio(0);
@@ -405,6 +422,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       // 3.7 us/step at B = 256; round 4, same box: behind every wave's publish 3.19 vs 3.19,
       // from registers right after the barrier 3.35 vs 3.19 us/step); every wave puts step s's
       // into the out ring (gates as fp16).
+      if (IO && (a.dbg_mode & (1 << 17))) io_load(s + 1);  // (slot s+1 & 1 was last read before barrier s)
       if (IO && s > 0) io_store(s - 1);
       IOSTAMP(6);
       unsigned short* og = reinterpret_cast<unsigned short*>(ob);
@@ -742,7 +760,7 @@ __global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
 // stay as they are)
 // DYB: dY (the layer output's gradient) arrives as bf16 (a.dYb) instead of fp32 (a.Y): half the
 // bytes in the cell-input stream (and in the producers' epilogues)
-template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false>  // HJ = 32 * TPW, H = 32 * NKC
+template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false, bool DBG = false>  // HJ = 32 * TPW, H = 32 * NKC
 __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = 32 * TPW;
   constexpr int H = NKC * 32;
@@ -1170,7 +1188,7 @@ size_t wide_lds(int H, int hj, bool fwd) {
   if (fwd)
     return (size_t)2 * 16 * H * 2 + (size_t)2 * 16 * (4 * hj + 8) * 2 +  // h image, gx ring
            (size_t)2 * 16 * (4 * hj * 2 + 2 * hj * 4 + 16) +              // out ring
-           (size_t)8 * (hj / 32) * 2 * 64 * 16 +  // + the LDS-resident A-fragments (KLF = 2)
+           (size_t)8 * (hj / 32) * FWD_KLF * 64 * 16 +  // + the LDS-resident A-fragments
            (size_t)2 * (16 * hj / 8) * 4;         // + dropout keep bits
   return (size_t)2 * 16 * 4 * hj * 2 +
          (size_t)8 * (H / 128) * (hj / 32) * 64 * 16 +  // + LDS-resident B-fragments (KLB = KC/4)
@@ -1233,11 +1251,16 @@ WidePlan wide_plan(int B, int H, bool fwd) {
 
 template <int TPW, int NKC, int OCC>
 int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  auto k = fwd ? lstm_fwd_wide_kernel<TPW, NKC, OCC>
+  // DBG instances (phase stamps) only while a stamp buffer is set; the BPTT's only for the bf16
+  // train step's form (bf16 dY, no fp8 copy)
+  const bool dbg = a.dbg != nullptr;
+  auto k = fwd ? (dbg ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true> : lstm_fwd_wide_kernel<TPW, NKC, OCC>)
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
-                           : (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true>
-                                    : lstm_bwd_wide_kernel<TPW, NKC, OCC, false>));
+                           : (a.dYb ? (dbg ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true, true>
+                                           : lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true>)
+                                    : (dbg ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, false, true>
+                                           : lstm_bwd_wide_kernel<TPW, NKC, OCC, false>)));
   if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
     mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
     return 2;
