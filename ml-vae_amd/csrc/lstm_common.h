@@ -151,6 +151,15 @@ constexpr int STW0 = 64, STWN = 32;
         a.dbg[(size_t)a.T * 16 + (size_t)blockIdx.x * STWN * 16 + i_] = rts_lds[i_]; \
   } while (0)
 
+// Debug bit 29 (A/B): phase-stagger the independent recurrence chains.  Every group (one batch
+// group of one direction) runs in lock step with its own members only, yet all groups start
+// together and so issue their saved-activation stores / next-step loads in the same chip-wide
+// bursts.  Groups with ((gid ^ gid >> 3) & 1) start ((mode >> 5) & 7) x 1024 cycles late.
+__device__ __forceinline__ void stagger_start(int gid, int mode) {
+  if (!(mode & (1 << 29)) || !((gid ^ (gid >> 3)) & 1)) return;
+  for (int i = 0; i < ((mode >> 5) & 7); ++i) __builtin_amdgcn_s_sleep(16);
+}
+
 template <int PREC> struct Elt;
 template <> struct Elt<PREC_F32> { typedef float T; static constexpr int GE = 2; };   // per granule
 template <> struct Elt<PREC_BF16> { typedef short T; static constexpr int GE = 4; };

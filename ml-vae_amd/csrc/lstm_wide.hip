@@ -249,6 +249,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // else waves 0-3 poll the hand-off): each instance keeps only its own role's state live,
   // and both pass the same barriers.
   const bool late_bits = a.Ydb && !(a.dbg_mode & (1 << 27));
+  const bool late_dma_s = (2 * a.NB * a.NJ <= 64) != ((a.dbg_mode & (1 << 17)) != 0);
   auto run = [&](auto io_tag) {
     constexpr bool IO = decltype(io_tag)::value;
     if (IO) {
@@ -260,6 +261,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     float c[TPW];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) c[t] = 0.f;
+    stagger_start(gid, a.dbg_mode);
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
       IOSTAMP(0);
@@ -336,10 +338,12 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
         IOSTAMP(2);
-        // gx of step s+1: right behind the barrier, or (bit 17) behind the io wave's publish of
-        // step s, off its barrier -> publish path (the DMA issue stalled ~1,000 ticks there)
-        const bool late_dma = (a.dbg_mode & (1 << 17)) != 0;
-        if (IO && !late_dma) io_load(s + 1);
+        // gx of step s+1: right behind the barrier, or behind the io wave's publish of step s,
+        // off its barrier -> publish path (the DMA issue stalls ~1,000 ticks there) but in the
+        // pollers' window.  Same box, in the step: at 64 active workgroups (c2) the late DMA
+        // takes the forward 1.004 -> 0.962 ms per launch, at 128 (c5) and 256 (c3) it costs
+        // (1.016 -> 1.030, 1.266 -> 1.482): by grid size; bit 17 flips the choice (A/B)
+        if (IO && !late_dma_s) io_load(s + 1);
         IOSTAMP(3);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       // 3.7 us/step at B = 256; round 4, same box: behind every wave's publish 3.19 vs 3.19,
       // from registers right after the barrier 3.35 vs 3.19 us/step); every wave puts step s's
       // into the out ring (gates as fp16).
-      if (IO && (a.dbg_mode & (1 << 17))) io_load(s + 1);  // (slot s+1 & 1 was last read before barrier s)
+      if (IO && late_dma_s) io_load(s + 1);  // (slot s+1 & 1 was last read before barrier s)
       if (IO && s > 0) io_store(s - 1);
       IOSTAMP(6);
       unsigned short* og = reinterpret_cast<unsigned short*>(ob);
@@ -1127,6 +1131,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     }
     return true;
   };
+  stagger_start(gid, a.dbg_mode);
   for (int s = 0; s < T; ++s)
     if (!step(s)) break;
   LSTAMP_FLUSH();
