@@ -243,6 +243,14 @@ int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B
                       int ldc, const float* alpha, const float* bias1, const float* bias2, int epi,
                       unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
                       void* stream);
+/* C [M][N] (fp32) = (*alpha) * A^T B over fp8 e4m3 operands stored [K][M] and [K][N] (m- and
+ * n-contiguous rows of lda / ldb bytes): the layer-1 weight gradient dW_ih = dG^T X over the K
+ * frames (ref:src/modules/decoder.py:14-15,22, nn.LSTM's W_ih gradient) on the e4m3 dG the fp8
+ * BPTT writes and the e4m3 layer input the forward writes.  M, N, lda, ldb % 16, 16-byte aligned
+ * operands; deterministic split-K through ws (mlvae_gemm_fp8_tn_workspace_size bytes). */
+size_t mlvae_gemm_fp8_tn_workspace_size(int M, int N, int K);
+int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
+                      const float* alpha, float* ws, size_t ws_bytes, void* stream);
 size_t mlvae_fp8_scale_workspace_size(void);
 int mlvae_fp8_scale(size_t n, const float* x, float other_scale, float* out, float* ws, size_t ws_bytes,
                     void* stream);

@@ -171,3 +171,15 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
   w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
   return (unsigned)w;
 }
+
+// Workgroup barrier for LDS reuse only: the LDS operations done, the global stores left in flight.
+// (__syncthreads() also waits for every outstanding global store: in the 256-squared GEMM's staged
+// epilogue that put four HBM write round trips of the chip-wide store burst into every tile -- the
+// projection's per-tile fixed cost was 13.0 us, 2.35 us without the epilogue, tools/gemm_kscan.py.)
+// Register data a thread loaded from global memory before the barrier is waited for by the
+// compiler's own counted vmcnt where it is used.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+

@@ -46,23 +46,44 @@ __device__ __forceinline__ bf16x8 trfrag(const short* img, int ld, int base, int
   return bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
 }
 
-// Stage rows [t0 - p, t0 - p + R) of utterance b (zero outside [0, T) and for channels >= C)
-// as bf16 into img[R][ld]; fp32 source [N][lds].  C % 4 == 0, CP % 4 == 0.  SUM: add the
-// thread's values to colsum (its column group is fixed when CT % (CP / 4) == 0).
-template <bool SUM>
-__device__ __forceinline__ void stage_rows(short* img, int ld, const float* src, int lds, int b, int T,
-                                           int t_first, int R, int C, int CP, float (&colsum)[4]) {
-  const int c4n = CP / 4;
-  for (int e = threadIdx.x; e < R * c4n; e += CT) {
-    const int r = e / c4n, c = (e - r * c4n) * 4, t = t_first + r;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (t >= 0 && t < T && c < C) v = *(const f32x4*)(src + ((size_t)b * T + t) * lds + c);
-    if (SUM) {
-      colsum[0] += v[0]; colsum[1] += v[1]; colsum[2] += v[2]; colsum[3] += v[3];
-    }
-    *(bf16x4*)(img + r * ld + c) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+// Rows [t_first, t_first + R) of utterance b (zero outside [0, T) and for channels >= C) of an
+// fp32 source [N][lds], element group e = tid + j * CT (row e / (CP / 4), channels 4 (e % (CP / 4))
+// ...): NL 16-byte loads per thread, all issued before any is used, so a tile's rows are in
+// flight together -- and the next tile's while this one's MFMAs run (the one-load-at-a-time
+// staging loop held a few KB in flight per CU: 12 % of HBM).  C % 4 == 0, CP % 4 == 0.
+template <int NL>
+__device__ __forceinline__ void load_rows(f32x4 (&v)[NL], const float* src, int lds, int b, int T, int t_first,
+                                          int R, int C, int CP) {
+  const int c4n = CP / 4, n = R * c4n;
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int e = threadIdx.x + j * CT, r = e / c4n, c = (e - r * c4n) * 4, t = t_first + r;
+    v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e < n && t >= 0 && t < T && c < C) v[j] = *(const f32x4*)(src + ((size_t)b * T + t) * lds + c);
   }
 }
+
+// ... then as bf16 into img[R][ld].  SUM: add the thread's values to colsum (its column group is
+// fixed when CT % (CP / 4) == 0).
+template <bool SUM, int NL>
+__device__ __forceinline__ void store_rows(short* img, int ld, const f32x4 (&v)[NL], int R, int CP,
+                                           float (&colsum)[4]) {
+  const int c4n = CP / 4, n = R * c4n;
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int e = threadIdx.x + j * CT, r = e / c4n, c = (e - r * c4n) * 4;
+    if (e < n) {
+      if (SUM) {
+        colsum[0] += v[j][0]; colsum[1] += v[j][1]; colsum[2] += v[j][2]; colsum[3] += v[j][3];
+      }
+      *(bf16x4*)(img + r * ld + c) = bf16x4{f2bf(v[j][0]), f2bf(v[j][1]), f2bf(v[j][2]), f2bf(v[j][3])};
+    }
+  }
+}
+
+constexpr int NLW = 9;   // window loads per thread: (BM + K - 1) * CinP / 4 <= 72 * 32 = 9 * CT
+constexpr int NLD = 4;   // weight gradient: dy rows, BM * Cout / 4 <= 4 * CT
+constexpr int NLX = 8;   // weight gradient: x window, (BM + K - 1) * Cin16 / 4 <= 8 * CT (host-checked)
 
 struct ConvArgs {
   int T, Cin, Cout, K, CinP;   // product dims (dgrad: Cin = the layer's Cout, Cout = its Cin)
@@ -112,11 +133,21 @@ __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int f = 16 * wave + l15;  // this lane's frame in the tile (B operand column)
   float unused[4];
+  f32x4 win[NLW];
+  if (blockIdx.x < a.ntiles) {
+    const int b = blockIdx.x / a.tpu, t0 = (blockIdx.x - b * a.tpu) * BM;
+    load_rows(win, a.x, a.ldx, b, a.T, t0 - p, BM + K - 1, a.Cin, CinP);
+  }
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int b = tile / a.tpu, t0 = (tile - b * a.tpu) * BM;
-    __syncthreads();  // weights staged / the previous tile's reads done
-    stage_rows<false>(Xl, ldxl, a.x, a.ldx, b, a.T, t0 - p, BM + K - 1, a.Cin, CinP, unused);
-    __syncthreads();
+    lds_barrier();  // weights staged / the previous tile's reads done (its stores stay in flight)
+    store_rows<false>(Xl, ldxl, win, BM + K - 1, CinP, unused);
+    lds_barrier();
+    const int nx = tile + gridDim.x;  // the next tile's window streams in under this tile's MFMAs
+    if (nx < a.ntiles) {
+      const int nb = nx / a.tpu, nt0 = (nx - nb * a.tpu) * BM;
+      load_rows(win, a.x, a.ldx, nb, a.T, nt0 - p, BM + K - 1, a.Cin, CinP);
+    }
     f32x4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -181,12 +212,19 @@ __global__ __launch_bounds__(CT) void conv_wgrad_kernel(WgArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[u][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+  f32x4 vdy[NLD], vx[NLX];
+  auto load_tile = [&](int tile) {
     const int b = tile / a.tpu, t0 = (tile - b * a.tpu) * BM;
-    __syncthreads();
-    stage_rows<true>(DYl, lddy, a.dy, a.lddy, b, a.T, t0, BM, Cout, Cout, bsum);
-    stage_rows<false>(Xl, ldxl, a.x, a.ldx, b, a.T, t0 - p, BM + K - 1, a.Cin, Cin16, bsum);
-    __syncthreads();
+    load_rows(vdy, a.dy, a.lddy, b, a.T, t0, BM, Cout, Cout);
+    load_rows(vx, a.x, a.ldx, b, a.T, t0 - p, BM + K - 1, a.Cin, Cin16);
+  };
+  if (blockIdx.x < a.ntiles) load_tile(blockIdx.x);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    lds_barrier();
+    store_rows<true>(DYl, lddy, vdy, BM, Cout, bsum);
+    store_rows<false>(Xl, ldxl, vx, BM + K - 1, Cin16, bsum);
+    lds_barrier();
+    if (tile + (int)gridDim.x < a.ntiles) load_tile(tile + gridDim.x);  // in flight under the MFMAs
 #pragma unroll
     for (int kk = 0; kk < BM; kk += 32) {
       bf16x8 bf[NT];
@@ -297,7 +335,7 @@ bool dims_ok(int B, int T, int Cin, int Cout, int K) {
 
 extern "C" int mlvae_conv1d_supported(int Cin, int Cout, int K) {
   return dims_ok(1, 1, Cin, Cout, K) && dims_ok(1, 1, Cout, Cin, K) && (Cout == 16 || Cout == 32 || Cout == 64) &&
-         K * round_up(Cin, 16) <= 16 * 4 * MTW;
+         K * round_up(Cin, 16) <= 16 * 4 * MTW && (BM + K - 1) * round_up(Cin, 16) / 4 <= NLX * CT;
 }
 
 extern "C" int mlvae_conv1d_fwd(int B, int T, int Cin, int Cout, int K, const float* x, int ldx, const float* w,

@@ -48,7 +48,8 @@ struct GFArgs {
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
   int c16;            // C stored as 16-bit: 1 fp16 (epi bit EPI_OUT_F16), 2 bf16 (EPI_OUT_BF16)
   const float* alpha; // device scalar multiplying A.B (fp8 operand scales), or null
-  int abl;            // ablation bits (MLVAE_GEMM_ABL, timing only): 1 no MFMA, 2 no staging loads
+  int abl;            // ablation bits (MLVAE_GEMM_ABL, timing only): 1 no MFMA, 2 no staging loads (VAR 6),
+                      // 4 the direct (unstaged) epilogue, 8 no epilogue
   float* ws;
 };
 
@@ -194,6 +195,48 @@ __device__ __forceinline__ i32x8 frag8(const short* img, int base, int lane) {
   return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
 }
 
+// ---- fp8 e4m3 operands stored m/n-contiguous (VAR 9: the weight gradients dW = dG^T X over
+// frames, both operands [frames][columns] as the recurrences write them).  Image: [128 k][256 m]
+// bytes (one K-tile = 128 frames, the same 32 KB as a 64-deep bf16 image); the 16-byte chunk c of
+// k-row kr at slot c ^ swz8(kr).  Fragments by ds_read_b64_tr_b8 (profiles/r04_probe_tr8.txt: in
+// each 16-lane group, lane 2r + h supplies row r's bytes 8h .. 8h + 7 of a 16-column segment and
+// lane i receives column i of the 8 rows), conflict-free: the 16 rows of a 32-lane half (r < 8 of
+// k-rows 8s + r and 32 + 8s + r) take 16 distinct slots.
+__device__ __forceinline__ int swz8(int kr) { return (kr & 7) | (((kr >> 5) & 1) << 3); }
+
+// this wave's 4 LDS-DMA pieces (1 KB each) of one [128 k][256 m] fp8 image; element (m, k) at byte
+// p[k * ld + m]; rows [r0, r0 + 256) bounded by R (R % 16 == 0), k [k0, k0 + 128) by kend
+__device__ __forceinline__ void stage8_mc(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R, int k0,
+                                          int kend, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int piece = wave * 4 + j;
+    const int p = piece * 64 + lane;
+    const int kr = p >> 4, c = (p & 15) ^ swz8(kr);
+    const int gk = k0 + kr, gm = r0 + 16 * c;
+    const unsigned off = (gk < kend && gm < R) ? (unsigned)((size_t)gk * ld + gm) : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+  }
+}
+
+// operand fragment of v_mfma_scale_f32_16x16x128_f8f6f4 from such an image: lane l holds row
+// base + (l & 15) at k = 32 (l >> 4) + j, j < 32 -- four transposed 8-row reads
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v2i_t* lds_v2i_t;
+__device__ __forceinline__ i32x8 frag8_mc(const short* img, int base, int lane) {
+  const char* im = reinterpret_cast<const char*>(img);
+  const int g = lane >> 4, i = lane & 15, r = i >> 1, h = i & 1, cb = base >> 4;
+  i32x8 o;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int kr = 32 * g + 8 * s + r;
+    const v2i_t v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i_t)(im + kr * 256 + ((cb ^ swz8(kr)) << 4) + 8 * h));
+    o[2 * s] = v[0];
+    o[2 * s + 1] = v[1];
+  }
+  return o;
+}
+
 // VAR 0: stage the next K-tile's 8 pieces per wave at the top of the K-step (two buffers);
 // 4: VAR 0 with both k-halves' fragments read up front; 12: ping-pong over a BK-32 ring;
 // 8: fp8 e4m3 operands (both k-contiguous), one 16x16x128 block-scaled MFMA (unit scales) per
@@ -236,7 +279,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   const auto rb = make_rsrc(Bp, OOB);
   const int kbeg = kz * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
-  constexpr int SBK = VAR == 12 ? DBK : TBK;  // K per main-loop step
+  constexpr int SBK = VAR == 12 ? DBK : (VAR == 9 ? 128 : TBK);  // K per main-loop step
   const int nk = kend > kbeg ? (kend - kbeg + SBK - 1) / SBK : 0;
 
   f32x4 acc[8][4];
@@ -344,6 +387,36 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     }
     if (grpw == 0) __builtin_amdgcn_s_barrier();  // both groups pass the same number of barriers
     __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
+  } else if constexpr (VAR == 9) {
+    static_assert(!AKC && !BKC, "VAR 9: fp8 operands stored m/n-contiguous");
+    auto stage_both = [&](int buf, int k0) {
+      stage8_mc(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, wave, lane);
+      stage8_mc(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, wave, lane);
+    };
+    if (nk > 0) {
+      stage_both(0, kbeg);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < nk) stage_both(cur ^ 1, kbeg + (it + 1) * SBK);
+      const short* As = lds + (cur * 2 + 0) * IMG;
+      const short* Bs = lds + (cur * 2 + 1) * IMG;
+      i32x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag8_mc(Bs, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = frag8_mc(As, wm * 128 + i * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0, 0, 0, 127,
+                                                                       0, 127);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   } else if constexpr (VAR == 8) {
     static_assert(AKC && BKC, "fp8 operands are k-contiguous");
     auto stage_both = [&](int buf, int k0) {
@@ -419,6 +492,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   }
   }
 
+  if (g.abl & 8) return;  // timing ablation: no epilogue at all
   if (g.alpha) {  // fp8 operand scales
     const float al = *g.alpha;
 #pragma unroll
@@ -437,12 +511,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   // store instruction then writes one whole 1 KB row segment instead of 16 rows x 64 B
   // (fp32 output, no beta; split partial slabs too).  c2 skinny projection: 88 -> 56 us.
   const bool bias_vec = ((uintptr_t)g.bias1 % 16) == 0 && ((uintptr_t)g.bias2 % 16) == 0;
-  if ((g.N % 4) == 0 && g.beta == 0.f &&
+  if ((g.N % 4) == 0 && g.beta == 0.f && !(g.abl & 4) &&  // (ablation bit 4: the direct stores)
       (split || (vec && bias_vec && (g.epi == EPI_NONE || g.epi == EPI_DROPOUT || g.epi == EPI_LRELU)))) {
     constexpr int LSR = TBN + 4;  // staged row stride (floats)
     float* st = reinterpret_cast<float*>(smem);  // [64][LSR] = 66.5 KB of the 128 KB
     float* dst = split ? wsz : Cb;
     const int ldd = split ? g.N : g.ldc;
+    // the bias columns of this thread, loaded before the first store: a load issued behind the
+    // stores would wait for them (vmcnt counts in issue order)
+    const int c4 = tid & 63, col = n0 + 4 * c4;
+    f32x4 b = {0.f, 0.f, 0.f, 0.f};
+    if (!split && col < g.N) {
+      if (g.bias1) b += *reinterpret_cast<const f32x4*>(g.bias1 + col);
+      if (g.bias2) b += *reinterpret_cast<const f32x4*>(g.bias2 + col);
+    }
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
 #pragma unroll
@@ -453,13 +535,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
           *reinterpret_cast<f32x4*>(st + lr * LSR + wn * 64 + j * 16 + 4 * (lane >> 4)) =
               acc[2 * pass + ii][j];
         }
-      __syncthreads();
-      const int c4 = tid & 63, col = n0 + 4 * c4;
-      f32x4 b = {0.f, 0.f, 0.f, 0.f};
-      if (!split && col < g.N) {
-        if (g.bias1) b += *reinterpret_cast<const f32x4*>(g.bias1 + col);
-        if (g.bias2) b += *reinterpret_cast<const f32x4*>(g.bias2 + col);
-      }
+      lds_barrier();
 #pragma unroll 2  // (fully unrolled, the four passes outgrew the unroller: acc went to scratch)
       for (int q = 0; q < 8; ++q) {
         const int lr = q * 8 + (tid >> 6);  // wave w stores staged rows w, w + 8, ...
@@ -484,7 +560,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
         else
           *reinterpret_cast<f32x4*>(dst + (size_t)row * ldd + col) = v;
       }
-      __syncthreads();  // the staging rows are rewritten by the next pass
+      lds_barrier();  // the staging rows are rewritten by the next pass
     }
     return;
   }
@@ -508,6 +584,26 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       if (row >= g.M) continue;
       if (split) {  // N % 4 == 0 whenever split (checked on the host)
         *reinterpret_cast<f32x4*>(wsz + (size_t)row * g.N + col) = acc[i][j];
+        continue;
+      }
+      if (g.c16) {  // (reached with ablation bit 4 only: 16-bit C always takes the staged path)
+        f32x4 v = acc[i][j] + b;
+        if (g.epi == EPI_DROPOUT) {
+          const unsigned long long rq = drop_quad(dkey, (g.doff + (size_t)row * g.ldc + col) >> 2);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] *= drop_elem_scale(rq, r, g.dkeep, g.dscale);
+        }
+        if (g.epi == EPI_LRELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r]);
+        }
+        unsigned short* cp16 = reinterpret_cast<unsigned short*>(Cb) + (size_t)row * g.ldc + col;
+        if (g.c16 == 2)
+          *reinterpret_cast<u32x2*>(cp16) =
+              u32x2{(unsigned)(unsigned short)f2bf(v[0]) | ((unsigned)(unsigned short)f2bf(v[1]) << 16),
+                    (unsigned)(unsigned short)f2bf(v[2]) | ((unsigned)(unsigned short)f2bf(v[3]) << 16)};
+        else
+          *reinterpret_cast<u32x2*>(cp16) = f2h4(v);
         continue;
       }
       float* cp = Cb + (size_t)row * g.ldc + col;
@@ -746,6 +842,82 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     int blocks = (int)((MN + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     splitk_reduce_fast<<<dim3(blocks, batch), 256, 0, st>>>(g);
+    MLVAE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// C[M,N] (fp32) = (*alpha) * A^T B over fp8 e4m3 (OCP) operands stored [K][M] and [K][N] (m- and
+// n-contiguous: the weight gradient dW = dG^T X over K frames), deterministic split-K through the
+// workspace (mlvae_gemm_fp8_tn_workspace_size).  gemm256_kernel VAR 9.
+static void fp8_tn_plan(int M, int N, int K, int* splits, int* kchunk) {
+  const long tiles = (long)((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
+  int s = 1;
+  if (tiles < 128 && K >= 128 * 16) {
+    s = (int)((split_target() + tiles - 1) / tiles);
+    const int maxs = K / (128 * 8);
+    if (s > maxs) s = maxs;
+    if (s > 32) s = 32;
+    if (s < 1) s = 1;
+  }
+  int kc = (K + s - 1) / s;
+  kc = (kc + 127) / 128 * 128;
+  if (kc < 128) kc = 128;
+  *splits = (K + kc - 1) / kc < 1 ? 1 : (K + kc - 1) / kc;
+  *kchunk = kc;
+}
+
+extern "C" size_t mlvae_gemm_fp8_tn_workspace_size(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  int s, kc;
+  fp8_tn_plan(M, N, K, &s, &kc);
+  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+}
+
+extern "C" int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C,
+                                 int ldc, const float* alpha, float* ws, size_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || !C || !alpha || (K > 0 && (!A || !B))) {
+    mlvae_set_error("mlvae_gemm_fp8_tn: bad shape/ptr");
+    return 1;
+  }
+  if (M == 0 || N == 0) return 0;
+  if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || (lda % 16) || (ldb % 16) || (M % 16) || (N % 16) ||
+      lda < M || ldb < N || N % 4 || ldc % 4 || ((uintptr_t)C % 16) || ldc < N) {
+    mlvae_set_error("mlvae_gemm_fp8_tn: M, N, lda, ldb %% 16, aligned operands, ldc %% 4, aligned C");
+    return 1;
+  }
+  if ((size_t)K * lda >= OOB || (size_t)K * ldb >= OOB) {
+    mlvae_set_error("mlvae_gemm_fp8_tn: operand larger than 2 GB");
+    return 1;
+  }
+  int s, kc;
+  fp8_tn_plan(M, N, K, &s, &kc);
+  if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * sizeof(float))) {
+    mlvae_set_error("mlvae_gemm_fp8_tn: workspace too small (%zu B)", ws_bytes);
+    return 1;
+  }
+  GFArgs g;
+  g.M = M; g.N = N; g.K = K;
+  g.A = static_cast<const short*>(A); g.lda = lda; g.a_bs = 0;   // byte units (VAR 9)
+  g.B = static_cast<const short*>(B); g.ldb = ldb; g.b_bs = 0;
+  g.C = C; g.ldc = ldc; g.c_bs = 0; g.beta = 0.f;
+  g.bias1 = nullptr; g.bias2 = nullptr; g.epi = EPI_NONE; g.aux = nullptr; g.ldaux = 0;
+  g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
+  g.dseed = 0; g.doff = 0; g.dkeep = 1.f; g.dscale = 1.f;
+  g.ws = ws; g.alpha = alpha; g.abl = 0;
+  g.splits = s; g.kchunk = kc;
+  g.group_m = 1;
+  g.c16 = 0;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), 1, s);
+  const int rc = launch_fast_v<false, false, 9>(g, grid, st);
+  if (rc) return rc;
+  MLVAE_CHECK_LAUNCH();
+  if (s > 1) {
+    const size_t MN = (size_t)M * N;
+    int blocks = (int)((MN + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    splitk_reduce_fast<<<dim3(blocks, 1), 256, 0, st>>>(g);
     MLVAE_CHECK_LAUNCH();
   }
   return 0;

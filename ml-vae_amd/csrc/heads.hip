@@ -600,11 +600,13 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
         if (rv) st_saved(a.dP1, (size_t)grow * C2 + col, acc6[j], 1);
       }
     }
-    __syncthreads();  // every wave's sums of this tile are in bred / red
+    // (LDS-only barriers: the tile's saved-intermediate stores and the next tile's prefetch stay
+    // in flight)
+    lds_barrier();  // every wave's sums of this tile are in bred / red
     for (int c = tid; c < NBS; c += 256)
       a.bias_ws[(size_t)tile * NBS + c] = (bred[0][c] + bred[1][c]) + (bred[2][c] + bred[3][c]);
     if (tid == 0) a.partials[tile] = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();  // bred / red are rewritten by the next tile
+    lds_barrier();  // bred / red are rewritten by the next tile
   }
 }
 

@@ -66,7 +66,16 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // 128-byte line, written by one store instruction.  (The earlier [slot][utt][H] layout
 // assembled each line from 16 granule stores of 8 waves: same box, B = 256 / 64 / 32 forward
 // 3.45 / 2.24 / 2.21 -> 3.22 / 1.99 / 1.95 us per step, profiles/ab/r04_fwd_variants.txt.)
-template <int TPW, int NKC, int OCC, bool DBG = false>  // M-tiles per wave (HJ = 32 * TPW), k-chunks of 32 (H = 32 * NKC)
+// AS: asymmetric tile split (TPW 1).  The io waves (4-7) issue the step's HBM traffic, whose
+// issue stalls for ~1,000 ticks behind the chip-wide bursts, so with equal tile shares they
+// published their units last (realtime stamps, tools/lstm_handoff.py: the last producer wave of
+// every hand-off was an io wave, 500-850 ns behind the pollers).  With AS the pollers own both
+// tiles of each SIMD and the io waves only move data: their DMA and stores right behind the
+// barrier, inside the pollers' MFMA / cell phase.  Same box, in the step: forward per launch
+// c2 0.954 -> 0.863, c5 (B = 64) 0.979 -> 0.872, c4 3.95 -> 3.49 ms (profiles/ab/r04_as.txt);
+// the default at TPW 1, debug bit 8 restores equal shares.  At TPW 2 the pollers' 3 tiles
+// spilled 46 VGPRs.
+template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false>  // HJ = 32 * TPW, H = 32 * NKC
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -77,7 +86,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // out ring bytes per utterance: gates fp16 [i f g o][HJ] | c fp32 [HJ] | h fp32 [HJ] | 16 B
   constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;
   constexpr int NC8 = 16 * HJ / 8;            // 8-unit chunks of h per step
-  constexpr int KLF = FWD_KLF;                // k-chunks whose A-fragments live in LDS (VGPR budget)
+  // k-chunks whose A-fragments live in LDS (VGPR budget; at TPW 1 one tile's 16 fit in registers)
+  constexpr int KLF = (TPW == 1 && !AS) ? 0 : FWD_KLF;
   constexpr int KR = NKC - KLF;               // ... and in registers
   constexpr int HB = 4;                       // B-fragments (h) read ahead per batch
   constexpr int NQ = 16 * 4 * HJ / 4;         // 16-byte quads of gx / gates per step
@@ -110,24 +120,30 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const int bglob = grp * BG + bi;
   const bool valid = bglob < a.B;
 
-  // resident A-fragments: tile m = wave*TPW + t, row r = bi -> unit 4m + (r >> 2), gate r & 3;
-  // k-chunks [0, KR) in registers, [KR, NKC) in LDS (lane-linear, conflict-free 16-B reads)
-  bf16x8 wreg[TPW][KR];
+  // tiles per poller / io wave (AS) and a wave's first tile
+  // (TPW 2 as 3 + 1 spilled 46 VGPRs: the split applies to TPW 1 only)
+  static_assert(!AS || TPW == 1, "asymmetric split: TPW 1 only");
+  constexpr int TPP = AS ? 2 : TPW;
+  constexpr int TPI = AS ? 0 : TPW;
+  static_assert(4 * TPP + 4 * TPI == WW * TPW, "every tile owned once");
+  // resident A-fragments: tile m, row r = bi -> unit 4m + (r >> 2), gate r & 3; k-chunks
+  // [0, KR) in registers, [KR, NKC) in LDS (lane-linear, conflict-free 16-B reads)
+  auto load_w = [&](auto* wreg, int m0, int mt) {
+    for (int t = 0; t < mt; ++t) {
+      const int m = m0 + t;
+      const float* wrow = W + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * H;
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int m = wave * TPW + t;
-    const float* wrow = W + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * H;
+      for (int kc = 0; kc < NKC; ++kc) {
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q + 4);
+        bf16x8 v;
 #pragma unroll
-    for (int kc = 0; kc < NKC; ++kc) {
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q);
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q + 4);
-      bf16x8 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] = f2bf(w0[e]); v[4 + e] = f2bf(w1[e]); }
-      if (kc < KR) wreg[t][kc < KR ? kc : 0] = v;
-      else wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane] = v;
+        for (int e = 0; e < 4; ++e) { v[e] = f2bf(w0[e]); v[4 + e] = f2bf(w1[e]); }
+        if (kc < KR) wreg[t][kc < KR ? kc : 0] = v;
+        else wlds[(m * KLF + (kc - KR)) * 64 + lane] = v;
+      }
     }
-  }
+  };
   // group members are blocks gid + k * gstride: one XCD under round-robin dispatch; verified
   // at run time, never assumed (lstm_common.h group_on_one_xcd)
   __shared__ int placement;
@@ -252,31 +268,38 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const bool late_dma_s = (2 * a.NB * a.NJ <= 64) != ((a.dbg_mode & (1 << 17)) != 0);
   auto run = [&](auto io_tag) {
     constexpr bool IO = decltype(io_tag)::value;
+    constexpr int MT = IO ? TPI : TPP;         // this wave's tiles
+    constexpr int MTA = MT > 0 ? MT : 1;       // (array extent)
+    const int m0 = IO ? 4 * TPP + (wave - 4) * TPI : wave * TPP;
+    bf16x8 wreg[MTA][KR];
+    load_w(wreg, m0, MT);
+    // AS with tile-less io waves: their DMA and stores right behind the barrier
+    constexpr bool PURE_IO = IO && MT == 0;
     if (IO) {
       io_load(0);
       io_load(1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    float c[TPW];
+    float c[MTA];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) c[t] = 0.f;
+    for (int t = 0; t < MTA; ++t) c[t] = 0.f;
     stagger_start(gid, a.dbg_mode);
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
       IOSTAMP(0);
-      f32x4 acc[TPW];
+      f32x4 acc[MTA];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < MTA; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       char* hb = himg + (s & 1) * HIMG;
       // this step's input projection (fp16, LDS ring): read before the MFMAs, so the LDS
       // latency is not exposed between the last MFMA and the cell update
-      float gxv[TPW][4];
+      float gxv[MTA][4];
       auto read_gx = [&]() {
         const unsigned short* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const int u = 4 * (wave * TPW + t) + q;
+        for (int t = 0; t < MT; ++t) {
+          const int u = 4 * (m0 + t) + q;
 #pragma unroll
           for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = h2f(gx[g4 * HJ + u]);
         }
@@ -343,14 +366,16 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // pollers' window.  Same box, in the step: at 64 active workgroups (c2) the late DMA
         // takes the forward 1.004 -> 0.962 ms per launch, at 128 (c5) and 256 (c3) it costs
         // (1.016 -> 1.030, 1.266 -> 1.482): by grid size; bit 17 flips the choice (A/B)
-        if (IO && !late_dma_s) io_load(s + 1);
+        if (IO && (PURE_IO || !late_dma_s)) io_load(s + 1);
+        if (PURE_IO && s > 0) io_store(s - 1);  // (out ring slot s-1 & 1 complete at barrier s)
         IOSTAMP(3);
         read_gx();
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
         // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
         // waves' cells following both MFMA streams (same box, alternating: c3 12.06 -> 11.99,
         // c2 4.95 -> 4.79 ms/step).  A/B bits: 25 off; 26 the pollers first instead (no gain)
-        const bool first = IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
+        // (AS: the pollers, owning most tiles, go first)
+        const bool first = AS ? !IO : IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
         if (first) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int k0 = 0; k0 < NKC; k0 += HB) {
@@ -363,9 +388,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           for (int i = 0; i < HB; ++i) {
             const int kc = k0 + i;
 #pragma unroll
-            for (int t = 0; t < TPW; ++t) {
+            for (int t = 0; t < MT; ++t) {
               const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
-                                        : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
+                                        : wlds[((m0 + t) * KLF + (kc - KR)) * 64 + lane];
               acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag[i], acc[t], 0, 0, 0);
             }
           }
@@ -376,9 +401,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
       char* ob = outr + (s & 1) * 16 * OUB + bi * OUB;
-      float hvals[TPW], gates[TPW][4];
+      float hvals[MTA], gates[MTA][4];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) {
+      for (int t = 0; t < MT; ++t) {
         const float ig = sigmoid_fast(acc[t][0] + gxv[t][0]);
         const float fg = sigmoid_fast(acc[t][1] + gxv[t][1]);
         const float gg = tanh_fast(acc[t][2] + gxv[t][2]);
@@ -390,9 +415,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (s + 1 < T) {
         // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
         const unsigned tag = step_tag_lg(s, nlg);
-        unsigned long long gr[TPW];
+        unsigned long long gr[MTA];
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
+        for (int t = 0; t < MT; ++t) {
           // units 4m+1..3 of lane (bi, 0) sit in lanes bi + 16, 32, 48: VALU permlane swaps
           // (lane row 0 of each result) instead of three LDS-routed ds_bpermute round trips
           const unsigned hu = __float_as_uint(hvals[t]);
@@ -402,7 +427,14 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
           gr[t] = pack_bf16(hvals[t], h1, h2, h3, tag);
         }
-        if (q == 0) {
+        if (AS && q == 0) {  // one 8-byte granule per tile
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            const int u0 = j0 + 4 * (m0 + t);
+            publish(xr, ((unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7)) * sizeof(short),
+                    gr[t], same_xcd);
+          }
+        } else if (q == 0) {
           const int u0 = j0 + 4 * TPW * wave;  // the wave's first unit
           const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7);
           if constexpr (TPW == 2) {
@@ -426,14 +458,14 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       // 3.7 us/step at B = 256; round 4, same box: behind every wave's publish 3.19 vs 3.19,
       // from registers right after the barrier 3.35 vs 3.19 us/step); every wave puts step s's
       // into the out ring (gates as fp16).
-      if (IO && late_dma_s) io_load(s + 1);  // (slot s+1 & 1 was last read before barrier s)
-      if (IO && s > 0) io_store(s - 1);
+      if (IO && !PURE_IO && late_dma_s) io_load(s + 1);  // (slot s+1 & 1 was last read before barrier s)
+      if (IO && !PURE_IO && s > 0) io_store(s - 1);
       IOSTAMP(6);
       unsigned short* og = reinterpret_cast<unsigned short*>(ob);
       float* of = reinterpret_cast<float*>(ob + 8 * HJ);
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const int u = 4 * (wave * TPW + t) + q;
+      for (int t = 0; t < MT; ++t) {
+        const int u = 4 * (m0 + t) + q;
         og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
         og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
         of[u] = c[t]; of[HJ + u] = hvals[t];
@@ -771,10 +803,15 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int NJ = H / HJ;                  // workgroups per (dir, group) = producers = consumers
   constexpr int NTW = NKC / 4;                // N-tiles (16 units) per wave: 8 waves cover H
   constexpr int KC = 4 * HJ / 32;             // k-chunks of the own-dG operand (K = 4 HJ)
-  // k-chunks whose B-fragments live in LDS (VGPR budget).  The <2,16> build reloads ~11 spilled
-  // dwords once, in the prologue (not in the step loop: checked in the ISA)
-  constexpr int KLB = KC / 4;
+  // k-chunks whose B-fragments live in LDS (VGPR budget at TPW 2; TPW 1 keeps all of them in
+  // registers).  The <2,16> build reloads ~11 spilled dwords once, in the prologue (not in the
+  // step loop: checked in the ISA)
+  constexpr int KLB = TPW == 1 ? 0 : KC / 4;
   constexpr int KR = KC - KLB;
+  // k-chunks per batch of fragment reads: all 4 at TPW 1 (c2 BPTT 0.999 -> 0.966 ms, c5 1.10 ->
+  // 1.04); at TPW 2 one per batch, the compiler's own order (4: c3 1.230 -> 1.249 ms)
+  constexpr int BKB = TPW == 1 ? 4 : 1;
+  constexpr bool BWL = false;                 // ... with the LDS B-fragments (VGPR budget at TPW 2)
   constexpr int ROWB = 4 * HJ * 2;            // bytes of one A-image row
   constexpr int AIMG = 16 * ROWB;
   constexpr int NPL = NJ / 8;                 // producers per lane in the reduce-scatter
@@ -815,6 +852,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   // resident B-fragments: tile nt -> global units n = (wave*NTW + nt)*16 + col;
   // B[k][n] = W_hh[g*H + j0 + u][n], k = g*HJ + u
   bf16x8 wreg[NTW][KR];
+  static_assert(KLB > 0 || KR == KC, "");
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt) {
     const int n = (wave * NTW + nt) * 16 + bi;
@@ -1077,14 +1115,36 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       f32x4 acc[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // The A-fragments (and, with BWL, the batch's LDS-resident B-fragments) of a batch of BKB
+      // k-chunks are read before its MFMAs: left to itself the compiler issued each read one
+      // k-chunk ahead and waited for it (5 exposed LDS round trips per step at TPW 1)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, kc * 4 + q) * 16);
+      for (int k0 = 0; k0 < KC; k0 += BKB) {
+        bf16x8 afr[BKB];
+        bf16x8 wl[BWL ? NTW : 1][BWL ? BKB : 1];
 #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-          const bf16x8 wf = kc < KR ? wreg[nt][kc < KR ? kc : 0]
-                                    : wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
-          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf, acc[nt], 0, 0, 0);
+        for (int i = 0; i < BKB; ++i)
+          afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
+        if constexpr (BWL) {
+#pragma unroll
+          for (int i = 0; i < BKB; ++i)
+            if (k0 + i >= KR)
+#pragma unroll
+              for (int nt = 0; nt < NTW; ++nt)
+                wl[nt][i] = wlds[((wave * NTW + nt) * KLB + (k0 + i - KR)) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
+#pragma unroll
+        for (int i = 0; i < BKB; ++i) {
+          const int kc = k0 + i;
+#pragma unroll
+          for (int nt = 0; nt < NTW; ++nt) {
+            bf16x8 wf;
+            if (kc < KR) wf = wreg[nt][kc < KR ? kc : 0];
+            else if constexpr (BWL) wf = wl[nt][i];
+            else wf = wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wf, acc[nt], 0, 0, 0);
+          }
         }
       }
       const unsigned tag = step_tag_lg(s, nlg);
@@ -1196,7 +1256,7 @@ size_t wide_lds(int H, int hj, bool fwd) {
            (size_t)8 * (hj / 32) * FWD_KLF * 64 * 16 +  // + the LDS-resident A-fragments
            (size_t)2 * (16 * hj / 8) * 4;         // + dropout keep bits
   return (size_t)2 * 16 * 4 * hj * 2 +
-         (size_t)8 * (H / 128) * (hj / 32) * 64 * 16 +  // + LDS-resident B-fragments (KLB = KC/4)
+         (size_t)8 * (H / 128) * (hj == 32 ? 0 : hj / 32) * 64 * 16 +  // + LDS B-fragments (KLB)
          (size_t)2 * 16 * ((4 * hj * 2 + 16) + 2 * (hj * 4 + 32));  // + staged cell inputs
 }
 
@@ -1259,7 +1319,9 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   // DBG instances (phase stamps) only while a stamp buffer is set; the BPTT's only for the bf16
   // train step's form (bf16 dY, no fp8 copy)
   const bool dbg = a.dbg != nullptr;
-  auto k = fwd ? (dbg ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true> : lstm_fwd_wide_kernel<TPW, NKC, OCC>)
+  const bool as = TPW == 1 && !(a.dbg_mode & (1 << 8));   // the asymmetric split; bit 8: equal shares
+  auto k = fwd ? (dbg ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, true>)
+                      : (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? (dbg ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true, true>

@@ -110,6 +110,8 @@ _SIGS = {
     "mlvae_lstm_bwd_fp8_ex": [I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_fp8_delayed_scale": [P, P, P, F, P, P],
     "mlvae_gemm_fp8_ex": [I, I, I, P, I, P, I, P, I, P, P, P, I, U64, U64, F, P],
+    "mlvae_gemm_fp8_tn_workspace_size": [I, I, I],
+    "mlvae_gemm_fp8_tn": [I, I, I, P, I, P, I, P, I, P, P, SZ, P],
     "mlvae_norm_supported": [I],
     "mlvae_norm_stats": [I, I, I, P, P, P, P, F, P],
     "mlvae_norm_update": [I, P, P, P, I, F, F, P],
@@ -119,6 +121,7 @@ _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
     "mlvae_conv1d_wgrad_workspace_size": SZ,
     "mlvae_fp8_scale_workspace_size": SZ,
+    "mlvae_gemm_fp8_tn_workspace_size": SZ,
     "mlvae_gemm_workspace_size": SZ,
     "mlvae_gemm_ex_workspace_size": SZ,
     "mlvae_colsum_workspace_size": SZ,

@@ -73,6 +73,41 @@ def test_gemm_fp8_matches_fp64_on_the_same_operands(M, N, K, f16):
     assert rel_err(C.float(), ref) < (1e-3 if f16 else 1e-4)
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 8000), (256, 256, 128), (512, 272, 1000), (1040, 512, 5000),
+                                   (4096, 1024, 2000)])
+def test_gemm_fp8_tn_matches_fp64_on_the_same_operands(M, N, K):
+    """mlvae_gemm_fp8_tn: C = alpha A^T B over fp8 operands stored [K][M], [K][N] (the fp8 weight
+    gradient dW_ih = dG^T X over frames; VAR 9, transposed 8-bit LDS reads), split-K deterministic,
+    ragged K (not a multiple of the 128-frame K-tile) and edge tiles."""
+    need_gpu()
+    torch.manual_seed(M + 3 * N + K)
+    A = (torch.randn(K, M, device="cuda") * 4).clamp(-448, 448).to(torch.float8_e4m3fn)
+    B = (torch.randn(K, N, device="cuda") * 4).clamp(-448, 448).to(torch.float8_e4m3fn)
+    alpha = torch.tensor([0.0123], device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    nb = lib().mlvae_gemm_fp8_tn_workspace_size(M, N, K)
+    ws = torch.empty(nb // 4 + 1, device="cuda")
+    check(lib().mlvae_gemm_fp8_tn(M, N, K, A.data_ptr(), M, B.data_ptr(), N, P(C), N, P(alpha), P(ws), nb, stream()))
+    torch.cuda.synchronize()
+    ref = (A.cpu().double().t() @ B.cpu().double()) * 0.0123
+    assert rel_err(C, ref) < 1e-4, rel_err(C, ref)
+    C2 = torch.empty_like(C)   # deterministic: the same bits again
+    check(lib().mlvae_gemm_fp8_tn(M, N, K, A.data_ptr(), M, B.data_ptr(), N, P(C2), N, P(alpha), P(ws), nb, stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
+
+
+def test_gemm_fp8_tn_rejects_bad_shapes():
+    need_gpu()
+    C = torch.empty(16, 16, device="cuda")
+    a = torch.empty(16 * 16, dtype=torch.uint8, device="cuda")
+    alpha = torch.ones(1, device="cuda")
+    assert lib().mlvae_gemm_fp8_tn(16, 16, 16, a.data_ptr(), 8, a.data_ptr(), 16, P(C), 16, P(alpha), None, 0,
+                                   stream()) != 0   # lda < M
+    assert lib().mlvae_gemm_fp8_tn(12, 16, 16, a.data_ptr(), 16, a.data_ptr(), 16, P(C), 16, P(alpha), None, 0,
+                                   stream()) != 0   # M % 16
+
+
 def test_fp8_mode_training_step_matches_oracle():
     """configs[4]'s fp8 mode through the whole fused step (per-GPU batch of B=512 over 8 GPUs:
     64), the layer-1 input projection on fp8 operands, against the fp32 oracle.  Bounds are the

@@ -48,9 +48,12 @@ def _reference(B, T, seed):
     return w, gx, y.detach(), torch.cat(cs, -1).detach(), torch.cat(gates, -1).detach(), dy, dG
 
 
-@pytest.mark.parametrize("B,T,force", [(256, 16, False), (128, 20, False), (200, 12, False),
-                                       (20, 15, True), (48, 9, True)])
-def test_wide_recurrence_matches_fp64_loop(B, T, force):
+# mode: extra debug bits -- 256 (bit 8) runs the TPW 1 forward with equal tile shares instead of the
+# default asymmetric split (the io waves without tiles)
+@pytest.mark.parametrize("B,T,force,mode", [(256, 16, False, 0), (128, 20, False, 0), (200, 12, False, 0),
+                                            (20, 15, True, 0), (48, 9, True, 0), (128, 20, False, 256),
+                                            (48, 9, True, 256)])
+def test_wide_recurrence_matches_fp64_loop(B, T, force, mode):
     need_gpu()
     w, gx, y, cs, gates, dy, dG = _reference(B, T, B + T)
     N = B * T
@@ -65,8 +68,8 @@ def test_wide_recurrence_matches_fp64_loop(B, T, force):
     xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
     err = torch.zeros(1, device="cuda", dtype=torch.int32)
     seed, doff, p = 0x5EED + B, 4 * 2 * H, 0.15
-    if force:
-        lib().mlvae_lstm_set_debug_mode(4096)
+    if force or mode:
+        lib().mlvae_lstm_set_debug_mode((4096 if force else 0) | mode)
     try:
         assert lib().mlvae_lstm_gates_fp16(B, H, 1) == 1
         G0 = G.clone()
@@ -98,7 +101,7 @@ def test_wide_recurrence_matches_fp64_loop(B, T, force):
         # bias-gradient rows: per batch group sums of dG over utterances and steps
         ref_rows = torch.nn.functional.pad(dG, (0, 0, 0, 0, 0, (-B) % 16)).view(-1, 16, T, 8 * H).sum((1, 2))
         assert norm_rel(rows, ref_rows) < 2e-2 and torch.isfinite(rows).all()
-        print(f"\nB={B} T={T} force={force}: Y {rel_err(Y.view(B, T, 2 * H), y):.2e}  dG max-rel {e1:.2e} "
+        print(f"\nB={B} T={T} force={force} mode={mode}: Y {rel_err(Y.view(B, T, 2 * H), y):.2e}  dG max-rel {e1:.2e} "
               f"norm-rel {e2:.2e}")
         assert e1 < TOL_DG and e2 < 2e-2
     finally:

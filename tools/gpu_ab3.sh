@@ -14,7 +14,7 @@ for r in 1 2; do
       python3 -c "
 import json
 d=json.load(open('gpurun_out/ab/${v}_${c}_$r.json')); k=d['kernel_ms']
-print('$v', '$c', $r, f\"{d['ms_per_step']:.3f} ms/step\", ' '.join(f'{n}={k[n]:.3f}' for n in ('lstm_fwd','lstm_bwd','dgrad_l1','proj_l1') if n in k))
+print('$v', '$c', $r, f\"{d['ms_per_step']:.3f} ms/step\", ' '.join(f'{n}={k[n]:.3f}' for n in ('lstm_fwd','lstm_bwd','dgrad_l1','proj_l1','conv_fwd','conv_bwd') if n in k))
 " >> gpurun_out/ab/summary3.txt
     done
   done
