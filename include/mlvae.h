@@ -172,6 +172,14 @@ int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* 
                        float* cells, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
                        unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
                        void* xbuf, size_t xbytes, int* err, void* stream);
+/* As mlvae_lstm_fwd_fp8 with the recurrent product h_{t-1} W_hh^T (ref:src/modules/decoder.py:22,
+ * nn.LSTM's hidden GEMM) itself on e4m3 operands where the wide kernels run their per-GPU-batch
+ * <= 128 form: W_hh with one E8M0 scale per 32-element block, h at 2^8; the exchange of h stays
+ * bf16.  y_drop_bf16 / y_drop_fp8 optional (the top layer has no next-layer input). */
+int mlvae_lstm_fwd_fp8r(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
+                        float* cells, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
+                        unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                        void* xbuf, size_t xbytes, int* err, void* stream);
 int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
                        const float* cells, const float* dy, void* dg_bf16, float* dbias_rows,
                        void* dg_fp8, const float* dg8_scale, unsigned* dg_amax, void* xbuf,

@@ -134,19 +134,37 @@ __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
   const int f = 16 * wave + l15;  // this lane's frame in the tile (B operand column)
   float unused[4];
   f32x4 win[NLW];
+  // input gradient: the LeakyReLU output of the layer below at this lane's frame and channels,
+  // loaded with the tile's window (a load in the epilogue would wait for the next tile's window
+  // loads issued before it: vmcnt counts in issue order)
+  f32x4 axc[NT], axn[NT];
+  auto load_aux = [&](int tile_) {
+    const int b_ = tile_ / a.tpu, t_ = (tile_ - b_ * a.tpu) * BM + f;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      axn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t_ < a.T) axn[nt] = *(const f32x4*)(a.aux + ((size_t)b_ * a.T + t_) * a.ldaux + 16 * nt + 4 * q);
+    }
+  };
   if (blockIdx.x < a.ntiles) {
     const int b = blockIdx.x / a.tpu, t0 = (blockIdx.x - b * a.tpu) * BM;
     load_rows(win, a.x, a.ldx, b, a.T, t0 - p, BM + K - 1, a.Cin, CinP);
+    if (DG && a.aux) load_aux(blockIdx.x);
   }
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int b = tile / a.tpu, t0 = (tile - b * a.tpu) * BM;
     lds_barrier();  // weights staged / the previous tile's reads done (its stores stay in flight)
     store_rows<false>(Xl, ldxl, win, BM + K - 1, CinP, unused);
+    if (DG && a.aux) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) axc[nt] = axn[nt];
+    }
     lds_barrier();
     const int nx = tile + gridDim.x;  // the next tile's window streams in under this tile's MFMAs
     if (nx < a.ntiles) {
       const int nb = nx / a.tpu, nt0 = (nx - nb * a.tpu) * BM;
       load_rows(win, a.x, a.ldx, nb, a.T, nt0 - p, BM + K - 1, a.Cin, CinP);
+      if (DG && a.aux) load_aux(nx);
     }
     f32x4 acc[NT];
 #pragma unroll
@@ -176,10 +194,9 @@ __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r]);
         }
-        if (a.aux) {
-          const f32x4 ax = *(const f32x4*)(a.aux + row * a.ldaux + o);
+        if (DG && a.aux) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] *= lrelu_d(ax[r]);
+          for (int r = 0; r < 4; ++r) v[r] *= lrelu_d(axc[nt][r]);
         }
         *(f32x4*)(a.y + row * a.ldy + o) = v;
       }
@@ -242,22 +259,19 @@ __global__ __launch_bounds__(CT) void conv_wgrad_kernel(WgArgs a) {
       }
     }
   }
-  // slab: dW in torch layout [Cout][Cin][K], then db [Cout]
-  const size_t S = (size_t)Cout * a.Cin * K + Cout;
+  // slab: dW in the accumulators' own order -- [m-tile][n-tile][lane][4], one 16-byte store per
+  // lane and tile pair (1 KB per wave instruction; the torch-layout scatter of 4-byte stores
+  // was the kernel's slowest part) -- then db [Cout]; the reduce writes the torch layout
+  const int NW = MT * NT * 256;
+  const size_t S = (size_t)NW + Cout;
   float* slab = a.slabs + (size_t)blockIdx.x * S;
 #pragma unroll
   for (int u = 0; u < MTW; ++u) {
     const int mt = wave + 4 * u;
     if (mt < MT) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int o = 16 * nt + l15;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * mt + 4 * q + r, j = m / Cin16, i = m - j * Cin16;
-          if (i < a.Cin) slab[((size_t)o * a.Cin + i) * K + j] = acc[u][nt][r];
-        }
-      }
+      for (int nt = 0; nt < NT; ++nt)
+        *reinterpret_cast<f32x4*>(slab + ((size_t)(mt * NT + nt) * 64 + lane) * 4) = acc[u][nt];
     }
   }
   // bias: thread tid summed columns 4 (tid % (Cout / 4)) .. + 3 of its rows
@@ -269,16 +283,41 @@ __global__ __launch_bounds__(CT) void conv_wgrad_kernel(WgArgs a) {
     const int c = threadIdx.x, g = c / 4, r = c - 4 * g;
     float s = 0.f;
     for (int t = g; t < CT; t += c4n) s += red[r * CT + t];
-    slab[(size_t)Cout * a.Cin * K + c] = s;
+    slab[(size_t)NW + c] = s;
   }
 }
 
-__global__ void slab_reduce_kernel(const float* slabs, int G, size_t S, size_t nw, float* dw, float* db) {
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < S; e += (size_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += slabs[(size_t)g * S + e];
-    if (e < nw) dw[e] = s;
-    else if (db) db[e - nw] = s;
+// The slabs are summed in two fixed-order stages (deterministic): block (column chunk, z) sums
+// slabs [z G / NZ, (z + 1) G / NZ) into part[z]; then the NZ partial rows in order.  (One pass
+// with a thread per column walked all G = 256 slabs alone: ~25 K threads, each a 256-deep chain
+// of dependent-address loads -- latency-bound.)
+constexpr int NZ = 16;
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* slabs, int G, size_t S, float* part) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= S) return;
+  const int z = blockIdx.y, g0 = z * G / NZ, g1 = (z + 1) * G / NZ;
+  float s = 0.f;
+#pragma unroll 8  // loads in flight; the adds keep their order
+  for (int g = g0; g < g1; ++g) s += slabs[(size_t)g * S + e];
+  part[(size_t)z * S + e] = s;
+}
+
+// e < nw: slab order ((m-tile * NT + n-tile) * 64 + lane) * 4 + r -> dW[o][i][j] (torch layout) with
+// o = 16 n-tile + (lane & 15), m = 16 m-tile + 4 (lane >> 4) + r = j * Cin16 + i (i < Cin)
+__global__ __launch_bounds__(256) void slab_reduce2_kernel(const float* part, size_t S, size_t nw, int NT, int Cin,
+                                                           int Cin16, int K, float* dw, float* db) {
+  const size_t e = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= S) return;
+  float s = 0.f;
+#pragma unroll
+  for (int z = 0; z < NZ; ++z) s += part[(size_t)z * S + e];
+  if (e < nw) {
+    const int r = (int)(e & 3), lane = (int)((e >> 2) & 63), tp = (int)(e >> 8);
+    const int mt = tp / NT, nt = tp - mt * NT;
+    const int o = 16 * nt + (lane & 15), m = 16 * mt + 4 * (lane >> 4) + r, j = m / Cin16, i = m - j * Cin16;
+    if (i < Cin) dw[((size_t)o * Cin + i) * K + j] = s;
+  } else if (db) {
+    db[e - nw] = s;
   }
 }
 
@@ -374,9 +413,12 @@ static int wgrad_grid(int B, int T) {
   return tiles < device_cus() ? tiles : device_cus();
 }
 
+// slab floats: the accumulators (K * Cin16 / 16 m-tiles x Cout / 16 n-tiles x 256) + the bias row
+static size_t wgrad_slab(int Cin, int Cout, int K) { return (size_t)K * round_up(Cin, 16) * Cout + Cout; }
+
 extern "C" size_t mlvae_conv1d_wgrad_workspace_size(int B, int T, int Cin, int Cout, int K) {
   if (B <= 0 || T <= 0) return 0;
-  return (size_t)wgrad_grid(B, T) * ((size_t)Cout * Cin * K + Cout) * sizeof(float);
+  return ((size_t)wgrad_grid(B, T) + NZ) * wgrad_slab(Cin, Cout, K) * sizeof(float);  // slabs + partials
 }
 
 extern "C" int mlvae_conv1d_wgrad(int B, int T, int Cin, int Cout, int K, const float* dy, int lddy,
@@ -403,10 +445,13 @@ extern "C" int mlvae_conv1d_wgrad(int B, int T, int Cin, int Cout, int K, const 
                : Cout == 32 ? launch_lds(conv_wgrad_kernel<2>, g, lds, s, a)
                             : launch_lds(conv_wgrad_kernel<4>, g, lds, s, a);
   if (rc) return rc;
-  const size_t S = (size_t)Cout * Cin * K + Cout;
+  const size_t S = wgrad_slab(Cin, Cout, K);
   const int rb = (int)((S + 255) / 256);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rb), dim3(256), 0, s, static_cast<const float*>(ws), g, S,
-                     S - Cout, dw, db);
+  float* part = static_cast<float*>(ws) + (size_t)g * S;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rb, NZ), dim3(256), 0, s, static_cast<const float*>(ws), g, S, part);
+  MLVAE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(rb), dim3(256), 0, s, static_cast<const float*>(part), S, S - Cout,
+                     Cout / 16, Cin, a.Cin16, K, dw, db);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -49,6 +49,7 @@ struct LstmArgs {
   const float* g8scale;
   unsigned* g8amax;
   const unsigned short* dYb;  // wide BPTT, optional: dY as bf16 [B*T, 2H] instead of Y (fp32)
+  int rec8;                   // fp8 mode, wide forward at TPW 1: h W_hh on e4m3 operands (F8R)
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -202,6 +203,7 @@ struct WideFp8 {  // the fp8 mode's fused outputs of the wide kernels (LstmArgs 
   unsigned char* dg8 = nullptr;
   const float* g8scale = nullptr;
   unsigned* g8amax = nullptr;
+  int rec8 = 0;  // forward: h W_hh on e4m3 operands (F8R)
 };
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,

@@ -75,7 +75,11 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // c2 0.954 -> 0.863, c5 (B = 64) 0.979 -> 0.872, c4 3.95 -> 3.49 ms (profiles/ab/r04_as.txt);
 // the default at TPW 1, debug bit 8 restores equal shares.  At TPW 2 the pollers' 3 tiles
 // spilled 46 VGPRs.
-template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false>  // HJ = 32 * TPW, H = 32 * NKC
+// F8R (fp8 mode, with AS at TPW 1): h W_hh on the block-scaled 16x16x128 e4m3 MFMA -- W_hh in
+// registers as e4m3 with one E8M0 scale per lane's 32-element k-block (half the VGPRs of bf16),
+// h converted to e4m3 at 2^8 (|h| < 1) as the pollers write it into the LDS image; a quarter of
+// the MFMAs at twice the cycles each.  The exchange stays bf16.
+template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool F8R = false>  // HJ = 32 * TPW, H = 32 * NKC
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -87,7 +91,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;
   constexpr int NC8 = 16 * HJ / 8;            // 8-unit chunks of h per step
   // k-chunks whose A-fragments live in LDS (VGPR budget; at TPW 1 one tile's 16 fit in registers)
-  constexpr int KLF = (TPW == 1 && !AS) ? 0 : FWD_KLF;
+  constexpr int KLF = ((TPW == 1 && !AS) || F8R) ? 0 : FWD_KLF;
+  static_assert(!F8R || (AS && TPW == 1 && NKC % 4 == 0), "fp8 recurrence: the asymmetric TPW-1 form");
+  constexpr int K8 = NKC / 4;                 // F8R: 128-deep k-chunks
+  constexpr int ROW8 = H;                     // F8R: bytes of one e4m3 h-image row
   constexpr int KR = NKC - KLF;               // ... and in registers
   constexpr int HB = 4;                       // B-fragments (h) read ahead per batch
   constexpr int NQ = 16 * 4 * HJ / 4;         // 16-byte quads of gx / gates per step
@@ -271,8 +278,37 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     constexpr int MT = IO ? TPI : TPP;         // this wave's tiles
     constexpr int MTA = MT > 0 ? MT : 1;       // (array extent)
     const int m0 = IO ? 4 * TPP + (wave - 4) * TPI : wave * TPP;
-    bf16x8 wreg[MTA][KR];
-    load_w(wreg, m0, MT);
+    bf16x8 wreg[F8R ? 1 : MTA][F8R ? 1 : KR];
+    i32x8 w8[F8R ? MTA : 1][F8R ? K8 : 1];
+    int w8s[F8R ? MTA : 1][F8R ? K8 : 1];
+    if constexpr (F8R) {
+      // lane (row bi, k-block q): 32 consecutive k of each 128-deep chunk, scaled by 2^(8 - e)
+      // where max |w| of the block = m 2^e, m in [0.5, 1): |w 2^(8-e)| < 256 <= 448
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = m0 + t;
+        const float* wrow = W + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * H;
+#pragma unroll
+        for (int kc = 0; kc < K8; ++kc) {
+          f32x4 v[8];
+          float am = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] = *reinterpret_cast<const f32x4*>(wrow + kc * 128 + 32 * q + 4 * e);
+            am = fmaxf(am, fmaxf(fmaxf(fabsf(v[e][0]), fabsf(v[e][1])), fmaxf(fabsf(v[e][2]), fabsf(v[e][3]))));
+          }
+          // am = m 2^ex, m in [0.5, 1) (normal am; a zero / denormal block gets scale 1)
+          const int ex = am >= 1.17549435e-38f ? (int)((__float_as_uint(am) >> 23) & 255u) - 126 : 8;
+          const float sc = __uint_as_float((unsigned)(127 + 8 - ex) << 23);  // 2^(8 - ex)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w8[t][kc][e] = (int)pack4_fp8(v[e][0] * sc, v[e][1] * sc, v[e][2] * sc, v[e][3] * sc);
+          w8s[t][kc] = 127 + ex - 8;  // E8M0: the block's values are w8 x 2^(ex - 8)
+          __builtin_amdgcn_sched_barrier(0);  // (one chunk's 32 floats live at a time)
+        }
+      }
+    } else {
+      load_w(wreg, m0, MT);
+    }
     // AS with tile-less io waves: their DMA and stores right behind the barrier
     constexpr bool PURE_IO = IO && MT == 0;
     if (IO) {
@@ -351,9 +387,26 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           }
           LSTAMP(1);
           RTS(8 + wave);
+          if constexpr (F8R) {
+            // e4m3 image [16 utt][H bytes]: 16-byte chunk c of row bi at slot c ^ bi; this lane's
+            // 8 units are half q & 1 of chunk 2 (wave PL + i) + q / 2
 #pragma unroll
-          for (int i = 0; i < PL; ++i)
-            *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
+            for (int i = 0; i < PL; ++i) {
+              float f[8];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                f[2 * e] = __uint_as_float(hv[i][e] << 16) * 256.f;
+                f[2 * e + 1] = __uint_as_float(hv[i][e] & 0xffff0000u) * 256.f;
+              }
+              const int c8 = 2 * (wave * PL + i) + (q >> 1);
+              *reinterpret_cast<u32x2*>(hb + bi * ROW8 + ((c8 ^ bi) << 4) + 8 * (q & 1)) =
+                  u32x2{pack4_fp8(f[0], f[1], f[2], f[3]), pack4_fp8(f[4], f[5], f[6], f[7])};
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < PL; ++i)
+              *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
+          }
         }
         LWSTAMP();
         __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
@@ -377,6 +430,24 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // (AS: the pollers, owning most tiles, go first)
         const bool first = AS ? !IO : IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
         if (first) __builtin_amdgcn_s_setprio(1);
+        if constexpr (F8R) {
+          // B-fragments: lane (utt bi, k-block q) reads 32 e4m3 of h at k = 128 kc + 32 q + j
+          i32x8 hf8[K8];
+#pragma unroll
+          for (int kc = 0; kc < K8; ++kc) {
+            const int c8 = 8 * kc + 2 * q;
+            const u32x4 lo = *reinterpret_cast<const u32x4*>(hb + bi * ROW8 + ((c8 ^ bi) << 4));
+            const u32x4 hi = *reinterpret_cast<const u32x4*>(hb + bi * ROW8 + (((c8 + 1) ^ bi) << 4));
+            hf8[kc] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kc = 0; kc < K8; ++kc)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)  // h at E8M0 119 = 2^-8
+              acc[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w8[t][kc], hf8[kc], acc[t], 0, 0, 0,
+                                                                        w8s[t][kc], 0, 119);
+        } else
 #pragma unroll
         for (int k0 = 0; k0 < NKC; k0 += HB) {
           bf16x8 hfrag[HB];
@@ -1320,8 +1391,10 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   // train step's form (bf16 dY, no fp8 copy)
   const bool dbg = a.dbg != nullptr;
   const bool as = TPW == 1 && !(a.dbg_mode & (1 << 8));   // the asymmetric split; bit 8: equal shares
+  const bool f8r = as && a.rec8 && !dbg;    // fp8 mode: e4m3 h W_hh (the asymmetric TPW-1 form only)
   auto k = fwd ? (dbg ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, true>)
-                      : (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
+                      : (f8r ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, TPW == 1>
+                             : as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? (dbg ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true, true>
@@ -1393,6 +1466,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;
   a.dbias = dbias; a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
   a.Y8 = f8.y8; a.x8scale = f8.x8scale; a.dG8 = f8.dg8; a.g8scale = f8.g8scale; a.g8amax = f8.g8amax;
+  a.rec8 = f8.rec8;
   a.dYb = fwd ? nullptr : dyb;
   if (a.Y8 && (!ydb || p.il)) {
     mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one (one-group forward)");

@@ -106,6 +106,7 @@ _SIGS = {
     "mlvae_lstm_set_debug": [P],
     "mlvae_lstm_set_debug_mode": [I],
     "mlvae_lstm_fwd_fp8": [I, I, I, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
+    "mlvae_lstm_fwd_fp8r": [I, I, I, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_bwd_fp8": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_fp8_ex": [I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_fp8_delayed_scale": [P, P, P, F, P, P],
@@ -151,7 +152,12 @@ def lib():
                 f"{LIB_PATH} is missing: build it with `python -m mlvae_hip.build` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
         h = C.CDLL(LIB_PATH)
+        # MLVAE_LIB_PATH (same-box A/B against an older build): entry points that build lacks
+        # stay unbound (a call to one raises); the default library must export every one
+        ab = "MLVAE_LIB_PATH" in os.environ
         for name, args in _SIGS.items():
+            if ab and not hasattr(h, name):
+                continue
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, I)

@@ -375,6 +375,15 @@ class VAEEngine:
                             for li in range(1, cfg.L)}
                 self.g8 = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
                 self.g8_amax = {li: torch.zeros(2, device=self.device, dtype=torch.int32) for li in range(1, cfg.L)}
+                # the fp8 weight gradient dW_ih = dG^T X (e4m3 dG and layer input): alpha =
+                # 1 / (q_dG * x-scale); MLVAE_FP8_WGRAD=0 keeps it in bf16 (A/B)
+                self.fp8_wgrad = os.environ.get("MLVAE_FP8_WGRAD", "1") != "0"
+                # ... and, opt-in (MLVAE_FP8_REC=1), the forward recurrence's h W_hh on e4m3
+                # operands (mlvae_lstm_fwd_fp8r): measured slower at the c5 shard (same box: forward
+                # 0.893 -> 0.936 ms per launch, step 4.94 -> 5.05 ms), so off by default
+                self.fp8_rec = os.environ.get("MLVAE_FP8_REC", "0") == "1"
+                self.x8s = torch.tensor([x8_scale(cfg.dropout)], device=self.device)
+                self.g8w = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
                 self.g8_ready = False  # a previous step's amax exists (the first step's dgrad is bf16)
                 self.g8_par = 0
                 self.f8ws = torch.empty(lib().mlvae_fp8_scale_workspace_size() // 4 + 1, device=self.device)
@@ -757,8 +766,19 @@ class VAEEngine:
             # fp8 mode: the recurrence also writes the next layer's e4m3 input (no cast pass)
             x8_fused = (cfg.fp8 and fuse_drop and not need_y and w.X8 is not None and 2 * H % 16 == 0)
             w.__dict__.setdefault("x8_fused", {})[li + 1] = x8_fused
+            # fp8 mode, opt-in: the recurrent product h W_hh^T on e4m3 operands too
+            # (mlvae_lstm_fwd_fp8r; the wide kernels' per-GPU-batch <= 128 form)
+            rec8 = bool(cfg.fp8 and w.g16 and not need_y and self.fp8_rec)
             with self._timed("lstm_fwd"):
-                if x8_fused:
+                if rec8:
+                    check(l.mlvae_lstm_fwd_fp8r(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
+                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
+                                                _p(w.Cs[li]), _pb(w.Yb[li]),
+                                                _pb(w.Ydb[li]) if fuse_drop else None,
+                                                w.X8.data_ptr() if x8_fused else None, x8_scale(cfg.dropout),
+                                                seed, self._drop_off, cfg.dropout if fuse_drop else 0.0,
+                                                _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd_fp8r")
+                elif x8_fused:
                     check(l.mlvae_lstm_fwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
                                                _p(w.Cs[li]), _pb(w.Yb[li]), _pb(w.Ydb[li]), w.X8.data_ptr(),
@@ -977,6 +997,9 @@ class VAEEngine:
                     ran_f8 = True
                     par = self.g8_par   # this step's amax word; the other holds the last step's
                     am = self.g8_amax[li].data_ptr()
+                    if f8_dgrad and self.fp8_wgrad:  # [q_dG, 1 / (q_dG x-scale)] of the fp8 weight gradient
+                        check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), None, _p(self.x8s), G8_MARGIN,
+                                                        _p(self.g8w[li]), s), "fp8_delayed_scale")
                     check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), am + 4 * par, _p(self.w8s[li]), G8_MARGIN,
                                                     _p(self.g8[li]), s), "fp8_delayed_scale")
                     dyb = bool(getattr(w, "dy_bf16", {}).get(li, False))
@@ -1013,8 +1036,12 @@ class VAEEngine:
                 finally:
                     l.mlvae_gemm_bf16_set_split_target(prev)
 
+            # configs[4]: dW_ih of an fp8 layer on the e4m3 dG (this step's BPTT) and e4m3 input
+            f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and ldx == din and din % 16 == 0
+                       and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, din, N) <= w.gws_bytes)
+
             def wgl_body(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx,
-                         Ybl=Ybl):
+                         Ybl=Ybl, f8w=f8w):
                 if li == 0 and w.enc_fused:
                     # both directions' dW_hh_l0 in one batched 256² launch; dW_ih_l0 and the
                     # biases follow the encoder backward on the main stream (skinny_tn below)
@@ -1027,8 +1054,15 @@ class VAEEngine:
                     # in one batched launch (the two weights are adjacent in the flat gradient);
                     # HIP-event timed when they run on the main stream (the full-chip case)
                     with self._timed(f"wgrad_ih_l{li}"):
-                        self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
-                                   gp(f"decoder.rnn.weight_ih_l{li}"), din)
+                        if f8w:
+                            ws = w.gws_side if self._on_side else w.gws
+                            check(lib().mlvae_gemm_fp8_tn(8 * H, din, N, w.dG8.data_ptr(), 8 * H, w.X8.data_ptr(),
+                                                          din, gp(f"decoder.rnn.weight_ih_l{li}"), din,
+                                                          _p(self.g8w[li], 1), _p(ws), w.gws_bytes, self._stream()),
+                                  "gemm_fp8_tn")
+                        else:
+                            self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
+                                       gp(f"decoder.rnn.weight_ih_l{li}"), din)
                     with self._timed(f"wgrad_hh_l{li}"):
                         self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
                                    gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,

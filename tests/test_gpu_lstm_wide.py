@@ -108,6 +108,45 @@ def test_wide_recurrence_matches_fp64_loop(B, T, force, mode):
         lib().mlvae_lstm_set_debug_mode(0)
 
 
+@pytest.mark.parametrize("B,T", [(64, 24), (40, 17)])
+def test_fp8_recurrence_forward(B, T):
+    """mlvae_lstm_fwd_fp8r (the fp8 mode's forward: h W_hh on e4m3 operands, W_hh with per-32
+    E8M0 block scales, h at 2^8) against the fp64 loop: e4m3 keeps 3 mantissa bits, so the
+    bound is the fp8 one (measured errors printed); the outputs it shares with the bf16 kernel
+    (bf16 h, e4m3 dropout(h)) keep their formats."""
+    need_gpu()
+    w, gx, y, cs, gates, dy, dG = _reference(B, T, 7 * B + T)
+    N = B * T
+    G = gx.reshape(N, 8 * H).to(torch.float16).cuda().contiguous()
+    Cs = torch.empty(N, 2 * H, device="cuda")
+    Yb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+    Ydb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+    Y8 = torch.empty(N, 2 * H, device="cuda", dtype=torch.uint8)
+    W0, W1 = w[0].float().cuda(), w[1].float().cuda()
+    xb = ctypes.c_size_t()
+    check(lib().mlvae_lstm_workspace_size(B, H, 1, ctypes.byref(xb)))
+    xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    seed, doff, p = 0x5EED + B, 0, 0.15
+    check(lib().mlvae_lstm_fwd_fp8r(B, T, H, P(W0), P(W1), P(G), P(Cs), Yb.data_ptr(), Ydb.data_ptr(), Y8.data_ptr(),
+                                    256.0, seed, doff, p, P(xbuf), xb.value, P(err), stream()))
+    torch.cuda.synchronize()
+    assert err.item() == 0
+    yv = Yb.float().view(B, T, 2 * H)
+    e_max, e_norm = rel_err(yv, y), norm_rel(yv, y)
+    e_c = norm_rel(Cs.view(B, T, 2 * H), cs)
+    print(f"\nfp8 recurrence B={B} T={T}: h max-rel {e_max:.2e} norm-rel {e_norm:.2e}, c norm-rel {e_c:.2e}")
+    assert e_norm < 3e-2 and e_c < 3e-2 and e_max < 0.25
+    mask = torch.from_numpy(dropout_mask(seed, doff + N * 2 * H, p)[doff:]).cuda().view(N, 2 * H)
+    assert norm_rel(Ydb.float(), Yb.float() * mask) < 1e-2   # (from the fp32 h, rounded once)
+    # the top layer's form: no dropout outputs
+    G1, Yb1 = gx.reshape(N, 8 * H).to(torch.float16).cuda().contiguous(), torch.empty_like(Yb)
+    check(lib().mlvae_lstm_fwd_fp8r(B, T, H, P(W0), P(W1), P(G1), P(Cs), Yb1.data_ptr(), None, None, 0.0, 0, 0, 0.0,
+                                    P(xbuf), xb.value, P(err), stream()))
+    torch.cuda.synchronize()
+    assert err.item() == 0 and torch.equal(Yb1, Yb)
+
+
 def test_gate_buffer_format_is_checked():
     """fp16 gates only where the wide kernels run; the wide backward needs the bf16 dG output."""
     need_gpu()

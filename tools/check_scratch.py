@@ -20,7 +20,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ALLOWED = ("lstm_bwd_wide_kernel",)
 # the forward recurrence's stamp-instrumented debug instances (DBG = true: mode bits 1-4 only,
 # never the timed path)
-ALLOWED_RE = (re.compile(r"lstm_fwd_wide_kernelILi\d+ELi\d+ELi\d+ELb1E"),)
+ALLOWED_RE = (re.compile(r"lstm_fwd_wide_kernelILi\d+ELi\d+ELi\d+ELb1E"),
+              # the fp8-recurrence forward (F8R): the W_hh quantization in the prologue spills,
+              # the step loop has no scratch access (checked in the ISA)
+              re.compile(r"lstm_fwd_wide_kernelILi\d+ELi\d+ELi\d+ELb0ELb1ELb1E"))
 
 
 def usage(src):

@@ -53,7 +53,7 @@ def main():
             ksteps = np.array(KS) / 64.0
             slope, icpt = np.polyfit(ksteps, np.array(us) / waves, 1)
             tf = [2.0 * M * N * K / (u * 1e-6) / 1e12 for K, u in zip(KS, us)]
-            print(f"VAR {var:2d} {name} (MLVAE_GEMM_ABL={os.environ.get('MLVAE_GEMM_ABL', '0')}): " + " ".join(f"K{K}:{u:.0f}us({t:.0f}TF)" for K, u, t in zip(KS, us, tf)))
+            print(f"VAR {var:2d} {name} (MLVAE_GEMM_ABL={os.environ.get('MLVAE_GEMM_ABL', '0')} STAGGER={os.environ.get('MLVAE_GEMM_STAGGER', '1')}): " + " ".join(f"K{K}:{u:.0f}us({t:.0f}TF)" for K, u, t in zip(KS, us, tf)))
             print(f"   per tile: {slope:.2f} us per 64-deep K-step (MFMA floor at 2.4 GHz 0.85 us), "
                   f"fixed {icpt:.2f} us (prologue + epilogue); at K=1024 fixed share "
                   f"{icpt / (icpt + 16 * slope) * 100:.1f} %", flush=True)
