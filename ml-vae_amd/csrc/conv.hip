@@ -408,9 +408,15 @@ extern "C" int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const 
   return launch_conv<true>(a, B, (hipStream_t)stream);
 }
 
+// weight-gradient workgroups (one slab each): MLVAE_CONV_WG_MULT per CU (A/B; default 1)
 static int wgrad_grid(int B, int T) {
-  const int tiles = B * ((T + BM - 1) / BM);
-  return tiles < device_cus() ? tiles : device_cus();
+  static const int mult = [] {
+    const char* e = getenv("MLVAE_CONV_WG_MULT");
+    const int m = e ? atoi(e) : 1;
+    return m < 1 ? 1 : (m > 4 ? 4 : m);
+  }();
+  const int tiles = B * ((T + BM - 1) / BM), g = mult * device_cus();
+  return tiles < g ? tiles : g;
 }
 
 // slab floats: the accumulators (K * Cin16 / 16 m-tiles x Cout / 16 n-tiles x 256) + the bias row
