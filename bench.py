@@ -362,7 +362,7 @@ def extra_runs(args, device):
         dyb = 2 if getattr(eng, "dy_bf16", False) else 4
         lv = loss.tolist()
         out[key] = {"global_batch": B, "seq_len": T,
-                    "dtype": "fp8-e4m3 layer-1 projection/dgrad, bf16 elsewhere" if cname in FP8 else prec,
+                    "dtype": "fp8-e4m3 layer-1 projection/dgrad/weight gradient, bf16 elsewhere" if cname in FP8 else prec,
                     "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
                     "loss": lv[2]}
