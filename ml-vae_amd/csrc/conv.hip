@@ -106,27 +106,27 @@ __global__ __launch_bounds__(CT) void conv_kernel(ConvArgs a) {
   // packed bf16 weights, once per workgroup: Wl[o][j * CinP + c].  The fp32 weight is read in
   // its own order (coalesced 16-byte loads) and scattered into the LDS image; the padding
   // channels c in [Cin, CinP) are zeroed first.
-  if (a.Cin < CinP) {
+  if (a.Cin < CinP) {  // padding channels [Cin, CinP) of every (o, tap) row: zero
     const int padc = CinP - a.Cin;
-    for (int e = threadIdx.x; e < a.Cout * K * padc; e += CT) {
-      const int o = e / (K * padc), rem = e - o * K * padc, j = rem / padc, c = a.Cin + rem - j * padc;
-      Wl[o * ldw + j * CinP + c] = 0;
+    for (int r = threadIdx.x; r < a.Cout * K; r += CT) {
+      const int o = r / K, jt = r - o * K;
+      short* dst = Wl + o * ldw + jt * CinP + a.Cin;
+      for (int c = 0; c < padc; ++c) dst[c] = 0;
     }
   }
   {
-    const int total4 = a.Cout * a.Cin * K / 4;  // the layer weight [Lo][Li][K], Lo * Li * K elements
-    const f32x4* w4 = reinterpret_cast<const f32x4*>(a.w);
-    for (int e4 = threadIdx.x; e4 < total4; e4 += CT) {
-      const f32x4 v = w4[e4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int idx = 4 * e4 + r, j = idx % K, rc = idx / K;
-        const int lo = rc / a.Lc, li = rc - lo * a.Lc;  // layer (out, in) channel
-        // forward: product row o = lo, column c = li, tap j; input gradient: o = li, c = lo,
-        // tap K - 1 - j (transposed, time-flipped)
-        const int o = DG ? li : lo, c = DG ? lo : li, jj = DG ? K - 1 - j : j;
-        Wl[o * ldw + jj * CinP + c] = f2bf(v[r]);
-      }
+    // the layer weight [Lo][Li][K]: one thread per (lo, li) pair reads its K contiguous taps --
+    // one integer division per pair (per element, three had made this prologue most of a
+    // workgroup's time at c4's 4 tiles per workgroup)
+    const int npair = a.Cout * a.Cin;  // Lo * Li
+    for (int pr = threadIdx.x; pr < npair; pr += CT) {
+      const int lo = pr / a.Lc, li = pr - lo * a.Lc;  // layer (out, in) channel
+      // forward: product row o = lo, column c = li, tap j; input gradient: o = li, c = lo,
+      // tap K - 1 - j (transposed, time-flipped)
+      const int o = DG ? li : lo, c = DG ? lo : li;
+      const float* wp = a.w + (size_t)pr * K;
+      short* dst = Wl + o * ldw + c;
+      for (int j = 0; j < K; ++j) dst[(DG ? K - 1 - j : j) * CinP] = f2bf(wp[j]);
     }
   }
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
