@@ -356,7 +356,13 @@ int launch_conv(ConvArgs& a, int B, hipStream_t s) {
     mlvae_set_error("conv1d: LDS image %zu bytes > 160 KB", lds);
     return 1;
   }
-  int g = a.ntiles < 2 * device_cus() ? a.ntiles : 2 * device_cus();
+  // persistent workgroups per CU (each stages the weights once): MLVAE_CONV_MULT (A/B; default 2)
+  static const int mult = [] {
+    const char* e = getenv("MLVAE_CONV_MULT");
+    const int m = e ? atoi(e) : 2;
+    return m < 1 ? 1 : (m > 4 ? 4 : m);
+  }();
+  int g = a.ntiles < mult * device_cus() ? a.ntiles : mult * device_cus();
   switch (a.Cout / 16) {
 #define CASE(n) case n: return launch_lds(conv_kernel<n, DG>, g, lds, s, a);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)

@@ -1059,11 +1059,13 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   }
   if (K == 0) { s = 1; kc = TBK; }
   g.splits = s; g.kchunk = kc;
-  // tile order: groups of 4 M-panels walked column-major (projection at c2: 189 -> 173 us);
+  // tile order: groups of 8 M-panels walked column-major (projection at c2: plain row-major
+  // runs 189 -> 173 us with groups of 4; groups of 8 at c3, same box, alternating: projection
+  // 1.098 -> 1.069 ms per launch, profiles/ab/r04_gemm_group.txt);
   // MLVAE_GEMM_GROUP_M overrides (0/1 = plain row-major runs)
   static const int group_m = [] {
     const char* e = getenv("MLVAE_GEMM_GROUP_M");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 8;
   }();
   g.group_m = group_m;
   g.c16 = c16;
@@ -1247,7 +1249,7 @@ extern "C" int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, co
   if (g.K == 0) g.kchunk = TBK;
   static const int group_m = [] {
     const char* e = getenv("MLVAE_GEMM_GROUP_M");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 8;
   }();
   g.group_m = group_m;
   g.c16 = c16;
