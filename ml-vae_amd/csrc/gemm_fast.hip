@@ -50,7 +50,8 @@ struct GFArgs {
   const float* alpha; // device scalar multiplying A.B (fp8 operand scales), or null
   int stagger;        // VAR 14: realtime ticks per start phase for workgroups with fewer tiles (0: off)
   int abl;            // ablation bits (MLVAE_GEMM_ABL, timing only): 1 no MFMA, 2 no staging loads (VAR 6),
-                      // 4 the direct (unstaged) epilogue, 8 no epilogue; VAR 14: 16 start-phase
+                      // 4 the direct (unstaged) epilogue, 8 no epilogue, 64 4-column 16-bit C stores;
+                      // VAR 14: 16 start-phase
                       // stagger of (abl >> 8) & 255 realtime ticks per phase
   float* ws;
 };
@@ -62,26 +63,63 @@ constexpr int EPI_OUT_BF16 = 32; // flag bit of the ABI's epi: C is bf16 (staged
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(3))) bf16x4* lds_b4_t;
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// The raw words of make_rsrc()'s buffer descriptor (stride 0, flags 0x00020000) for inline asm.
+__device__ __forceinline__ i32x4 rsrc_words(const void* base, unsigned bytes) {
+  const unsigned long long b = (unsigned long long)(uintptr_t)base;
+  return i32x4{(int)(unsigned)b, (int)((unsigned)(b >> 32) & 0xffffu), (int)bytes, 0x00020000};
+}
+
+// One 16-byte-per-lane LDS-DMA piece.  ADMA: issued from inline asm.  The compiler tracks a
+// buffer_load ... lds builtin as a pending LDS write and, before any ds_read_b64_tr_b16 /
+// ds_read_b64_tr_b8 builtin (whose aliasing it cannot resolve), inserts s_waitcnt vmcnt(0): the
+// K-step it has just staged then lands before the current one's fragments are read, and the
+// m/n-contiguous loops lost all load/compute overlap.  Issued from asm the DMA is invisible to it;
+// the kernels' own counted vmcnt waits and barriers order every LDS access (as in the
+// k-contiguous loops, where the compiler never inserted such waits).  m0 is set in the same
+// statement (and is the only thing these kernels use m0 for).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+template <bool ADMA>
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, i32x4 rw, short* dst, unsigned off) {
+  if constexpr (ADMA) {
+    const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr_t)dst);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                 :: "v"(off), "s"(rw), "s"(la) : "memory", "m0");
+  } else {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, 0);
+  }
+}
+#pragma clang diagnostic pop
+
 __device__ __forceinline__ unsigned mc_swz(int r) { return 2u * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
-// Time-shifted K rows (the recurrent dW_hh: row k reads k + sh when 0 <= k % T + sh < T): time
-// index of row k0 + kr, kr < span.  k0 % T is wave-uniform (one scalar division per stage); a
-// lane then needs one conditional subtract when T >= span (wgrad hh: 1.6x faster staging than a
-// per-lane modulo)
-__device__ __forceinline__ bool shift_ok(int k0, int kr, int shT, int sh, int span) {
-  int t = k0 % shT + kr;
-  if (shT >= span) t = t >= shT ? t - shT : t;
-  else t %= shT;
-  t += sh;
-  return t >= 0 && t < shT;
+// Time-shifted K rows (the recurrent dW_hh: row k reads k + sh when 0 <= k % T + sh < T).
+// Byte offset of the 16-byte chunk of an m/n-contiguous operand at k-row k0 + kr, column gr, or OOB.
+// 32-bit arithmetic (the host bounds every operand below 2 GB): the lane part is loop-invariant and
+// the K-step adds one wave-uniform term.  tk = k0 % T is wave-uniform (one scalar division per
+// stage); a lane then needs one unsigned-min wrap when T >= span (wgrad hh: 1.6x faster staging
+// than a per-lane modulo).
+__device__ __forceinline__ unsigned mc_off(int kr, int gr, int ld, int R, int k0, int kend, int shT, int sh, int tk,
+                                           int span) {
+  bool ok = k0 + kr < kend && gr < R;
+  const unsigned e = (unsigned)(k0 + sh) * (unsigned)ld + (unsigned)(kr * ld + gr);
+  if (sh != 0) {
+    int t = tk + kr;
+    t = shT >= span ? (int)min((unsigned)t, (unsigned)(t - shT)) : t % shT;
+    ok = ok && (unsigned)(t + sh) < (unsigned)shT;
+  }
+  return ok ? e * 2u : OOB;
 }
 
 // Issue this wave's 4 LDS-DMA pieces (1 KB each) of one 256 x 64 operand tile.
 //   KC: element (row, k) at p[row * ld + k];   MC: element (row, k) at p[k * ld + row]
 // rows [r0, r0 + 256) bounded by R; k [k0, k0 + 64) bounded by kend (and by the time shift).
-template <bool KC>
-__device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
+template <bool KC, bool ADMA = false>
+__device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, i32x4 rw, int ld, int r0, int R,
                                       int k0, int kend, int shT, int sh, int wave, int lane) {
+  const int tk = (!KC && sh != 0) ? k0 % shT : 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int piece = wave * 4 + j;
@@ -93,16 +131,9 @@ __device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, int
       off = (gr < R && gk < kend) ? (unsigned)(((size_t)gr * ld + gk) * 2) : OOB;
     } else {
       const int kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr);
-      int gk = k0 + kr;
-      const int gr = r0 + 8 * c;
-      bool ok = gk < kend && gr < R;
-      if (sh != 0) {
-        ok = ok && shift_ok(k0, kr, shT, sh, TBK);
-        gk += sh;
-      }
-      off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
+      off = mc_off(kr, r0 + 8 * c, ld, R, k0, kend, shT, sh, tk, TBK);
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+    dma16<ADMA>(rs, rw, img + piece * 512, off);
   }
 }
 
@@ -133,9 +164,10 @@ constexpr int DIMG = TBM * DBK;  // elements per operand image (16 KB)
 __device__ __forceinline__ int kc_swz(int row) { return ((row >> 2) & 1) << 1; }  // 32-k rows
 
 // NP pieces (1 KB each) per wave: 2 with all 8 waves staging, 4 with one 4-wave group
-template <bool KC, int NP = 2>
-__device__ __forceinline__ void stage32(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R,
+template <bool KC, int NP = 2, bool ADMA = false>
+__device__ __forceinline__ void stage32(short* img, __amdgpu_buffer_rsrc_t rs, i32x4 rw, int ld, int r0, int R,
                                         int k0, int kend, int shT, int sh, int wave, int lane) {
+  const int tk = (!KC && sh != 0) ? k0 % shT : 0;
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     const int piece = wave * NP + j;
@@ -147,16 +179,9 @@ __device__ __forceinline__ void stage32(short* img, __amdgpu_buffer_rsrc_t rs, i
       off = (gr < R && gk < kend) ? (unsigned)(((size_t)gr * ld + gk) * 2) : OOB;
     } else {             // [32 k][256 rows]: 32 chunks per k-row, as the 64-deep image
       const int kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr);
-      int gk = k0 + kr;
-      const int gr = r0 + 8 * c;
-      bool ok = gk < kend && gr < R;
-      if (sh != 0) {
-        ok = ok && shift_ok(k0, kr, shT, sh, DBK);
-        gk += sh;
-      }
-      off = ok ? (unsigned)(((size_t)gk * ld + gr) * 2) : OOB;
+      off = mc_off(kr, r0 + 8 * c, ld, R, k0, kend, shT, sh, tk, DBK);
     }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+    dma16<ADMA>(rs, rw, img + piece * 512, off);
   }
 }
 
@@ -207,7 +232,7 @@ __device__ __forceinline__ int swz8(int kr) { return (kr & 7) | (((kr >> 5) & 1)
 
 // this wave's 4 LDS-DMA pieces (1 KB each) of one [128 k][256 m] fp8 image; element (m, k) at byte
 // p[k * ld + m]; rows [r0, r0 + 256) bounded by R (R % 16 == 0), k [k0, k0 + 128) by kend
-__device__ __forceinline__ void stage8_mc(short* img, __amdgpu_buffer_rsrc_t rs, int ld, int r0, int R, int k0,
+__device__ __forceinline__ void stage8_mc(short* img, __amdgpu_buffer_rsrc_t rs, i32x4 rw, int ld, int r0, int R, int k0,
                                           int kend, int wave, int lane) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -215,8 +240,8 @@ __device__ __forceinline__ void stage8_mc(short* img, __amdgpu_buffer_rsrc_t rs,
     const int p = piece * 64 + lane;
     const int kr = p >> 4, c = (p & 15) ^ swz8(kr);
     const int gk = k0 + kr, gm = r0 + 16 * c;
-    const unsigned off = (gk < kend && gm < R) ? (unsigned)((size_t)gk * ld + gm) : OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(img + piece * 512), 16, off, 0, 0, 0);
+    const unsigned off = (gk < kend && gm < R) ? (unsigned)gk * (unsigned)ld + (unsigned)gm : OOB;
+    dma16<true>(rs, rw, img + piece * 512, off);
   }
 }
 
@@ -278,6 +303,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   const int sh = g.kshift + bz * g.kshift_bstep;
   const auto ra = make_rsrc(Ap, OOB);
   const auto rb = make_rsrc(Bp, OOB);
+  const i32x4 rwa = rsrc_words(Ap, OOB), rwb = rsrc_words(Bp, OOB);
+  constexpr bool ADMA = !(AKC && BKC);  // a transposed-read operand: LDS-DMA from asm (dma16)
   const int kbeg = kz * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   constexpr int SBK = VAR == 12 ? DBK : (VAR == 9 ? 128 : TBK);  // K per main-loop step
@@ -293,8 +320,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     // VAR 4: both k-halves' fragments (24 ds_reads) issued right after the barrier, so the
     // second half's MFMAs never wait on an LDS round trip in mid-step
     auto stage_both = [&](int buf, int k0) {
-      stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
-      stage<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+      stage<AKC, ADMA>(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+      stage<BKC, ADMA>(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
     };
     if (nk > 0) {
       stage_both(0, kbeg);
@@ -344,12 +371,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     // both groups retired (lgkmcnt(0)) before their barriers of the previous slots.
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const int grpw = wv >> 2, w4 = wv & 3;
+    // operands of one layout: each group's staging parameters selected once (one code path and
+    // one scalar set in the loop; two had spilled SGPRs into the m/n-contiguous loop)
+    const auto rs1 = grpw ? rb : ra;
+    const i32x4 rw1 = grpw ? rwb : rwa;
+    const int ld1 = grpw ? g.ldb : g.lda, r01 = grpw ? n0 : m0, R1 = grpw ? g.N : g.M;
+    const int shT1 = grpw ? g.kshiftT : 0, sh1 = grpw ? sh : 0;
     auto share = [&](int it) {
       const int buf = it & (DNB - 1), k0 = kbeg + it * DBK;
-      if (grpw == 0)
-        stage32<AKC, 4>(lds + (buf * 2 + 0) * DIMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, w4, lane);
+      if constexpr (AKC == BKC)
+        stage32<AKC, 4, ADMA>(lds + (buf * 2 + grpw) * DIMG, rs1, rw1, ld1, r01, R1, k0, kend, shT1, sh1, w4, lane);
+      else if (grpw == 0)
+        stage32<AKC, 4, ADMA>(lds + (buf * 2 + 0) * DIMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, w4, lane);
       else
-        stage32<BKC, 4>(lds + (buf * 2 + 1) * DIMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, w4, lane);
+        stage32<BKC, 4, ADMA>(lds + (buf * 2 + 1) * DIMG, rb, rwb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, w4, lane);
     };
     auto wait_younger = [&](int n) {  // this wave's shares: all but the n youngest landed
       if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -391,8 +426,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   } else if constexpr (VAR == 9) {
     static_assert(!AKC && !BKC, "VAR 9: fp8 operands stored m/n-contiguous");
     auto stage_both = [&](int buf, int k0) {
-      stage8_mc(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, wave, lane);
-      stage8_mc(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, wave, lane);
+      stage8_mc(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, wave, lane);
+      stage8_mc(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, wave, lane);
     };
     if (nk > 0) {
       stage_both(0, kbeg);
@@ -421,8 +456,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   } else if constexpr (VAR == 8) {
     static_assert(AKC && BKC, "fp8 operands are k-contiguous");
     auto stage_both = [&](int buf, int k0) {
-      stage<true>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
-      stage<true>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, 0, 0, wave, lane);
+      stage<true>(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+      stage<true>(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, 0, 0, wave, lane);
     };
     if (nk > 0) {
       stage_both(0, kbeg);
@@ -452,8 +487,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     }
   } else {
   auto stage_both = [&](int buf, int k0) {
-    stage<AKC>(lds + (buf * 2 + 0) * IMG, ra, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
-    stage<BKC>(lds + (buf * 2 + 1) * IMG, rb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+    stage<AKC, ADMA>(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+    stage<BKC, ADMA>(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
   };
   if (nk > 0) {
     stage_both(0, kbeg);
@@ -521,8 +556,24 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     // the bias columns of this thread, loaded before the first store: a load issued behind the
     // stores would wait for them (vmcnt counts in issue order)
     const int c4 = tid & 63, col = n0 + 4 * c4;
-    f32x4 b = {0.f, 0.f, 0.f, 0.f};
-    if (!split && col < g.N) {
+    // 16-bit C: a lane stores 8 columns (16 B) -- half the store instructions of 4-column lanes
+    // (the tile's store burst is issue-bound: cdna_hip_programming.md T21)
+    const bool w8 = !split && g.c16 && (g.N % 8) == 0 && (g.ldc % 8) == 0 && ((uintptr_t)Cb % 16) == 0 &&
+                    !(g.abl & 64);
+    const int c8 = tid & 31, col8 = n0 + 8 * c8;
+    f32x4 b = {0.f, 0.f, 0.f, 0.f}, b2 = {0.f, 0.f, 0.f, 0.f};
+    if (w8) {
+      if (col8 < g.N) {
+        if (g.bias1) {
+          b += *reinterpret_cast<const f32x4*>(g.bias1 + col8);
+          b2 += *reinterpret_cast<const f32x4*>(g.bias1 + col8 + 4);
+        }
+        if (g.bias2) {
+          b += *reinterpret_cast<const f32x4*>(g.bias2 + col8);
+          b2 += *reinterpret_cast<const f32x4*>(g.bias2 + col8 + 4);
+        }
+      }
+    } else if (!split && col < g.N) {
       if (g.bias1) b += *reinterpret_cast<const f32x4*>(g.bias1 + col);
       if (g.bias2) b += *reinterpret_cast<const f32x4*>(g.bias2 + col);
     }
@@ -537,6 +588,46 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
               acc[2 * pass + ii][j];
         }
       lds_barrier();
+      if (w8) {
+#pragma unroll 2
+        for (int q = 0; q < 4; ++q) {
+          const int lr = q * 16 + (tid >> 5);  // 16 staged rows per round, 32 lanes per row
+          const int row = m0 + (lr >> 5) * 128 + (2 * pass + ((lr >> 4) & 1)) * 16 + (lr & 15);
+          if (row >= g.M || col8 >= g.N) continue;
+          f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * LSR + 8 * c8) + b;
+          f32x4 v2 = *reinterpret_cast<const f32x4*>(st + lr * LSR + 8 * c8 + 4) + b2;
+          if (g.epi == EPI_DROPOUT) {
+            const unsigned long long rq = drop_quad(dkey, (g.doff + (size_t)row * g.ldc + col8) >> 2);
+            const unsigned long long rq2 = drop_quad(dkey, ((g.doff + (size_t)row * g.ldc + col8) >> 2) + 1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] *= drop_elem_scale(rq, r, g.dkeep, g.dscale);
+              v2[r] *= drop_elem_scale(rq2, r, g.dkeep, g.dscale);
+            }
+          }
+          if (g.epi == EPI_LRELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] = lrelu(v[r]);
+              v2[r] = lrelu(v2[r]);
+            }
+          }
+          u32x2 lo, hi;
+          if (g.c16 == 2) {
+            lo = u32x2{(unsigned)(unsigned short)f2bf(v[0]) | ((unsigned)(unsigned short)f2bf(v[1]) << 16),
+                       (unsigned)(unsigned short)f2bf(v[2]) | ((unsigned)(unsigned short)f2bf(v[3]) << 16)};
+            hi = u32x2{(unsigned)(unsigned short)f2bf(v2[0]) | ((unsigned)(unsigned short)f2bf(v2[1]) << 16),
+                       (unsigned)(unsigned short)f2bf(v2[2]) | ((unsigned)(unsigned short)f2bf(v2[3]) << 16)};
+          } else {
+            lo = f2h4(v);
+            hi = f2h4(v2);
+          }
+          *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned short*>(Cb) + (size_t)row * g.ldc + col8) =
+              u32x4{lo[0], lo[1], hi[0], hi[1]};
+        }
+        lds_barrier();
+        continue;
+      }
 #pragma unroll 2  // (fully unrolled, the four passes outgrew the unroller: acc went to scratch)
       for (int q = 0; q < 8; ++q) {
         const int lr = q * 8 + (tid >> 6);  // wave w stores staged rows w, w + 8, ...
@@ -697,9 +788,9 @@ __global__ __launch_bounds__(512) void gemm256_persist_kernel(GFArgs g) {
   auto share_next = [&]() {
     const int buf = sh_gs & (DNB - 1), k0 = sh_ks * DBK;
     if (grpw == 0)
-      stage32<AKC, 4>(lds + (buf * 2 + 0) * DIMG, ra, g.lda, sh_m0, g.M, k0, g.K, 0, 0, w4, lane);
+      stage32<AKC, 4>(lds + (buf * 2 + 0) * DIMG, ra, i32x4{}, g.lda, sh_m0, g.M, k0, g.K, 0, 0, w4, lane);
     else
-      stage32<BKC, 4>(lds + (buf * 2 + 1) * DIMG, rb, g.ldb, sh_n0, g.N, k0, g.K, 0, 0, w4, lane);
+      stage32<BKC, 4>(lds + (buf * 2 + 1) * DIMG, rb, i32x4{}, g.ldb, sh_n0, g.N, k0, g.K, 0, 0, w4, lane);
     ++sh_gs;
     if (++sh_ks == nk) {
       sh_ks = 0;
