@@ -84,7 +84,9 @@ __device__ __forceinline__ i32x4 rsrc_words(const void* base, unsigned bytes) {
 template <bool ADMA>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, i32x4 rw, short* dst, unsigned off) {
   if constexpr (ADMA) {
-    const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_ptr_t)dst);
+    // the low 32 bits of a generic pointer into LDS are its LDS address (the aperture is the high
+    // half): no addrspacecast, whose null check cost three scalar instructions per piece
+    const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                  :: "v"(off), "s"(rw), "s"(la) : "memory", "m0");
   } else {
@@ -112,6 +114,53 @@ __device__ __forceinline__ unsigned mc_off(int kr, int gr, int ld, int R, int k0
   }
   return ok ? e * 2u : OOB;
 }
+
+// m/n-contiguous staging with the lane-invariant part computed once per tile: per piece and K-step
+// a lane then spends a compare, an add and a select (plus the wrap test for time-shifted rows)
+// instead of re-deriving its column, swizzle and bounds -- the ping-pong loop's fragment-read slot
+// has ~512 MFMA cycles of the other group to hide the staging in.  Pieces pb .. pb + NP - 1 of a
+// [span k][256 cols] image (piece = 2 k-rows of 512 B).
+template <int NP>
+struct McLanes {
+  unsigned off2[NP];  // 2 (kr ld + gr), or OOB for a column >= R
+  int kr0;            // this lane's k-row in piece pb (piece pb + j: kr0 + 2 j)
+  __device__ __forceinline__ void init(int pb, int lane, int ld, int r0, int R) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int p = (pb + j) * 64 + lane, kr = p >> 5, c = (p & 31) ^ (int)mc_swz(kr), gr = r0 + 8 * c;
+      off2[j] = gr < R ? 2u * (unsigned)(kr * ld + gr) : OOB;
+    }
+    kr0 = (pb * 64 + lane) >> 5;
+  }
+  // SH: 0 no time shift; 1 rows read k + sh inside each length-shT sequence with shT >= the image
+  // depth (one unsigned-min wrap); 2 any shT (per-lane modulo)
+  template <int SH, bool ADMA>
+  __device__ __forceinline__ void stage(short* img, __amdgpu_buffer_rsrc_t rs, i32x4 rw, int ld, int k0, int kend,
+                                        int shT, int sh, int pb) const {
+    const unsigned base = 2u * (unsigned)(k0 + sh) * (unsigned)ld;  // wraps for k0 + sh < 0: those rows fail
+    const int lim = kend - k0;
+    const int tk = SH ? k0 % shT : 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int kr = kr0 + 2 * j;
+      bool ok = kr < lim && off2[j] < OOB;
+      if constexpr (SH == 1) {
+        const int t = tk + kr;
+        ok = ok && (unsigned)((int)min((unsigned)t, (unsigned)(t - shT)) + sh) < (unsigned)shT;
+      } else if constexpr (SH == 2) {
+        ok = ok && (unsigned)((tk + kr) % shT + sh) < (unsigned)shT;
+      }
+      dma16<ADMA>(rs, rw, img + (pb + j) * 512, ok ? off2[j] + base : OOB);
+    }
+  }
+  template <bool ADMA>
+  __device__ __forceinline__ void stage_any(short* img, __amdgpu_buffer_rsrc_t rs, i32x4 rw, int ld, int k0, int kend,
+                                            int shT, int sh, int pb, int span) const {
+    if (sh == 0) stage<0, ADMA>(img, rs, rw, ld, k0, kend, shT, 0, pb);
+    else if (shT >= span) stage<1, ADMA>(img, rs, rw, ld, k0, kend, shT, sh, pb);
+    else stage<2, ADMA>(img, rs, rw, ld, k0, kend, shT, sh, pb);
+  }
+};
 
 // Issue this wave's 4 LDS-DMA pieces (1 KB each) of one 256 x 64 operand tile.
 //   KC: element (row, k) at p[row * ld + k];   MC: element (row, k) at p[k * ld + row]
@@ -377,9 +426,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     const i32x4 rw1 = grpw ? rwb : rwa;
     const int ld1 = grpw ? g.ldb : g.lda, r01 = grpw ? n0 : m0, R1 = grpw ? g.N : g.M;
     const int shT1 = grpw ? g.kshiftT : 0, sh1 = grpw ? sh : 0;
+    McLanes<4> ml1;
+    if constexpr (!AKC && !BKC) ml1.init(w4 * 4, lane, ld1, r01, R1);
     auto share = [&](int it) {
       const int buf = it & (DNB - 1), k0 = kbeg + it * DBK;
-      if constexpr (AKC == BKC)
+      if constexpr (!AKC && !BKC)
+        ml1.stage_any<ADMA>(lds + (buf * 2 + grpw) * DIMG, rs1, rw1, ld1, k0, kend, shT1, sh1, w4 * 4, DBK);
+      else if constexpr (AKC == BKC)
         stage32<AKC, 4, ADMA>(lds + (buf * 2 + grpw) * DIMG, rs1, rw1, ld1, r01, R1, k0, kend, shT1, sh1, w4, lane);
       else if (grpw == 0)
         stage32<AKC, 4, ADMA>(lds + (buf * 2 + 0) * DIMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, w4, lane);
@@ -486,9 +539,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       __syncthreads();
     }
   } else {
+  McLanes<4> mla, mlb;
+  const int pbw = __builtin_amdgcn_readfirstlane(wave) * 4;  // this wave's first piece (wave-uniform)
+  if constexpr (!AKC) mla.init(pbw, lane, g.lda, m0, g.M);
+  if constexpr (!BKC) mlb.init(pbw, lane, g.ldb, n0, g.N);
   auto stage_both = [&](int buf, int k0) {
-    stage<AKC, ADMA>(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
-    stage<BKC, ADMA>(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+    if constexpr (AKC)
+      stage<AKC, ADMA>(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+    else
+      mla.stage<0, ADMA>(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, k0, kend, 0, 0, pbw);
+    if constexpr (BKC)
+      stage<BKC, ADMA>(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
+    else
+      mlb.stage_any<ADMA>(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, k0, kend, g.kshiftT, sh, pbw, TBK);
   };
   if (nk > 0) {
     stage_both(0, kbeg);
