@@ -180,6 +180,18 @@ int mlvae_lstm_fwd_fp8r(int B, int T, int H, const float* w_hh_fwd, const float*
                         float* cells, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
                         unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
                         void* xbuf, size_t xbytes, int* err, void* stream);
+/* Wide forward of the bottom layer with its input projection fused (replaces the skinny
+ * projection + mlvae_lstm_fwd_ex2 pair for ref:src/modules/decoder.py:22, nn.LSTM layer 0 whose
+ * input is the 32-wide latent z): each step's gate inputs z_t W_ih^T + b_ih + b_hh are computed
+ * inside the recurrence from z (bf16 [B*T rows, ldz], Z = 32), so the 8H-wide projection is
+ * never written or read; gates receives the activated gates (fp16) as from mlvae_lstm_fwd_ex2.
+ * y (fp32 h), y_drop_bf16 and y_drop_fp8 (with x8_scale > 0) are optional. */
+int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, const void* z_bf16,
+                     int ldz, int Z, const float* w_ih_fwd, const float* w_ih_rev, const float* b_ih_fwd,
+                     const float* b_hh_fwd, const float* b_ih_rev, const float* b_hh_rev, void* gates,
+                     float* cells, float* y, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
+                     unsigned long long drop_seed, unsigned long long drop_offset, float drop_p, void* xbuf,
+                     size_t xbytes, int* err, void* stream);
 int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
                        const float* cells, const float* dy, void* dg_bf16, float* dbias_rows,
                        void* dg_fp8, const float* dg8_scale, unsigned* dg_amax, void* xbuf,

@@ -1056,6 +1056,7 @@ struct WideExtra {  // outputs only the wide kernels write
   float p = 0.f;
   WideFp8 f8;                     // fp8 mode: e4m3 dropout(h) / dG copies, dG amax
   const unsigned short* dyb = nullptr;  // backward: dY as bf16 (Y unused)
+  WideZ wz;                             // forward: fused layer-0 input projection
 };
 
 int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W1, float* G,
@@ -1077,7 +1078,7 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     if (!fwd && !dgb) { mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 (NULL)"); return 1; }
     if (ex.ydb && !(ex.p >= 0.f && ex.p < 1.f)) { mlvae_set_error("lstm: dropout p=%g", ex.p); return 1; }
     return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.dbias, ex.ydb,
-                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode, ex.f8, ex.dyb);
+                         ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode, ex.f8, ex.dyb, ex.wz);
   }
   if (ex.dyb) { mlvae_set_error("lstm: bf16 dY only on the wide-batch path (fp16 gates)"); return 1; }
   if (ex.ydb || ex.dbias || !Y) {
@@ -1206,6 +1207,33 @@ extern "C" int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, co
   ex.f8.x8scale = x8_scale;
   return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, nullptr,
              xbuf, xbytes, err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
+}
+// Wide forward of layer 0 with its input projection fused: G = z W_ih^T + b_ih + b_hh is never
+// written -- each step's gate inputs come from the 32-wide bf16 layer input z [B*T rows, ldz]
+// inside the recurrence (one MFMA per tile); gates receives the activated gates as from
+// mlvae_lstm_fwd_ex2.  y (fp32 h), y_drop_bf16 and y_drop_fp8 (with x8_scale) are optional.
+extern "C" int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                const void* z_bf16, int ldz, int Z, const float* w_ih_fwd,
+                                const float* w_ih_rev, const float* b_ih_fwd, const float* b_hh_fwd,
+                                const float* b_ih_rev, const float* b_hh_rev, void* gates, float* cells,
+                                float* y, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
+                                unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                                void* xbuf, size_t xbytes, int* err, void* stream) {
+  if (Z != 32 || !z_bf16 || !use_wide(B, H, PREC_BF16) || (y_drop_fp8 && (!y_drop_bf16 || !(x8_scale > 0.f)))) {
+    mlvae_set_error("lstm_fwd_z: Z = 32 on wide-batch shapes; an e4m3 dropout output needs the bf16 one and a scale");
+    return 1;
+  }
+  WideExtra ex;
+  ex.ydb = static_cast<unsigned short*>(y_drop_bf16);
+  ex.seed = drop_seed; ex.off = drop_offset; ex.p = drop_p;
+  ex.f8.y8 = static_cast<unsigned char*>(y_drop_fp8);
+  ex.f8.x8scale = x8_scale;
+  ex.wz.zb = static_cast<const unsigned short*>(z_bf16);
+  ex.wz.ldz = ldz;
+  ex.wz.w0 = w_ih_fwd; ex.wz.w1 = w_ih_rev;
+  ex.wz.b[0] = b_ih_fwd; ex.wz.b[1] = b_hh_fwd; ex.wz.b[2] = b_ih_rev; ex.wz.b[3] = b_hh_rev;
+  return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, y, xbuf, xbytes,
+             err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
 }
 // fp8 mode forward with the recurrent product on e4m3 operands (F8R: where the wide kernels run
 // the asymmetric TPW-1 form -- per-GPU batches <= 128 -- elsewhere as mlvae_lstm_fwd_fp8's

@@ -50,6 +50,14 @@ struct LstmArgs {
   unsigned* g8amax;
   const unsigned short* dYb;  // wide BPTT, optional: dY as bf16 [B*T, 2H] instead of Y (fp32)
   int rec8;                   // fp8 mode, wide forward at TPW 1: h W_hh on e4m3 operands (F8R)
+  // wide forward, optional (ZP): the layer input z (bf16 [B*T rows, ldz], 32 wide) whose
+  // projection z W_ih^T + b_ih + b_hh the kernel computes itself -- G then only receives the
+  // activated gates (no 8H-wide fp16 projection written and read back)
+  const unsigned short* Zb;
+  int ldz;
+  const float* Wz0;           // W_ih forward / reverse [4H, 32]
+  const float* Wz1;
+  const float* bz[4];         // b_ih, b_hh forward; b_ih, b_hh reverse [4H]
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -205,12 +213,19 @@ struct WideFp8 {  // the fp8 mode's fused outputs of the wide kernels (LstmArgs 
   unsigned* g8amax = nullptr;
   int rec8 = 0;  // forward: h W_hh on e4m3 operands (F8R)
 };
+struct WideZ {  // the wide forward's fused layer-0 input projection (LstmArgs Zb ... bz)
+  const unsigned short* zb = nullptr;
+  int ldz = 0;
+  const float* w0 = nullptr;
+  const float* w1 = nullptr;
+  const float* b[4] = {nullptr, nullptr, nullptr, nullptr};
+};
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
                   unsigned long long* dbg, int dbg_mode, const WideFp8& f8 = WideFp8(),
-                  const unsigned short* dyb = nullptr);
+                  const unsigned short* dyb = nullptr, const WideZ& wz = WideZ());
 // debug-mode bits the wide plans read (bit 21: one workgroup per CU, no two-per-CU plan)
 void lstm_wide_set_mode(int mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply

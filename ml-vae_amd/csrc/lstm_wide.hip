@@ -79,7 +79,11 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // registers as e4m3 with one E8M0 scale per lane's 32-element k-block (half the VGPRs of bf16),
 // h converted to e4m3 at 2^8 (|h| < 1) as the pollers write it into the LDS image; a quarter of
 // the MFMAs at twice the cycles each.  The exchange stays bf16.
-template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool F8R = false>  // HJ = 32 * TPW, H = 32 * NKC
+// ZP: the layer-0 input projection fused (a.Zb): io wave 4 DMAs the step's 16 z rows (64 B each)
+// into the gx ring's space and each tile's gate inputs are one v_mfma_f32_16x16x32_bf16 of the
+// resident W_ih fragment (K = 32 = the latent width) onto the tile's b_ih + b_hh -- instead of
+// reading 8 KB of fp16 projection per utterance and step that a separate kernel wrote.
+template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool F8R = false, bool ZP = false>
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -178,9 +182,20 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   auto rowof = [&](int b_, int t_) -> size_t { return tmaj ? (size_t)t_ * a.B + b_ : (size_t)b_ * T + t_; };
   // (the probe's absolute descriptor: range-checked to the gate buffer, at most 4 GB)
   const auto rgx_abs = make_rsrc(G16, (unsigned)min((size_t)a.B * T * 8 * H * 2, (size_t)0xffffffffu));
+  // ZP: z rows [16 utt][32] bf16 per ring slot, lane-linear (lane 4 u + c: 16 B chunk c of utt u)
+  unsigned short* zr = gxr;
+  const auto rz = make_rsrc(a.Zb, (unsigned)min((size_t)a.B * T * a.ldz * 2, (size_t)0x7fffffff));
   auto io_load = [&](int s_) {  // input projection of step s_ into gx ring slot s_ & 1
     if (s_ >= T || (s_ > 0 && (a.dbg_mode & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
+    if constexpr (ZP) {
+      if (wave == 4) {
+        const int u = lane >> 2, b = grp * BG + u;
+        const unsigned off = b < a.B ? (unsigned)((((size_t)b * T + t_) * a.ldz + 8 * (lane & 3)) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_ptr_t)(zr + (s_ & 1) * 16 * 32), 16, off, 0, 0, NT_AUX);
+      }
+      return;
+    }
     constexpr int UPW = 16 / 4;  // utterances per io wave
     // one descriptor over the group's 16 utterances (per-utterance descriptors spilled SGPRs
     // into the io waves' MFMA phase); the host keeps 16 T 8H halfs under 4 GB
@@ -309,6 +324,26 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     } else {
       load_w(wreg, m0, MT);
     }
+    // ZP: the tiles' W_ih fragments (row bi: gate bi & 3, unit 4 m + (bi >> 2); k = 8 q .. 8 q + 7)
+    // and b_ih + b_hh in the accumulator layout (element g: gate g of unit 4 m + q)
+    bf16x8 wz[ZP ? MTA : 1];
+    f32x4 bz4[ZP ? MTA : 1];
+    if constexpr (ZP) {
+      const float* Wz = dir ? a.Wz1 : a.Wz0;
+      const float* bih = a.bz[2 * dir];
+      const float* bhh = a.bz[2 * dir + 1];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = m0 + t;
+        const float* wrow = Wz + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * 32 + 8 * q;
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(wrow);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(wrow + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { wz[t][e] = f2bf(w0[e]); wz[t][4 + e] = f2bf(w1[e]); }
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) bz4[t][g4] = bih[g4 * H + j0 + 4 * m + q] + bhh[g4 * H + j0 + 4 * m + q];
+      }
+    }
     // AS with tile-less io waves: their DMA and stores right behind the barrier
     constexpr bool PURE_IO = IO && MT == 0;
     if (IO) {
@@ -332,6 +367,18 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       // latency is not exposed between the last MFMA and the cell update
       float gxv[MTA][4];
       auto read_gx = [&]() {
+        if constexpr (ZP) {
+          if constexpr (MT > 0) {
+            const bf16x8 zf = *reinterpret_cast<const bf16x8*>(zr + (s & 1) * 16 * 32 + bi * 32 + 8 * q);
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+              const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wz[t], zf, bz4[t], 0, 0, 0);
+#pragma unroll
+              for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = r[g4];
+            }
+          }
+          return;
+        }
         const unsigned short* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -1392,8 +1439,11 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   const bool dbg = a.dbg != nullptr;
   const bool as = TPW == 1 && !(a.dbg_mode & (1 << 8));   // the asymmetric split; bit 8: equal shares
   const bool f8r = as && a.rec8 && !dbg;    // fp8 mode: e4m3 h W_hh (the asymmetric TPW-1 form only)
+  const bool zp = a.Zb != nullptr;          // fused layer-0 projection (checked: no DBG / F8R with it)
   auto k = fwd ? (dbg ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, true>)
                       : (f8r ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, TPW == 1>
+                             : zp ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, false, true>
+                                        : lstm_fwd_wide_kernel<TPW, NKC, OCC, false, false, false, true>)
                              : as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
@@ -1446,7 +1496,8 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,
                   unsigned short* yb, unsigned short* dgb, float* dbias, unsigned short* ydb,
                   unsigned long long dseed, unsigned long long doff, float dp,
-                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8, const unsigned short* dyb) {
+                  unsigned long long* dbg, int dbg_mode, const WideFp8& f8, const unsigned short* dyb,
+                  const WideZ& wz) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return -1;
   // the kernels address a batch group's rows through one buffer descriptor (32-bit offsets)
@@ -1468,6 +1519,16 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.Y8 = f8.y8; a.x8scale = f8.x8scale; a.dG8 = f8.dg8; a.g8scale = f8.g8scale; a.g8amax = f8.g8amax;
   a.rec8 = f8.rec8;
   a.dYb = fwd ? nullptr : dyb;
+  if (wz.zb) {
+    if (!fwd || p.il || dbg || f8.rec8 || !wz.w0 || !wz.w1 || !wz.b[0] || !wz.b[1] || !wz.b[2] || !wz.b[3] ||
+        wz.ldz < 32 || wz.ldz % 8 || ((uintptr_t)wz.zb % 16)) {
+      mlvae_set_error("lstm_wide: the fused z projection needs the plain forward (no stamps / fp8 recurrence), "
+                      "both W_ih and all four biases, a 16-byte aligned z with ldz >= 32, ldz %% 8 == 0");
+      return 1;
+    }
+    a.Zb = wz.zb; a.ldz = wz.ldz; a.Wz0 = wz.w0; a.Wz1 = wz.w1;
+    for (int i = 0; i < 4; ++i) a.bz[i] = wz.b[i];
+  }
   if (a.Y8 && (!ydb || p.il)) {
     mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one (one-group forward)");
     return 1;

@@ -407,6 +407,9 @@ class VAEEngine:
         self.split_tail = int(os.environ.get("MLVAE_SPLIT_TAIL", "160"))
         # layer-0 input projection (K = latent width) on skinny_proj instead of the 256² GEMM
         self.skinny_proj = os.environ.get("MLVAE_PROJ0", "skinny") == "skinny"
+        # ... or fused into the layer-0 forward recurrence (mlvae_lstm_fwd_z: the 8H-wide fp16
+        # projection is never written; MLVAE_ZPROJ=0: the skinny kernel + mlvae_lstm_fwd_ex2, A/B)
+        self.zproj = os.environ.get("MLVAE_ZPROJ", "1") != "0"
         # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
         self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
         self.side_stream = torch.cuda.Stream(self.device)
@@ -715,7 +718,12 @@ class VAEEngine:
         w.layer_in = []
         for li in range(cfg.L):
             w.layer_in.append((xin, xin_bf, din, ldx))
-            if w.bf and din <= 32 and din % 8 == 0 and self.skinny_proj:
+            # layer 0 on the 32-wide latent: the projection inside the recurrence (below)
+            zproj = bool(li == 0 and self.zproj and w.bf and w.g16 and din == 32 and ldx % 8 == 0 and
+                         xin_bf is not None and not (cfg.fp8 and self.fp8_rec))
+            if zproj:
+                pass
+            elif w.bf and din <= 32 and din % 8 == 0 and self.skinny_proj:
                 # K = latent width: the write-bound skinny projection kernel (skinny.hip)
                 check(l.mlvae_skinny_proj_ex(N, 8 * H, din, _pb(xin_bf), ldx,
                                              wb(f"decoder.rnn.weight_ih_l{li}"), din,
@@ -770,7 +778,19 @@ class VAEEngine:
             # (mlvae_lstm_fwd_fp8r; the wide kernels' per-GPU-batch <= 128 form)
             rec8 = bool(cfg.fp8 and w.g16 and not need_y and self.fp8_rec)
             with self._timed("lstm_fwd"):
-                if rec8:
+                if zproj:
+                    rp = lambda n: self._ptr(f"decoder.rnn.{n}")
+                    check(l.mlvae_lstm_fwd_z(B, T, H, rp("weight_hh_l0"), rp("weight_hh_l0_reverse"), _pb(xin_bf),
+                                             ldx, din, rp("weight_ih_l0"), rp("weight_ih_l0_reverse"),
+                                             rp("bias_ih_l0"), rp("bias_hh_l0"), rp("bias_ih_l0_reverse"),
+                                             rp("bias_hh_l0_reverse"), _p(w.G[li]), _p(w.Cs[li]),
+                                             _p(w.Y[li]) if need_y else None, _pb(w.Yb[li]),
+                                             _pb(w.Ydb[li]) if fuse_drop else None,
+                                             w.X8.data_ptr() if x8_fused else None,
+                                             x8_scale(cfg.dropout) if x8_fused else 0.0, seed, self._drop_off,
+                                             cfg.dropout if fuse_drop else 0.0, _p(w.xbuf), w.xbuf.numel(),
+                                             _p(self.err), s), "lstm_fwd_z")
+                elif rec8:
                     check(l.mlvae_lstm_fwd_fp8r(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                 self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
                                                 _p(w.Cs[li]), _pb(w.Yb[li]),
@@ -1186,12 +1206,14 @@ class VAEEngine:
                 check(l.mlvae_conv1d_wgrad(B, T, cin, E, K, _p(dy), E, xin, cin, gp(f"{ep}.{name}.weight"),
                                            gp(f"{ep}.{name}.bias"), _p(ws), ws.numel() * 4, self._stream()),
                       "conv1d_wgrad")
-            self._side(lambda: wgc(E, w.dE2, _p(w.E1), 2, w.conv_ws[1]))
+            # the whole Conv1d backward in the timed region: the layer-2 weight gradient on the side
+            # stream beside the input gradient, then the layer-1 weight gradient, joined
             with self._timed("conv_bwd"):
+                self._side(lambda: wgc(E, w.dE2, _p(w.E1), 2, w.conv_ws[1]))
                 check(l.mlvae_conv1d_dgrad(B, T, E, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1), E,
                                            _p(w.dE1), E, s), "conv1d_dgrad")
                 wgc(Fd, w.dE1, _p(w.x), 0, w.conv_ws[0])
-            self._join_side()
+                self._join_side()
             return
 
         def wge1():

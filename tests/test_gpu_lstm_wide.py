@@ -20,11 +20,12 @@ H = 512
 TOL_Y, TOL_DG = 3e-2, 1.5e-1
 
 
-def _reference(B, T, seed):
+def _reference(B, T, seed, gx=None):
     torch.manual_seed(seed)
     k = 1.0 / H ** 0.5
     w = [(torch.rand(4 * H, H, dtype=torch.float64) * 2 - 1) * k for _ in range(2)]
-    gx = torch.randn(B, T, 8 * H, dtype=torch.float64) * 0.5
+    if gx is None:
+        gx = torch.randn(B, T, 8 * H, dtype=torch.float64) * 0.5
     gxl = gx.clone().requires_grad_(True)
     outs, cs, gates = [], [], []
     for d, rev in ((0, False), (1, True)):
@@ -145,6 +146,70 @@ def test_fp8_recurrence_forward(B, T):
                                     P(xbuf), xb.value, P(err), stream()))
     torch.cuda.synchronize()
     assert err.item() == 0 and torch.equal(Yb1, Yb)
+
+
+# mode 4096: the wide kernels forced at a small batch; 256: TPW 1 with equal tile shares
+@pytest.mark.parametrize("B,T,ldz,mode", [(256, 16, 32, 0), (64, 20, 40, 0), (48, 9, 32, 4096), (64, 12, 32, 256)])
+def test_fused_z_projection_forward(B, T, ldz, mode):
+    """mlvae_lstm_fwd_z (layer 0 with its input projection z W_ih^T + b_ih + b_hh computed inside the
+    recurrence from the 32-wide bf16 latent) against the fp64 loop on the same projection: h, c, the
+    activated gates, bf16 h and the Philox dropout(h) exactly as mlvae_lstm_fwd_ex2 writes them."""
+    need_gpu()
+    N, Z = B * T, 32
+    g = torch.Generator().manual_seed(99 + B)
+    zf = torch.randn(N, Z, generator=g, dtype=torch.float64).to(torch.bfloat16)
+    wih = [((torch.rand(4 * H, Z, generator=g, dtype=torch.float64) * 2 - 1) * 0.4).float() for _ in range(2)]
+    bias = [((torch.rand(4 * H, generator=g, dtype=torch.float64) * 2 - 1) * 0.1).float() for _ in range(4)]
+    gx = torch.cat([zf.double() @ wih[d].to(torch.bfloat16).double().t() + bias[2 * d].double() +
+                    bias[2 * d + 1].double() for d in range(2)], 1).view(B, T, 8 * H)
+    w, _, y, cs, gates, _, _ = _reference(B, T, 3 * B + T, gx=gx)
+    zpad = torch.zeros(N, ldz, dtype=torch.bfloat16)
+    zpad[:, :Z] = zf
+    zb = zpad.cuda().contiguous()
+    G = torch.full((N, 8 * H), float("nan"), device="cuda").to(torch.float16)   # output only
+    Cs = torch.empty(N, 2 * H, device="cuda")
+    Y = torch.empty(N, 2 * H, device="cuda")
+    Yb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+    Ydb = torch.empty(N, 2 * H, device="cuda", dtype=torch.bfloat16)
+    W0, W1 = w[0].float().cuda(), w[1].float().cuda()
+    wi = [x.cuda() for x in wih]
+    bs = [x.cuda() for x in bias]
+    xb = ctypes.c_size_t()
+    check(lib().mlvae_lstm_workspace_size(B, H, 1, ctypes.byref(xb)))
+    xbuf = torch.empty(xb.value, device="cuda", dtype=torch.uint8)
+    err = torch.zeros(1, device="cuda", dtype=torch.int32)
+    seed, doff, p = 0x2EED + B, 8 * 2 * H, 0.15
+    if mode:
+        lib().mlvae_lstm_set_debug_mode(mode)
+    try:
+        check(lib().mlvae_lstm_fwd_z(B, T, H, P(W0), P(W1), zb.data_ptr(), ldz, Z, P(wi[0]), P(wi[1]), P(bs[0]),
+                                     P(bs[1]), P(bs[2]), P(bs[3]), P(G), P(Cs), P(Y), Yb.data_ptr(), Ydb.data_ptr(),
+                                     None, 0.0, seed, doff, p, P(xbuf), xb.value, P(err), stream()))
+        torch.cuda.synchronize()
+        assert err.item() == 0
+        ey, ec, eg = (rel_err(Y.view(B, T, 2 * H), y), rel_err(Cs.view(B, T, 2 * H), cs),
+                      rel_err(G.float().view(B, T, 8 * H), gates))
+        print(f"\nfused z projection B={B} T={T} ldz={ldz} mode={mode}: h {ey:.2e} c {ec:.2e} gates {eg:.2e}")
+        assert ey < TOL_Y and ec < TOL_Y and eg < TOL_Y
+        assert torch.equal(Yb, Y.to(torch.bfloat16))
+        mask = torch.from_numpy(dropout_mask(seed, doff + N * 2 * H, p)[doff:]).cuda().view(N, 2 * H)
+        assert torch.equal(Ydb, (Y * mask).to(torch.bfloat16))
+        # the train step's form (no fp32 h, no dropout output): identical gates and bf16 h
+        G1, Yb1 = torch.empty_like(G), torch.empty_like(Yb)
+        check(lib().mlvae_lstm_fwd_z(B, T, H, P(W0), P(W1), zb.data_ptr(), ldz, Z, P(wi[0]), P(wi[1]), P(bs[0]),
+                                     P(bs[1]), P(bs[2]), P(bs[3]), P(G1), P(Cs), None, Yb1.data_ptr(), None, None,
+                                     0.0, 0, 0, 0.0, P(xbuf), xb.value, P(err), stream()))
+        torch.cuda.synchronize()
+        assert err.item() == 0 and torch.equal(Yb1, Yb) and torch.equal(G1, G)
+    finally:
+        lib().mlvae_lstm_set_debug_mode(0)
+    # argument checks: Z != 32, a misaligned ldz
+    assert lib().mlvae_lstm_fwd_z(B, T, H, P(W0), P(W1), zb.data_ptr(), ldz, 16, P(wi[0]), P(wi[1]), P(bs[0]),
+                                  P(bs[1]), P(bs[2]), P(bs[3]), P(G), P(Cs), None, Yb.data_ptr(), None, None, 0.0,
+                                  0, 0, 0.0, P(xbuf), xb.value, P(err), stream()) != 0
+    assert lib().mlvae_lstm_fwd_z(B, T, H, P(W0), P(W1), zb.data_ptr(), 36, Z, P(wi[0]), P(wi[1]), P(bs[0]),
+                                  P(bs[1]), P(bs[2]), P(bs[3]), P(G), P(Cs), None, Yb.data_ptr(), None, None, 0.0,
+                                  0, 0, 0.0, P(xbuf), xb.value, P(err), stream()) != 0
 
 
 def test_gate_buffer_format_is_checked():
