@@ -119,9 +119,12 @@ def conv_fwd_bytes(N, F, E):
     return N * 4 * (F + 3 * E)
 
 
-def conv_bwd_bytes(N, F, E):
-    """Layer-2 input gradient (read dE2, E1; write dE1) + layer-1 weight gradient (read dE1, x)."""
-    return N * 4 * (5 * E + F)
+def conv_bwd_bytes(N, F, E, fused=True):
+    """The Conv1d backward region below the top layer (fp32 activations): the layer-2 input
+    gradient dE1 = conv^T(dE2) * lrelu'(E1) and the layer-1 weight gradient dE1^T x.  Fused
+    (mlvae_conv1d_bwd2) dE1 stays on chip: read dE2, E1, x.  As two kernels: + write and read
+    dE1.  (Through round 4 this counted 5E + F per frame for the two kernels -- one E too many.)"""
+    return N * 4 * ((2 * E + F) if fused else (4 * E + F))
 
 
 def cpu_model():
@@ -331,7 +334,8 @@ def secondary(kern, B, T, cfg_name, dy_bytes=4):
     for name, nbytes, key in (("encoder_fwd", encoder_fwd_bytes(N, F, E, Z), "encoder_fwd"),
                               ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), "encoder_bwd"),
                               ("conv_fwd", conv_fwd_bytes(N, F, E), "conv_fwd"),
-                              ("conv_bwd", conv_bwd_bytes(N, F, E), "conv_bwd"),
+                              ("conv_bwd", conv_bwd_bytes(N, F, E, os.environ.get("MLVAE_CONV_BWD2", "1") != "0"),
+                               "conv_bwd"),
                               ("heads", heads_bytes(N, F, C, H, dy_bytes), "heads")):
         if name in kern:
             gbs = nbytes / (kern[name] * 1e-3) / 1e9

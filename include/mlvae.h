@@ -301,6 +301,16 @@ int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const float* dy, 
 size_t mlvae_conv1d_wgrad_workspace_size(int B, int T, int Cin, int Cout, int K);
 int mlvae_conv1d_wgrad(int B, int T, int Cin, int Cout, int K, const float* dy, int lddy, const float* x,
                        int ldx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
+/* The Conv1d encoder's backward below the top layer in one pass: the layer-2 input gradient
+ * dE1 = conv^T(dE2) * lrelu'(E1) (as mlvae_conv1d_dgrad with aux = E1) feeds the layer-1 weight
+ * and bias gradients (as mlvae_conv1d_wgrad with dy = dE1, x = the layer-1 input) through LDS:
+ * dE1 is never written (dx: optional fp32 copy).  E = the encoder width (layer 2: E -> E),
+ * F = the layer-1 input channels; limits of mlvae_conv1d_supported(F, E, K).  Workspace as
+ * mlvae_conv1d_wgrad's for (F, E, K). */
+size_t mlvae_conv1d_bwd2_workspace_size(int B, int T, int F, int E, int K);
+int mlvae_conv1d_bwd2(int B, int T, int F, int E, int K, const float* dy, int lddy, const float* w,
+                      const float* aux, int ldaux, const float* x, int ldx, float* dx, int lddx, float* dw,
+                      float* db, void* ws, size_t ws_bytes, void* stream);
 
 /* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
  * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */

@@ -356,7 +356,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   constexpr bool ADMA = !(AKC && BKC);  // a transposed-read operand: LDS-DMA from asm (dma16)
   const int kbeg = kz * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
-  constexpr int SBK = VAR == 12 ? DBK : (VAR == 9 ? 128 : TBK);  // K per main-loop step
+  constexpr int SBK = (VAR == 12 || VAR == 13) ? DBK : (VAR == 9 ? 128 : TBK);  // K per main-loop step
   const int nk = kend > kbeg ? (kend - kbeg + SBK - 1) / SBK : 0;
 
   f32x4 acc[8][4];
@@ -406,7 +406,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-  } else if constexpr (VAR == 12) {
+  } else if constexpr (VAR == 12 || VAR == 13) {
+    // (VAR 13: this loop with timing ablations, MLVAE_GEMM_ABL bit 1 no MFMAs, bit 2 no staging)
+    constexpr bool ABLV = VAR == 13;
     // VAR 12: ping-pong.  Two groups of four waves -- waves 0-3 and 4-7, one of each on every
     // SIMD -- run one barrier apart over a ring of four BK-32 buffers: while one group's waves
     // issue their 32 MFMAs, the other group's read their next fragments from LDS and stage a
@@ -459,17 +461,24 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) af[i] = frag32<AKC>(As, wm * 128 + i * 16, lane);
       }
-      if (it + 3 < nk) share(it + 3);
+      if (it + 3 < nk && !(ABLV && (g.abl & 2))) share(it + 3);
       if (it + 1 < nk) wait_younger(min(2, nk - it - 2));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);  // the MFMAs stay in their slot
       __builtin_amdgcn_s_setprio(1);
+      if (ABLV && (g.abl & 1)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bfr[j]));
+      } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -1073,6 +1082,9 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
     case 5: return launch_fast_v<AKC, BKC, 0>(g, grid, s);  // the previous default (A/B)
     case 6: return launch_fast_v<AKC, BKC, 6>(g, grid, s);  // VAR 0 with the MLVAE_GEMM_ABL switches
     case 12: return launch_fast_v<AKC, BKC, 12>(g, grid, s);
+    case 13:  // VAR 12 with the timing ablations (k-contiguous operands only)
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 13>(g, grid, s);
+      return 1;
     case 8:
       if constexpr (AKC && BKC) return launch_fast_v<true, true, 8>(g, grid, s);
       return 1;

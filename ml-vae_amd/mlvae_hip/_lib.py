@@ -50,7 +50,9 @@ _SIGS = {
     "mlvae_conv1d_fwd": [I, I, I, I, I, P, I, P, P, I, P, I, P],
     "mlvae_conv1d_dgrad": [I, I, I, I, I, P, I, P, P, I, P, I, P],
     "mlvae_conv1d_wgrad_workspace_size": [I, I, I, I, I],
+    "mlvae_conv1d_bwd2_workspace_size": [I, I, I, I, I],
     "mlvae_conv1d_wgrad": [I, I, I, I, I, P, I, P, I, P, P, P, SZ, P],
+    "mlvae_conv1d_bwd2": [I, I, I, I, I, P, I, P, P, I, P, I, P, I, P, P, P, SZ, P],
     "mlvae_boundary_fwd": [SZ, P, P, P, P, U64, U64, P, P, P, P],
     "mlvae_boundary_bwd": [SZ, P, P, P, P, U64, U64, P, P, P, P, P, P],
     "mlvae_lstm1_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
@@ -122,6 +124,7 @@ _SIGS = {
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
     "mlvae_conv1d_wgrad_workspace_size": SZ,
+    "mlvae_conv1d_bwd2_workspace_size": SZ,
     "mlvae_fp8_scale_workspace_size": SZ,
     "mlvae_gemm_fp8_tn_workspace_size": SZ,
     "mlvae_gemm_workspace_size": SZ,

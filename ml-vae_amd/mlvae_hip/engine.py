@@ -410,6 +410,9 @@ class VAEEngine:
         # ... or fused into the layer-0 forward recurrence (mlvae_lstm_fwd_z: the 8H-wide fp16
         # projection is never written; MLVAE_ZPROJ=0: the skinny kernel + mlvae_lstm_fwd_ex2, A/B)
         self.zproj = os.environ.get("MLVAE_ZPROJ", "1") != "0"
+        # Conv1d encoder: the layer-2 input gradient and layer-1 weight gradient as one pass
+        # (mlvae_conv1d_bwd2; MLVAE_CONV_BWD2=0: the two kernels, A/B)
+        self.conv_bwd2 = os.environ.get("MLVAE_CONV_BWD2", "1") != "0"
         # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
         self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
         self.side_stream = torch.cuda.Stream(self.device)
@@ -1206,14 +1209,18 @@ class VAEEngine:
                 check(l.mlvae_conv1d_wgrad(B, T, cin, E, K, _p(dy), E, xin, cin, gp(f"{ep}.{name}.weight"),
                                            gp(f"{ep}.{name}.bias"), _p(ws), ws.numel() * 4, self._stream()),
                       "conv1d_wgrad")
-            # the whole Conv1d backward in the timed region: the layer-2 weight gradient on the side
-            # stream beside the input gradient, then the layer-1 weight gradient, joined
+            self._side(lambda: wgc(E, w.dE2, _p(w.E1), 2, w.conv_ws[1]))
             with self._timed("conv_bwd"):
-                self._side(lambda: wgc(E, w.dE2, _p(w.E1), 2, w.conv_ws[1]))
-                check(l.mlvae_conv1d_dgrad(B, T, E, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1), E,
-                                           _p(w.dE1), E, s), "conv1d_dgrad")
-                wgc(Fd, w.dE1, _p(w.x), 0, w.conv_ws[0])
-                self._join_side()
+                if self.conv_bwd2:
+                    # layer-2 input gradient -> layer-1 weight gradient through LDS (dE1 never written)
+                    check(l.mlvae_conv1d_bwd2(B, T, Fd, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1), E,
+                                              _p(w.x), Fd, None, 0, gp(f"{ep}.0.weight"), gp(f"{ep}.0.bias"),
+                                              _p(w.conv_ws[0]), w.conv_ws[0].numel() * 4, s), "conv1d_bwd2")
+                else:
+                    check(l.mlvae_conv1d_dgrad(B, T, E, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1),
+                                               E, _p(w.dE1), E, s), "conv1d_dgrad")
+                    wgc(Fd, w.dE1, _p(w.x), 0, w.conv_ws[0])
+            self._join_side()
             return
 
         def wge1():
