@@ -334,7 +334,7 @@ def secondary(kern, B, T, cfg_name, dy_bytes=4):
     for name, nbytes, key in (("encoder_fwd", encoder_fwd_bytes(N, F, E, Z), "encoder_fwd"),
                               ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), "encoder_bwd"),
                               ("conv_fwd", conv_fwd_bytes(N, F, E), "conv_fwd"),
-                              ("conv_bwd", conv_bwd_bytes(N, F, E, os.environ.get("MLVAE_CONV_BWD2", "1") != "0"),
+                              ("conv_bwd", conv_bwd_bytes(N, F, E, os.environ.get("MLVAE_CONV_BWD2", "0") == "1"),
                                "conv_bwd"),
                               ("heads", heads_bytes(N, F, C, H, dy_bytes), "heads")):
         if name in kern:
@@ -343,6 +343,52 @@ def secondary(kern, B, T, cfg_name, dy_bytes=4):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": nbytes,
                          "traffic": pmc_traffic(f"{cfg_name}/{key}")}
+    return out
+
+
+def conv_standalone(cfg_name, device, iters=50):
+    """The Conv1d encoder's kernels timed alone (HIP events) at the config's shapes on synthetic
+    data: in the train step the backward shares the chip with the side-stream weight-gradient
+    GEMMs, so its in-step time measures that contention, not the kernels."""
+    from mlvae_hip._lib import check, lib
+    F, E, Z, H, L, C, B, T, _ = CONFIGS[cfg_name]
+    K, N, l = ENC_CONV[cfg_name], B * T, lib()
+    s = torch.cuda.current_stream(device).cuda_stream
+    g = torch.Generator(device=device).manual_seed(5)
+    x, e1, de2 = (torch.randn(N, c, device=device, generator=g) for c in (F, E, E))
+    w1, w2 = torch.randn(E, F, K, device=device) * 0.05, torch.randn(E, E, K, device=device) * 0.05
+    b1, de1, y1 = torch.zeros(E, device=device), torch.empty(N, E, device=device), torch.empty(N, E, device=device)
+    dw1, db1 = torch.empty_like(w1), torch.empty(E, device=device)
+    nb = l.mlvae_conv1d_wgrad_workspace_size(B, T, F, E, K)
+    ws = torch.empty(nb // 4 + 1, device=device)
+
+    def bwd():
+        check(l.mlvae_conv1d_dgrad(B, T, E, E, K, de2.data_ptr(), E, w2.data_ptr(), e1.data_ptr(), E,
+                                   de1.data_ptr(), E, s))
+        check(l.mlvae_conv1d_wgrad(B, T, F, E, K, de1.data_ptr(), E, x.data_ptr(), F, dw1.data_ptr(),
+                                   db1.data_ptr(), ws.data_ptr(), nb, s))
+
+    def fwd():
+        check(l.mlvae_conv1d_fwd(B, T, F, E, K, x.data_ptr(), F, w1.data_ptr(), b1.data_ptr(), 1, y1.data_ptr(), E, s))
+
+    out = {}
+    for name, fn, nbytes, what in (
+            ("conv_bwd", bwd, conv_bwd_bytes(N, F, E, False),
+             "layer-2 input gradient + layer-1 weight gradient (+ slab reduce), alone"),
+            ("conv_fwd_layer1", fwd, N * 4 * (F + E), "layer-1 forward (+ LeakyReLU), alone")):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(device)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        torch.cuda.synchronize(device)
+        ms = a.elapsed_time(b) / iters
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"what": what, "bound": "hbm", "avg_launch_ms": ms, "achieved": gbs, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": nbytes}
     return out
 
 
@@ -380,6 +426,7 @@ def extra_runs(args, device):
                 out[key]["pmc_bytes_per_launch"] = {k: pmc_traffic(f"{cname}/{k}") for k in
                                                     ("conv_fwd_layer", "conv_dgrad", "conv_wgrad")}
                 out[key]["pmc_source"] = pmc_source(cname)
+                out[key]["kernels_standalone"] = conv_standalone(cname, device)
             else:
                 sec = secondary(kern, B, T, cname, dyb)
                 if cname in FP8:  # against the fp8 (block-scaled) MFMA peak

@@ -411,8 +411,10 @@ class VAEEngine:
         # projection is never written; MLVAE_ZPROJ=0: the skinny kernel + mlvae_lstm_fwd_ex2, A/B)
         self.zproj = os.environ.get("MLVAE_ZPROJ", "1") != "0"
         # Conv1d encoder: the layer-2 input gradient and layer-1 weight gradient as one pass
-        # (mlvae_conv1d_bwd2; MLVAE_CONV_BWD2=0: the two kernels, A/B)
-        self.conv_bwd2 = os.environ.get("MLVAE_CONV_BWD2", "1") != "0"
+        # (mlvae_conv1d_bwd2), opt-in MLVAE_CONV_BWD2=1: it reads 38 % fewer bytes but standalone
+        # at configs[3] takes 65.7 us against the two kernels' 62.5 (one workgroup per CU runs
+        # the dgrad and weight-gradient phases back to back; profiles/ab/r04_conv_standalone.txt)
+        self.conv_bwd2 = os.environ.get("MLVAE_CONV_BWD2", "0") == "1"
         # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
         self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
         self.side_stream = torch.cuda.Stream(self.device)
