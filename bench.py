@@ -78,13 +78,14 @@ def lstm_launch_bytes(B, T, H, gate_bytes=4, dg_bytes=4, dy_bytes=4):
     return B * T * (8 * H * gate_bytes + 2 * H * 4 + 2 * H * dy_bytes + 8 * H * dg_bytes)
 
 
-def lstm_fwd_launch_bytes(B, T, H, L, gate_bytes=2, h_bytes=2, drop=True, fp8=False):
+def lstm_fwd_launch_bytes(B, T, H, L, gate_bytes=2, h_bytes=2, drop=True, fp8=False, zin=0):
     """Algorithmic HBM bytes of one forward-recurrence launch (both directions), averaged over
     the L layers' launches (the HIP-event timer averages them too).  Per frame: read the input
     projection [8H] (gate_bytes: 2 = fp16 on the wide path), write the activated gates [8H]
     (same width), c [2H] fp32 and h [2H] (h_bytes: 2 = the bf16 GEMM operand); layers below the
-    top also write dropout(h) [2H] bf16 (drop) and, in fp8 mode, its e4m3 copy [2H]."""
-    per = [8 * H * gate_bytes * 2 + 2 * H * 4 + 2 * H * h_bytes +
+    top also write dropout(h) [2H] bf16 (drop) and, in fp8 mode, its e4m3 copy [2H].  zin > 0:
+    layer 0 computes its projection itself (mlvae_lstm_fwd_z) and reads the bf16 latent [zin]."""
+    per = [(zin * 2 if (zin and l == 0) else 8 * H * gate_bytes) + 8 * H * gate_bytes + 2 * H * 4 + 2 * H * h_bytes +
            ((2 * H * 2 + (2 * H if fp8 else 0)) if (drop and l < L - 1) else 0) for l in range(L)]
     return B * T * sum(per) / L
 
@@ -502,6 +503,7 @@ def main():
     kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
     launches = {k: len(v) for k, v in timers.items()}
     dyb = 2 if getattr(eng, "dy_bf16", False) else 4   # dY width the engine's bf16 step used
+    zp = bool(getattr(eng, "zproj", False))             # layer 0's projection inside its forward
     del eng
     torch.cuda.empty_cache()
     if rank == 0:
@@ -512,7 +514,7 @@ def main():
             "lstm_fwd": recurrence_roofline(
                 "lstm_fwd", "persistent BiLSTM forward recurrence, both directions, one launch per layer",
                 lstm_fwd_launch_bytes(B, T, H, L, 2 if g16 else 4, 2 if bf else 4, True,
-                                      args.config in FP8 and bf),
+                                      args.config in FP8 and bf, Z if (zp and g16 and bf and Z == 32) else 0),
                 lstm_launch_flops(B, T, H), kern["lstm_fwd"], launches["lstm_fwd"], T, args.config, args.prec),
             "lstm_bwd": recurrence_roofline(
                 "lstm_bwd", "persistent BiLSTM BPTT recurrence, both directions, one launch per layer",
