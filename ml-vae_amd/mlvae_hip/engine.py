@@ -415,6 +415,10 @@ class VAEEngine:
         # at configs[3] takes 65.7 us against the two kernels' 62.5 (one workgroup per CU runs
         # the dgrad and weight-gradient phases back to back; profiles/ab/r04_conv_standalone.txt)
         self.conv_bwd2 = os.environ.get("MLVAE_CONV_BWD2", "0") == "1"
+        # full-chip steps, opt-in (MLVAE_TAIL_OVERLAP=1): the tail after the last BPTT overlaps its
+        # weight gradient -- measured slower at c3, 10.26 -> 10.39 ms/step: the 160-CU GEMM holds
+        # the encoder backward off the chip (0.105 -> 0.279 ms), profiles/ab/r04_tail_overlap.txt
+        self.tail_overlap = os.environ.get("MLVAE_TAIL_OVERLAP", "0") == "1"
         # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
         self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
         self.side_stream = torch.cuda.Stream(self.device)
@@ -1117,6 +1121,13 @@ class VAEEngine:
             # this GEMM).  Below the bottom layer nothing waits on the dgrad: its weight
             # gradients, the step's longest tail, go first.
             if li == 0:
+                if full and self.tail_overlap and self._env_overlap is None:
+                    # The last BPTT is queued: nothing in the step's tail waits on co-resident
+                    # recurrence workgroups any more, so dW_hh_l0 goes to the side stream on
+                    # 160 CUs beside the dZ / encoder backward / dW_ih_l0 chain (as below a full
+                    # chip) instead of ahead of it (opt-in, measured slower: see __init__)
+                    self.overlap = True
+                    split_tail = self.split_tail
                 self._defer_side(pending, wgl)
             dx = w.dZs if li == 0 else w.dY[li - 1]
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
