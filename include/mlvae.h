@@ -393,6 +393,16 @@ int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, const void* Bt,
 size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K);
 int mlvae_skinny_tn(int M, int NB, int K, const void* A, int lda, const void* B, int ldb, int nw,
                     float* W, float* bias1, float* bias2, float* ws, size_t ws_bytes, void* stream);
+/* dZ = dG W_ih_l0 (as mlvae_skinny_nt) and dW_ih_l0 | b_ih = b_hh gradients = dG^T [z | 1] (as
+ * mlvae_skinny_tn) from ONE pass over the layer-0 dG (ref:src/modules/decoder.py:14-15,22, the
+ * autograd of nn.LSTM's layer-0 input projection): dG [M][lda] bf16 with K8 = 8H columns
+ * (K8 % 256 == 0), Wt = W_ih^T [32][ldw] bf16, zb = [z | 1 | 0] [M][ldz >= 48] bf16 (Z = 32), dZ
+ * [M][lddz] fp32; W [K8][32], bias1 / bias2 [K8] (optional).  Deterministic (fixed-order slab
+ * reduce). */
+size_t mlvae_skinny_dzw_workspace_size(int M, int K8);
+int mlvae_skinny_dzw(int M, int K8, const void* A, int lda, const void* Wt, int ldw, const void* zb, int ldz, int Z,
+                     float* dZ, int lddz, float* W, float* bias1, float* bias2, float* ws, size_t ws_bytes,
+                     void* stream);
 /* Fused VanillaVAE encoder (bf16; mlvae_encoder_supported: E == 64, Z == 32, F in {64, 80}).
  * Forward: FC(F->E) LReLU FC(E->E) LReLU -> [mu | log_var] -> z = eps exp(lv/2) + mu, with the
  * masked KL sums in kl_partials[mlvae_encoder_partials_count] (read by mlvae_elbo_finalize).

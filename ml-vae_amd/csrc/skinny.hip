@@ -257,6 +257,129 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
   for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(out + 16 * j + 4 * q) = acc[j];
 }
 
+// skinny_dzw: dZ = dG W_ih (as skinny_nt) AND the slabs of dW_ih | db = dG^T [z | 1] (as
+// skinny_tn) from ONE pass over dG -- the two kernels each streamed the whole 1 GB dG of c3.
+// A workgroup (8 waves) owns NRB 128-frame row blocks and walks dG in 256-column chunks (chunks
+// outer, its row blocks inner): each [128 x 256] tile goes through LDS once and feeds both
+// products -- dZ by row-major fragments (accumulated over the chunks in registers), dW^T by
+// transposed reads (accumulated over the row blocks, one slab row-range per chunk).  The next
+// tile's 16-byte loads are issued before this tile's MFMAs.  Slabs [G][8H][NB] reduce in a
+// fixed order (skinny_reduce).  Z == 32, NB == 48 (z | 1 | pad), K8 % 256 == 0.
+constexpr int DZW_KC = 256, DZW_LA = DZW_KC + 8, DZW_NB = 48, DZW_LZ = DZW_NB + 8, DZW_Z = 32, DZW_NRB = 4;
+__global__ __launch_bounds__(512) void skinny_dzw_kernel(int M, int K8, const unsigned short* __restrict__ A, int lda,
+                                                         const unsigned short* __restrict__ Wt, int ldw,
+                                                         const unsigned short* __restrict__ Zb, int ldz,
+                                                         float* __restrict__ dZ, int lddz, float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) short smem[];
+  short* sa = smem;                             // [128 frames][DZW_LA]: the dG tile
+  short* sw = sa + 128 * DZW_LA;                // [32 z][DZW_LA]: W_ih^T chunk
+  short* sz = sw + DZW_Z * DZW_LA;              // [NRB][128 frames][DZW_LZ]: z | 1 | pad
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, q = lane >> 4;
+  const int rb0 = blockIdx.x * DZW_NRB;         // first 128-row block of this workgroup
+  const int nrb_all = (M + 127) / 128;
+  const int nrb = min(DZW_NRB, nrb_all - rb0);  // >= 1
+  const int nch = K8 / DZW_KC;
+  // z blocks (bf16, NB columns), once
+  for (int i = tid; i < nrb * 128 * (DZW_NB / 8); i += 512) {
+    const int r = i / (DZW_NB / 8), c8 = i % (DZW_NB / 8), f = rb0 * 128 + r;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (f < M) v = *reinterpret_cast<const u32x4*>(Zb + (size_t)f * ldz + 8 * c8);
+    *reinterpret_cast<u32x4*>(sz + r * DZW_LZ + 8 * c8) = v;
+  }
+  // dG tile loads: 128 rows x 32 16-byte pieces = 4096 pieces, 8 per thread
+  u32x4 va[8];
+  auto aload = [&](int c, int rb) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = tid + 512 * i, r = idx >> 5, c8 = idx & 31, f = (rb0 + rb) * 128 + r;
+      va[i] = f < M ? *reinterpret_cast<const u32x4*>(A + (size_t)f * lda + c * DZW_KC + 8 * c8) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto astore = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = tid + 512 * i, r = idx >> 5, c8 = idx & 31;
+      *reinterpret_cast<u32x4*>(sa + r * DZW_LA + 8 * c8) = va[i];
+    }
+  };
+  f32x4 adz[DZW_NRB][2];
+#pragma unroll
+  for (int b = 0; b < DZW_NRB; ++b) adz[b][0] = adz[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, i4 = lane & 15, qq = i4 >> 2, pp = i4 & 3;
+  aload(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    f32x4 aw[2][3];  // dW^T tiles: m-tiles wave, wave + 8 of the chunk's 16; n-tiles 0..2
+#pragma unroll
+    for (int t = 0; t < 2; ++t) aw[t][0] = aw[t][1] = aw[t][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb < nrb; ++rb) {
+      __syncthreads();  // the previous tile's (and chunk's) LDS reads are done
+      astore();
+      if (rb == 0) {  // this chunk's W_ih^T rows: 32 x 256
+        for (int i = tid; i < DZW_Z * (DZW_KC / 8); i += 512) {
+          const int r = i / (DZW_KC / 8), c8 = i % (DZW_KC / 8);
+          *reinterpret_cast<u32x4*>(sw + r * DZW_LA + 8 * c8) =
+              *reinterpret_cast<const u32x4*>(Wt + (size_t)r * ldw + c * DZW_KC + 8 * c8);
+        }
+      }
+      __syncthreads();
+      // next tile in flight under this one's MFMAs
+      if (rb + 1 < nrb) aload(c, rb + 1);
+      else if (c + 1 < nch) aload(c + 1, 0);
+      // dZ[rows 16 wave .. +15 of block rb][32] += tile . W_ih  (swapped: lane holds z 16 j + 4 q + r)
+#pragma unroll
+      for (int u = 0; u < DZW_KC / 32; ++u) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(sa + (16 * wave + l15) * DZW_LA + 32 * u + 8 * q);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(sw + (16 * j + l15) * DZW_LA + 32 * u + 8 * q);
+#pragma unroll
+          for (int b = 0; b < DZW_NRB; ++b)
+            if (b == rb) adz[b][j] = mfma16(bw, af, adz[b][j]);
+        }
+      }
+      // dW^T[chunk cols][NB] += tile^T . [z | 1]  (transposed reads over the 128 frames)
+      const short* zb = sz + rb * 128 * DZW_LZ;
+#pragma unroll
+      for (int kk = 0; kk < 128; kk += 32) {
+        const int r1 = kk + 8 * g + qq, r2 = r1 + 4;
+        bf16x8 bz[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(zb + r1 * DZW_LZ + 16 * j + 4 * pp));
+          const bf16x4 b2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(zb + r2 * DZW_LZ + 16 * j + 4 * pp));
+          bz[j] = bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int m0 = 16 * (wave + 8 * t);
+          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r1 * DZW_LA + m0 + 4 * pp));
+          const bf16x4 a2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r2 * DZW_LA + m0 + 4 * pp));
+          const bf16x8 af = {a1[0], a1[1], a1[2], a1[3], a2[0], a2[1], a2[2], a2[3]};
+#pragma unroll
+          for (int j = 0; j < 3; ++j) aw[t][j] = mfma16(bz[j], af, aw[t][j]);  // lane: P[m][16 j + 4 q + r]
+        }
+      }
+    }
+    // this chunk's slab rows: slab[blockIdx.x][c * 256 + m][NB]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int m = c * DZW_KC + 16 * (wave + 8 * t) + l15;
+      float* out = slabs + ((size_t)blockIdx.x * K8 + m) * DZW_NB;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) *reinterpret_cast<f32x4*>(out + 16 * j + 4 * q) = aw[t][j];
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < DZW_NRB; ++b) {
+    const int f = (rb0 + b) * 128 + 16 * wave + l15;
+    if (b < nrb && f < M) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) *reinterpret_cast<f32x4*>(dZ + (size_t)f * lddz + 16 * j + 4 * q) = adz[b][j];
+    }
+  }
+}
+
 // W[m][n] = sum_s P_s[m][n] for n < nw; bias1[m] = bias2[m] = sum_s P_s[m][nw] (if given)
 __global__ __launch_bounds__(256) void skinny_reduce(int M, int NB, int S, int nw, const float* __restrict__ ws,
                                                      float* __restrict__ W, float* __restrict__ b1,
@@ -458,6 +581,52 @@ extern "C" int mlvae_skinny_tn(int M, int NB, int K, const void* A, int lda, con
   int blocks = (int)((total + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   skinny_reduce<<<blocks, 256, 0, st>>>(M, NB, S, nw, ws, W, bias1, bias2);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// dZ = dG W_ih and dW_ih | b_ih = b_hh grads = dG^T [z | 1] in one pass over dG (skinny_dzw_kernel):
+// dG [M][lda] bf16 (K8 = 8H columns), Wt = W_ih^T [32][ldw] bf16, zb = [z | 1 | 0] [M][ldz] bf16 with
+// 48 columns, dZ [M][lddz] fp32; W [K8][32], bias1 / bias2 [K8] (both optional).
+extern "C" size_t mlvae_skinny_dzw_workspace_size(int M, int K8) {
+  const int G = ((M + 127) / 128 + DZW_NRB - 1) / DZW_NRB;
+  return (size_t)G * K8 * DZW_NB * sizeof(float);
+}
+
+extern "C" int mlvae_skinny_dzw(int M, int K8, const void* A, int lda, const void* Wt, int ldw, const void* zb, int ldz,
+                                int Z, float* dZ, int lddz, float* W, float* bias1, float* bias2, float* ws,
+                                size_t ws_bytes, void* stream) {
+  if (M <= 0) return 0;
+  if (!A || !Wt || !zb || !dZ || !W || Z != DZW_Z || K8 % DZW_KC || K8 <= 0 || lda % 8 || ldw % 8 || ldz % 8 ||
+      ldz < DZW_NB || lddz % 4 || lddz < Z || ((uintptr_t)A % 16) || ((uintptr_t)Wt % 16) || ((uintptr_t)zb % 16) ||
+      ((uintptr_t)dZ % 16)) {
+    mlvae_set_error("mlvae_skinny_dzw: Z = 32, 8H %% 256, z rows of >= 48 bf16 (z | 1 | 0), aligned 16-byte rows");
+    return 1;
+  }
+  const int G = ((M + 127) / 128 + DZW_NRB - 1) / DZW_NRB;
+  if (!ws || ws_bytes < mlvae_skinny_dzw_workspace_size(M, K8)) {
+    mlvae_set_error("mlvae_skinny_dzw: workspace too small");
+    return 1;
+  }
+  const size_t lds = ((size_t)(128 + DZW_Z) * DZW_LA + (size_t)DZW_NRB * 128 * DZW_LZ) * sizeof(short);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)skinny_dzw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess) {
+      mlvae_set_error("mlvae_skinny_dzw: cannot reserve %zu B LDS", lds);
+      return 2;
+    }
+    attr = true;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  skinny_dzw_kernel<<<G, 512, lds, st>>>(M, K8, static_cast<const unsigned short*>(A), lda,
+                                         static_cast<const unsigned short*>(Wt), ldw,
+                                         static_cast<const unsigned short*>(zb), ldz, dZ, lddz, ws);
+  MLVAE_CHECK_LAUNCH();
+  const size_t total = (size_t)K8 * (Z + 1);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  skinny_reduce<<<blocks, 256, 0, st>>>(K8, DZW_NB, G, Z, ws, W, bias1, bias2);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

@@ -76,6 +76,8 @@ _SIGS = {
     "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],
     "mlvae_skinny_tn_workspace_size": [I, I, I],
     "mlvae_skinny_tn": [I, I, I, P, I, P, I, I, P, P, P, P, SZ, P],
+    "mlvae_skinny_dzw": [I, I, P, I, P, I, P, I, I, P, I, P, P, P, P, SZ, P],
+    "mlvae_skinny_dzw_workspace_size": [I, I],
     "mlvae_encoder_supported": [I, I, I],
     "mlvae_encoder_partials_count": [I, I],
     "mlvae_encoder_workspace_size": [I, I, I, I, I],
@@ -125,6 +127,7 @@ _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
     "mlvae_conv1d_wgrad_workspace_size": SZ,
     "mlvae_conv1d_bwd2_workspace_size": SZ,
+    "mlvae_skinny_dzw_workspace_size": SZ,
     "mlvae_fp8_scale_workspace_size": SZ,
     "mlvae_gemm_fp8_tn_workspace_size": SZ,
     "mlvae_gemm_workspace_size": SZ,

@@ -292,6 +292,8 @@ class _Work:
         ws = max(ws, l.mlvae_gemm_bf16_workspace_size(4 * H, H, N, 2))  # both directions' dW_hh
         if self.enc_fused:
             ws = max(ws, l.mlvae_skinny_tn_workspace_size(8 * H, self.ZA, N))
+            if Z == 32 and (8 * H) % 256 == 0:
+                ws = max(ws, l.mlvae_skinny_dzw_workspace_size(N, 8 * H))
         cs = max(l.mlvae_colsum_workspace_size(N, c) for c in (F, C, 2 * C, 8 * H, 2 * Z, E))
         self.gws = empty(max(ws, cs, 16) // 4 + 1, **f)
         self.gws_side = empty(max(ws, cs, 16) // 4 + 1, **f)  # for the wgrad side stream
@@ -419,6 +421,8 @@ class VAEEngine:
         # weight gradient -- measured slower at c3, 10.26 -> 10.39 ms/step: the 160-CU GEMM holds
         # the encoder backward off the chip (0.105 -> 0.279 ms), profiles/ab/r04_tail_overlap.txt
         self.tail_overlap = os.environ.get("MLVAE_TAIL_OVERLAP", "0") == "1"
+        # layer 0's dZ and dW_ih_l0 from one pass over dG (MLVAE_DZW=0: the NT + TN pair, A/B)
+        self.dzw = os.environ.get("MLVAE_DZW", "1") != "0"
         # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
         self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
         self.side_stream = torch.cuda.Stream(self.device)
@@ -942,6 +946,7 @@ class VAEEngine:
         B, T, N = w.B, w.T, w.N
         full = self._full_chip(B)
         self.overlap = not full
+        dzw_done = False   # dW_ih_l0 already produced by the layer-0 skinny_dzw pass
         split_overlap, split_tail = (256, 256) if full else (self.split_overlap, self.split_tail)
         E, Z, H, C, Fd = cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
@@ -1133,9 +1138,21 @@ class VAEEngine:
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
             seed, mask_ptr = w._drop_seed[li - 1] if drop else (None, None)
             if li == 0 and w.enc_fused:
-                # dZ = dG W_ih_l0: [N, 8H] x [8H, Z] on the skinny NT kernel
-                check(l.mlvae_skinny_nt(N, Z, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[0]), 8 * H,
-                                        _p(w.dZs), Z, s), "skinny_nt")
+                if self.dzw and Z == 32 and w.ZA >= 48 and (8 * H) % 256 == 0 and N >= 65536:
+                    # dZ = dG W_ih_l0 and dW_ih_l0 | db = dG^T [z | 1] from one pass over dG
+                    # (skinny.hip skinny_dzw: the skinny NT and TN kernels each read all of it).
+                    # Same box, alternating: c3 10.70 -> 10.49 ms/step; at c2's 16,000 frames its
+                    # 32 workgroups and 786 KB weight slab per workgroup lose (4.36 -> 4.43), so
+                    # smaller batches keep the pair (profiles/ab/r04_dzw.txt)
+                    check(l.mlvae_skinny_dzw(N, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[0]), 8 * H, _pb(w.Zb),
+                                             w.ZA, Z, _p(w.dZs), Z, gp("decoder.rnn.weight_ih_l0"),
+                                             gp("decoder.rnn.bias_ih_l0"), gp("decoder.rnn.bias_hh_l0"),
+                                             _p(w.gws), w.gws_bytes, s), "skinny_dzw")
+                    dzw_done = True
+                else:
+                    # dZ = dG W_ih_l0: [N, 8H] x [8H, Z] on the skinny NT kernel
+                    check(l.mlvae_skinny_nt(N, Z, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[0]), 8 * H,
+                                            _p(w.dZs), Z, s), "skinny_nt")
                 self._flush_side(pending)
                 fused = False
             elif f8_dgrad:
@@ -1199,9 +1216,10 @@ class VAEEngine:
                                         w.enc_ws.numel() * 4, s), "encoder_bwd")
             # dW_ih_l0 | db_ih_l0 = db_hh_l0 = dG^T [z | 1] (skinny.hip), on the main stream
             # while the side stream finishes dW_hh_l0 (the step's two tails run side by side)
-            check(l.mlvae_skinny_tn(8 * H, w.ZA, N, _pb(w.dGb[0]), 8 * H, _pb(w.Zb), w.ZA, Z,
-                                    gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
-                                    gp("decoder.rnn.bias_hh_l0"), _p(w.gws), w.gws_bytes, s), "skinny_tn")
+            if not dzw_done:
+                check(l.mlvae_skinny_tn(8 * H, w.ZA, N, _pb(w.dGb[0]), 8 * H, _pb(w.Zb), w.ZA, Z,
+                                        gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
+                                        gp("decoder.rnn.bias_hh_l0"), _p(w.gws), w.gws_bytes, s), "skinny_tn")
             self._join_side()
             return
         check(l.mlvae_reparam_kl_bwd(B, T, Z, _p(w.ML), 2 * Z, _p(w.eps_used), _p(w.lens), count,

@@ -85,3 +85,41 @@ def test_skinny_proj_matches_fp32_reference(M, N, K, lda):
     # bad shapes are refused, not launched
     assert l.mlvae_skinny_proj(M, N, 40, Ad.data_ptr(), lda, Bd.data_ptr(), 40, None, None, P(C),
                                N, stream()) != 0
+
+
+@pytest.mark.parametrize("M,K8", [(16000, 4096), (1000, 4096), (333, 512), (128000, 4096)])
+def test_skinny_dzw_matches_fp64(M, K8):
+    """mlvae_skinny_dzw: dZ = dG W_ih_l0 and dW_ih_l0 | biases = dG^T [z | 1] from one pass over dG,
+    against fp64 products of the same bf16 operands (ragged M; the c3 shape N = 128,000), and bit-
+    identical reruns (fixed-order slab reduce)."""
+    need_gpu()
+    torch.manual_seed(M + K8)
+    Z, NB = 32, 48
+    dG = torch.randn(M, K8).to(torch.bfloat16)
+    Wt = torch.randn(Z, K8).to(torch.bfloat16)                 # W_ih_l0^T
+    zb = torch.zeros(M, NB)
+    zb[:, :Z] = torch.randn(M, Z)
+    zb[:, Z] = 1.0
+    zb = zb.to(torch.bfloat16)
+    dGd, Wd, zd = dG.cuda(), Wt.cuda(), zb.cuda()
+    ref_dz = (dGd.double() @ Wd.double().t()).cpu()
+    ref_w = (dGd.double().t() @ zd.double()).cpu()             # [K8, NB]
+    l = lib()
+    ws = torch.empty(l.mlvae_skinny_dzw_workspace_size(M, K8) // 4 + 1, device="cuda")
+    outs = []
+    for _ in range(2):
+        dZ = torch.full((M, Z), float("nan"), device="cuda")
+        W = torch.full((K8, Z), float("nan"), device="cuda")
+        b1 = torch.full((K8,), float("nan"), device="cuda")
+        b2 = torch.full((K8,), float("nan"), device="cuda")
+        check(l.mlvae_skinny_dzw(M, K8, dGd.data_ptr(), K8, Wd.data_ptr(), K8, zd.data_ptr(), NB, Z, P(dZ), Z, P(W),
+                                 P(b1), P(b2), P(ws), ws.numel() * 4, stream()))
+        torch.cuda.synchronize()
+        outs.append((dZ.cpu(), W.cpu(), b1.cpu(), b2.cpu()))
+    dZ, W, b1, b2 = outs[0]
+    assert rel_err(dZ, ref_dz) < 1e-5
+    assert rel_err(W, ref_w[:, :Z]) < 1e-5
+    assert rel_err(b1, ref_w[:, Z]) < 1e-5 and torch.equal(b1, b2)
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+    assert l.mlvae_skinny_dzw(M, K8, dGd.data_ptr(), K8, Wd.data_ptr(), K8, zd.data_ptr(), NB, 16, P(dZ), Z, P(W),
+                              None, None, P(ws), ws.numel() * 4, stream()) != 0
