@@ -37,7 +37,11 @@ def _worker(rank, world, port, q):
     assert torch.equal(buckets, flat)
     params = torch.full((5,), float(rank))
     mdist.broadcast_params(params)
-    q.put((rank, loss3[2].item(), flat.reshape(B, T, C), params))
+    # the recurrence timeout word: set on rank 1 only, every rank must see it (and skip Adam
+    # together) -- the MAX all-reduce the engine runs before the fused Adam
+    err = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)
+    mdist.allreduce_err(err)
+    q.put((rank, loss3[2].item(), flat.reshape(B, T, C), params, int(err.item())))
     dist.destroy_process_group()
 
 
@@ -67,7 +71,8 @@ def test_two_rank_allreduce_matches_global_masked_mean():
     ref = O.apply_lens_to_loss(loss, lens)
     lr = loss.clone().requires_grad_(True)
     O.apply_lens_to_loss(lr, lens).backward()
-    for rank, l, g, params in res:
+    for rank, l, g, params, err in res:
         assert abs(l - ref.item()) < 1e-6
         assert torch.allclose(g, lr.grad, atol=1e-7)
         assert torch.equal(params, torch.zeros(5))
+        assert err == 1   # rank 0 sees rank 1's timeout: both skip the update
