@@ -237,9 +237,13 @@ class _Work:
         self.enc_fused = self.bf and enc_fused
         self.ZA = Z + 16 if self.enc_fused else Z
         self.Zb = empty(N, self.ZA, **b16) if self.bf else None  # first layer's GEMM operand
-        self.X8 = empty(N, 2 * H, dtype=torch.uint8) if (self.bf and cfg.fp8) else None  # fp8 layer input
-        # fp8 mode: the top layer's e4m3 dG (the fp8 dgrad operand, written by the BPTT)
-        self.dG8 = empty(N, 8 * H, dtype=torch.uint8) if (self.bf and cfg.fp8) else None
+        # fp8 mode, per layer li >= 1: X8[li] the e4m3 layer input (written by layer li-1's
+        # forward recurrence or a cast), dG8[li] the layer's e4m3 dG (written by its BPTT); both
+        # per layer, because layer li's weight gradient on the side stream still reads them while
+        # the layers below run (one shared pair was overwritten at L >= 3)
+        f8 = self.bf and cfg.fp8
+        self.X8 = {li: empty(N, 2 * H, dtype=torch.uint8) for li in range(1, L)} if f8 else None
+        self.dG8 = {li: empty(N, 8 * H, dtype=torch.uint8) for li in range(1, L)} if f8 else None
         self.E1b = empty(N, E, **b16) if self.enc_fused else None
         self.E2b = empty(N, E, **b16) if self.enc_fused else None
         if self.bf:
@@ -757,8 +761,8 @@ class VAEEngine:
                         check(l.mlvae_cast_fp8(8 * H * din, _pb(self.wih_t[li]), 1, _p(self.w8s[li]), 0.0,
                                                self.w8t[li].data_ptr(), s), "cast_fp8")
                     if not w.__dict__.get("x8_fused", {}).get(li):  # else the recurrence wrote it
-                        check(l.mlvae_cast_fp8(N * din, _pb(xin_bf), 1, None, xs, w.X8.data_ptr(), s), "cast_fp8")
-                    check(l.mlvae_gemm_fp8(N, 8 * H, din, w.X8.data_ptr(), din, self.w8[li].data_ptr(), din,
+                        check(l.mlvae_cast_fp8(N * din, _pb(xin_bf), 1, None, xs, w.X8[li].data_ptr(), s), "cast_fp8")
+                    check(l.mlvae_gemm_fp8(N, 8 * H, din, w.X8[li].data_ptr(), din, self.w8[li].data_ptr(), din,
                                            _p(w.G[li]), 8 * H, _p(self.w8s[li], 1),
                                            self._ptr(f"decoder.rnn.bias_ih_l{li}"),
                                            self._ptr(f"decoder.rnn.bias_hh_l{li}"),
@@ -785,7 +789,9 @@ class VAEEngine:
                       (li == cfg.L - 1 and not (self.fused_heads and w.bf)))
             seed = self._drop_seed(li) if fuse_drop else 0
             # fp8 mode: the recurrence also writes the next layer's e4m3 input (no cast pass)
-            x8_fused = (cfg.fp8 and fuse_drop and not need_y and w.X8 is not None and 2 * H % 16 == 0)
+            x8_fused = (cfg.fp8 and fuse_drop and not need_y and w.X8 is not None and (li + 1) in w.X8
+                        and 2 * H % 16 == 0)
+            x8_ptr = w.X8[li + 1].data_ptr() if x8_fused else None
             w.__dict__.setdefault("x8_fused", {})[li + 1] = x8_fused
             # fp8 mode, opt-in: the recurrent product h W_hh^T on e4m3 operands too
             # (mlvae_lstm_fwd_fp8r; the wide kernels' per-GPU-batch <= 128 form)
@@ -799,7 +805,7 @@ class VAEEngine:
                                              rp("bias_hh_l0_reverse"), _p(w.G[li]), _p(w.Cs[li]),
                                              _p(w.Y[li]) if need_y else None, _pb(w.Yb[li]),
                                              _pb(w.Ydb[li]) if fuse_drop else None,
-                                             w.X8.data_ptr() if x8_fused else None,
+                                             x8_ptr,
                                              x8_scale(cfg.dropout) if x8_fused else 0.0, seed, self._drop_off,
                                              cfg.dropout if fuse_drop else 0.0, _p(w.xbuf), w.xbuf.numel(),
                                              _p(self.err), s), "lstm_fwd_z")
@@ -808,13 +814,13 @@ class VAEEngine:
                                                 self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
                                                 _p(w.Cs[li]), _pb(w.Yb[li]),
                                                 _pb(w.Ydb[li]) if fuse_drop else None,
-                                                w.X8.data_ptr() if x8_fused else None, x8_scale(cfg.dropout),
+                                                x8_ptr, x8_scale(cfg.dropout),
                                                 seed, self._drop_off, cfg.dropout if fuse_drop else 0.0,
                                                 _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd_fp8r")
                 elif x8_fused:
                     check(l.mlvae_lstm_fwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                               _p(w.Cs[li]), _pb(w.Yb[li]), _pb(w.Ydb[li]), w.X8.data_ptr(),
+                                               _p(w.Cs[li]), _pb(w.Yb[li]), _pb(w.Ydb[li]), x8_ptr,
                                                x8_scale(cfg.dropout), seed, self._drop_off, cfg.dropout,
                                                _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd_fp8")
                 else:
@@ -1022,7 +1028,7 @@ class VAEEngine:
             # fp8 mode: the layer's BPTT also writes dG as e4m3 under delayed scaling (the scale
             # from the previous step's amax, this step's amax for the next) for the fp8 dgrad;
             # the first step has no amax yet and keeps the bf16 dgrad
-            f8 = bool(cfg.fp8 and w.g16 and w.dG8 is not None and li in getattr(self, "g8", {}))
+            f8 = bool(cfg.fp8 and w.g16 and w.dG8 is not None and li in w.dG8 and li in getattr(self, "g8", {}))
             f8_dgrad = f8 and self.g8_ready
             with self._timed("lstm_bwd"):
                 # the layer-0 biases come with dW_ih_l0 from skinny_tn when the encoder is fused
@@ -1041,7 +1047,7 @@ class VAEEngine:
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
                                                _p(w.Cs[li]), _p(w.dY[li]), int(dyb), _pb(dGb),
                                                _p(rows) if rows is not None else None,
-                                               w.dG8.data_ptr() if f8_dgrad else None, _p(self.g8[li]),
+                                               w.dG8[li].data_ptr() if f8_dgrad else None, _p(self.g8[li]),
                                                am + 4 * par, _p(w.xbuf), w.xbuf.numel(), _p(self.err), s),
                           "lstm_bwd_fp8")
                 else:
@@ -1071,7 +1077,7 @@ class VAEEngine:
                     l.mlvae_gemm_bf16_set_split_target(prev)
 
             # configs[4]: dW_ih of an fp8 layer on the e4m3 dG (this step's BPTT) and e4m3 input
-            f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and ldx == din and din % 16 == 0
+            f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and li in w.X8 and ldx == din and din % 16 == 0
                        and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, din, N) <= w.gws_bytes)
 
             def wgl_body(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx,
@@ -1090,7 +1096,7 @@ class VAEEngine:
                     with self._timed(f"wgrad_ih_l{li}"):
                         if f8w:
                             ws = w.gws_side if self._on_side else w.gws
-                            check(lib().mlvae_gemm_fp8_tn(8 * H, din, N, w.dG8.data_ptr(), 8 * H, w.X8.data_ptr(),
+                            check(lib().mlvae_gemm_fp8_tn(8 * H, din, N, w.dG8[li].data_ptr(), 8 * H, w.X8[li].data_ptr(),
                                                           din, gp(f"decoder.rnn.weight_ih_l{li}"), din,
                                                           _p(self.g8w[li], 1), _p(ws), w.gws_bytes, self._stream()),
                                   "gemm_fp8_tn")
@@ -1165,7 +1171,7 @@ class VAEEngine:
                 if dyb:
                     w.dy_bf16[li - 1] = True
                 with self._timed(f"dgrad_l{li}"):
-                    check(l.mlvae_gemm_fp8_ex(N, din, 8 * H, w.dG8.data_ptr(), 8 * H, self.w8t[li].data_ptr(),
+                    check(l.mlvae_gemm_fp8_ex(N, din, 8 * H, w.dG8[li].data_ptr(), 8 * H, self.w8t[li].data_ptr(),
                                               8 * H, _p(dx), din, _p(self.g8[li], 1), None, None,
                                               epi8 | (EPI_OUT_BF16 if dyb else 0),
                                               (seed or 0) if epi8 else 0, self._drop_off, cfg.dropout, s),

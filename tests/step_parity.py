@@ -13,6 +13,8 @@ so a max-|delta| bound cannot tell a right update from a wrong one.  Two checks 
   * the norm-relative error of the update vector over those weights.
 A step that moved every parameter the wrong way scores 0 % agreement and error 2.
 """
+from collections import OrderedDict
+
 import numpy as np
 import torch
 
@@ -47,7 +49,19 @@ def run_step(cfg, B, T, seed, lens, x=None):
     new_ref, rec = O.train_step(params, {}, x, lens, eps,
                                 dict(L=cfg.L, loss_type=cfg.loss_type, kld_weight=cfg.kld_weight),
                                 masks, impl="aten")
+    rec["inputs"] = (x, lens, eps, masks)
     return eng, w, rec, new_ref, params
+
+
+def oracle_fp64(cfg, params, inputs):
+    """The oracle's step in fp64 on the SAME fp32-representable parameters, inputs and randomness
+    (promoted exactly): the truth both the engine and the fp32 oracle are measured against.  lens
+    stays fp32 -- length_to_mask's fp32 rel*T quirk is the reference's semantics, not rounding."""
+    x, lens, eps, masks = inputs
+    p64 = OrderedDict((k, v.double()) for k, v in params.items())
+    return O.train_step(p64, {}, x.double(), lens, eps.double(),
+                        dict(L=cfg.L, loss_type=cfg.loss_type, kld_weight=cfg.kld_weight),
+                        None if masks is None else masks.double(), impl="aten")
 
 
 def run_second_step(cfg, B, T, seed, lens):

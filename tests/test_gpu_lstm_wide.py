@@ -149,7 +149,8 @@ def test_fp8_recurrence_forward(B, T):
 
 
 # mode 4096: the wide kernels forced at a small batch; 256: TPW 1 with equal tile shares
-@pytest.mark.parametrize("B,T,ldz,mode", [(256, 16, 32, 0), (64, 20, 40, 0), (48, 9, 32, 4096), (64, 12, 32, 256)])
+@pytest.mark.parametrize("B,T,ldz,mode", [(256, 16, 32, 0), (64, 20, 40, 0), (48, 9, 32, 4096), (64, 12, 32, 256),
+                                           (200, 12, 32, 0), (40, 17, 40, 0)])
 def test_fused_z_projection_forward(B, T, ldz, mode):
     """mlvae_lstm_fwd_z (layer 0 with its input projection z W_ih^T + b_ih + b_hh computed inside the
     recurrence from the 32-wide bf16 latent) against the fp64 loop on the same projection: h, c, the

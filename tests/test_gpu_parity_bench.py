@@ -93,3 +93,21 @@ def test_c5_fp8_second_step_fp8_dgrad_matches_oracle():
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report("c5 fp8 step 2 (fp8 dgrad) B=64 T=500", e, grads)
     _check(e, grads, 0.12, 3e-2)
+
+
+def test_fp8_three_layers_second_step_matches_oracle():
+    """fp8 mode with a 3-layer decoder: layers 1 and 2 both run their projection,
+    dgrad and weight gradient on e4m3, and layer 2's weight gradient on the side stream reads its
+    own e4m3 input and dG while layer 1's BPTT and dgrad run -- per-layer X8 / dG8 buffers.  Step 2
+    (the fp8 dgrad / weight gradient are live from the second step on), B = 48 (ragged batch group
+    of the wide recurrence), T = 120."""
+    need_gpu()
+    from mlvae_hip.engine import VAEConfig
+    cfg = VAEConfig(F=80, E=64, Z=32, H=512, L=3, C=64, dropout=0.15, prec="bf16", fp8=True)
+    B, T = 48, 120
+    lens = torch.linspace(0.6, 1.0, B)
+    eng, w, rec, new_ref, params = run_second_step(cfg, B, T, 811, lens)
+    assert eng.g8_ready and all(float(eng.g8[li][0].item()) != 1.0 for li in (1, 2))
+    e, grads = errors(eng, w, rec, new_ref, params, B, T)
+    report("fp8 L=3 step 2 B=48 T=120", e, grads)
+    _check(e, grads, 0.12, 3e-2)

@@ -72,6 +72,22 @@ def test_c2_bf16_ragged_lengths_match_oracle():
     _check_bf16(e, grads, "c2")
 
 
+def test_c2_dims_ragged_batch_group_B40_matches_oracle():
+    """A batch that is not a multiple of the recurrence's 16-utterance groups: B = 40
+    under the default layer-0 forward with the fused z projection (mlvae_lstm_fwd_z), whose last
+    batch group is half empty (out-of-range rows zero-filled on load, never stored) -- the partial
+    last batch of an epoch takes this path."""
+    need_gpu()
+    cfg = VAEConfig(F=80, E=64, Z=32, H=512, L=2, C=64, dropout=0.15, prec="bf16")
+    B, T = 40, 160
+    lens = torch.linspace(0.5, 1.0, B)
+    eng, w, rec, new_ref, params = run_step(cfg, B, T, 779, lens)
+    assert eng.zproj
+    e, grads = errors(eng, w, rec, new_ref, params, B, T)
+    report("c2 dims bf16 B=40 T=160", e, grads)
+    _check_bf16(e, grads, "c2")
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_c1_dims_match_oracle(prec):
     """configs[0] dims through the HIP path (fp32 parity mode: ELBO 1e-5 relative)."""

@@ -23,11 +23,13 @@ randomness is the engine's own (in-kernel eps read back, dropout masks replayed 
   that intrinsic sensitivity.
 
 The per-step curves are printed (DESIGN.md section 2 records them)."""
+from collections import OrderedDict
+
 import numpy as np
 import pytest
 import torch
 
-from gpu_utils import need_gpu
+from gpu_utils import need_gpu, norm_rel
 from philox_np import dropout_mask
 from step_parity import errors, report, run_step
 
@@ -118,57 +120,106 @@ def test_elbo_trajectory_teacher_forced_160_steps(prec, bound):
         assert min(signs) >= 0.995 and max(uerrs) <= 0.15, (signs, uerrs)
 
 
-def test_elbo_trajectory_free_running_fp32_against_a_reordered_oracle():
+def _p64(params):
+    return OrderedDict((k, v.double()) for k, v in params.items())
+
+
+def _envelope(a):
+    """Running maximum: a signed ELBO difference crosses zero now and then, so the per-step |gap|
+    of two independent drifts can dip to ~0 at any step; its envelope is the stable quantity."""
+    return np.maximum.accumulate(np.asarray(a))
+
+
+def test_elbo_trajectory_free_running_fp32_against_fp64():
+    """Free-running fp32 trajectory anchored on the fp64 oracle.  The engine
+    (fp32 mode) and the fp32 oracle each train their own copy for 100 steps from the same fp32
+    parameters; the fp64 oracle trains a third copy on the same (exactly promoted) inputs, eps and
+    dropout masks.  Both fp32 runs drift from the fp64 truth through rounding amplified by the
+    training dynamics; an engine with only fp32-rounding-level error drifts no faster than the fp32
+    oracle does.  Pre-registered bound (round 5, before the first run): at every step until the
+    fp32 oracle itself is 1e-4 away from fp64, the envelope of the engine's ELBO gap to fp64 stays
+    within 3x the envelope of the fp32 oracle's gap (floored at the fp32 epsilon: no fp32 result
+    is closer to the truth than its own storage rounding).  Parameter-space distances to fp64 are
+    printed alongside."""
     need_gpu()
     from oracle import vae_cpu as O
     eng, params = _engine("fp32")
-    # the control: the oracle itself on the batch in reverse utterance order -- the same
-    # mathematics (the utterances are independent, every sum over them is order-free in exact
-    # arithmetic) summed in another order, so it rounds differently at every step, as a second
-    # fp32 implementation does
     data = _batches()
-    ref, st_ref, ctl, st_ctl = params, {}, params, {}
-    g_l, r_l, c_l = [], [], []
-    rv = torch.arange(B - 1, -1, -1)
+    p32, s32, p64, s64 = params, {}, _p64(params), {}
+    ge, go, de, do = [], [], [], []
     for st in range(FREE_STEPS):
         x, lens = data[st % 4]
         got, eps, masks = _gpu_step(eng, x, lens)
-        ref, rec = O.train_step(ref, st_ref, x, lens, eps, OCFG, masks, impl="aten")
-        ctl, recc = O.train_step(ctl, st_ctl, x[rv], lens[rv], eps[rv], OCFG, masks[:, rv], impl="aten")
-        g_l.append(got)
-        r_l.append(float(rec["out"]["loss"].item()))
-        c_l.append(float(recc["out"]["loss"].item()))
+        p32, r32 = O.train_step(p32, s32, x, lens, eps, OCFG, masks, impl="aten")
+        p64, r64 = O.train_step(p64, s64, x.double(), lens, eps.double(), OCFG, masks.double(), impl="aten")
+        truth = float(r64["out"]["loss"].item())
+        ge.append(abs(got - truth) / abs(truth))
+        go.append(abs(float(r32["out"]["loss"].item()) - truth) / abs(truth))
+        if st % 10 == 9 or st < 3:
+            n64 = sum(v.pow(2).sum().item() for v in p64.values()) ** 0.5
+            de.append((st, sum((eng.view(k).detach().cpu().double() - v).pow(2).sum().item()
+                               for k, v in p64.items()) ** 0.5 / n64,
+                       sum((p32[k].double() - v).pow(2).sum().item() for k, v in p64.items()) ** 0.5 / n64))
     eng.check_errors()
-    g_l, r_l, c_l = map(np.array, (g_l, r_l, c_l))
-    gap = np.abs(g_l - r_l) / np.abs(r_l)
-    ctl_gap = np.abs(c_l - r_l) / np.abs(r_l)
-    print("\n[free-running fp32] step: engine-vs-oracle / reordered-oracle-vs-oracle gap  " +
-          " ".join(f"s{i}:{gap[i]:.1e}/{ctl_gap[i]:.1e}" for i in (0, 10, 20, 30, 40, 60, 80, FREE_STEPS - 1)))
-    assert gap[:20].max() <= 1e-4, gap[:20].max()
-    # later steps: the engine stays about as close to the oracle as the oracle is to itself
-    # summing in another order (a kernel error would open a gap far beyond that)
-    late = slice(40, FREE_STEPS)
-    assert np.median(gap[late]) <= 30 * max(np.median(ctl_gap[late]), 1e-6), \
-        (np.median(gap[late]), np.median(ctl_gap[late]))
+    ge, go = np.array(ge), np.array(go)
+    env_e, env_o = _envelope(ge), _envelope(go)
+    over = np.nonzero(go > 1e-4)[0]
+    stop = int(over[0]) if len(over) else FREE_STEPS
+    print("\n[free-running fp32 vs fp64] step: |ELBO - fp64| engine / fp32 oracle  " +
+          " ".join(f"s{i}:{ge[i]:.1e}/{go[i]:.1e}" for i in (0, 1, 2, 5, 10, 20, 30, 40, 60, 80, FREE_STEPS - 1)))
+    print(f"[free-running fp32 vs fp64] window: steps 0..{stop - 1} (fp32 oracle first past 1e-4 at "
+          f"{stop}); envelope ratio max {np.max(env_e[:stop] / np.maximum(env_o[:stop], FP32_EPS)):.2f}")
+    print("[free-running fp32 vs fp64] |theta - theta64| / |theta64| engine / fp32 oracle  " +
+          " ".join(f"s{s_}:{a:.1e}/{b:.1e}" for s_, a, b in de))
+    assert stop >= 10, f"the fp32 oracle left fp64 after {stop} steps: no window to compare in"
+    bound = 3.0 * np.maximum(env_o[:stop], FP32_EPS)
+    bad = np.nonzero(env_e[:stop] > bound)[0]
+    assert len(bad) == 0, (int(bad[0]), float(env_e[bad[0]]), float(bound[bad[0]]))
 
 
+FP32_EPS = 2.0 ** -23
+
+
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize("B_,seed", [(32, 1301), (256, 1303)])
 def test_fp32_mode_whole_step_at_bench_sizes(B_, seed):
-    """The fp32 parity mode at c2's B=32, T=500 and at the bench's c3_fp32 size B=256, T=500:
-    the ELBO within 1e-4 relative (north star), outputs and gradients at fp32 accuracy, the Adam
-    update checks of step_parity.py."""
+    """The fp32 parity mode at c2's B=32, T=500 and at the bench's c3_fp32 size B=256, T=500,
+    three ways: the engine and the fp32 oracle each against the fp64 oracle on
+    the same parameters, inputs and randomness.  Pre-registered bound (round 5): for the ELBO, the
+    encoder / decoder outputs and every gradient tensor, the engine's norm-relative error to fp64
+    is <= 3x the fp32 oracle's (floored at the fp32 epsilon); plus the absolute bounds of the
+    earlier test (ELBO 1e-4 relative -- the north star -- and the Adam update checks)."""
     need_gpu()
     from mlvae_hip.engine import VAEConfig
+    from step_parity import oracle_fp64
     cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec="fp32")
     Tn = 500
     lens = torch.linspace(0.6, 1.0, B_)
     lens[3], lens[7] = 127 / 500, 254 / 500
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     eng, w, rec, new_ref, params = run_step(cfg, B_, Tn, seed, lens)
     e, grads = errors(eng, w, rec, new_ref, params, B_, Tn)
-    report(f"fp32 mode B={B_} T=500", e, grads)
+    report(f"fp32 mode B={B_} T=500 vs fp32 oracle", e, grads)
+    _, r64 = oracle_fp64(cfg, params, rec["inputs"])
+    o64 = r64["out"]
+    rel = lambda a, b: abs(float(a) - float(b)) / abs(float(b))
+    outs = {"loss": (w.loss[2].item(), rec["out"]["loss"].item(), o64["loss"].item()),
+            "kld_loss": (w.loss[0].item(), rec["out"]["kld_loss"].item(), o64["kld_loss"].item()),
+            "recon_loss": (w.loss[1].item(), rec["out"]["recon_loss"].item(), o64["recon_loss"].item())}
+    rows = [(k, rel(a, t), rel(b, t)) for k, (a, b, t) in outs.items()]
+    tens = {"mu": (w.ML[:, :Z].reshape(B_, Tn, Z), rec["out"]["enc"]["mean"], o64["enc"]["mean"]),
+            "log_var": (w.ML[:, Z:].reshape(B_, Tn, Z), rec["out"]["enc"]["log_var"], o64["enc"]["log_var"]),
+            "mu_x": (w.MUX.reshape(B_, Tn, -1), rec["out"]["dec"]["mean"], o64["dec"]["mean"]),
+            "log_var_x": (w.LVX.reshape(B_, Tn, -1), rec["out"]["dec"]["log_var"], o64["dec"]["log_var"])}
+    rows += [(k, norm_rel(a, t), norm_rel(b, t)) for k, (a, b, t) in tens.items()]
+    rows += [(k, norm_rel(g, r64["grads"][k]), norm_rel(rec["grads"][k], r64["grads"][k]))
+             for k, g in eng.named_grads().items()]
+    print(f"[fp32 mode B={B_} T=500, error vs fp64] name: engine / fp32 oracle (ratio)")
+    for k, a, b in rows:
+        print(f"  {k:42s} {a:.2e} / {b:.2e} ({a / max(b, FP32_EPS):.2f})")
+    worst = max(rows, key=lambda r: r[1] / max(r[2], FP32_EPS))
+    print(f"[fp32 mode B={B_}] worst engine/oracle ratio {worst[1] / max(worst[2], FP32_EPS):.2f} ({worst[0]})")
+    for k, a, b in rows:
+        assert a <= 3.0 * max(b, FP32_EPS), (k, a, b)
     assert e["loss"] <= 1e-4 and e["recon_loss"] <= 1e-4 and e["kld_loss"] <= 1e-4, e
-    for k in ("mu", "log_var", "mu_x", "log_var_x"):
-        assert e[k] <= 1e-4, (k, e[k])
-    for k, v in grads.items():
-        assert v <= 1e-3, (k, v)
     assert e["update_sign"] >= 0.999 and e["update_err"] <= 1e-2, e

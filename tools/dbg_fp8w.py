@@ -27,8 +27,8 @@ def main():
     w = eng.work(B, T)
     N = B * T
     print("g8", eng.g8[1].tolist(), "g8w", eng.g8w[1].tolist(), "x8s", eng.x8s.tolist(), "w8s", eng.w8s[1].tolist())
-    dG8 = w.dG8.view(torch.float8_e4m3fn).view(N, 8 * H).cpu().double()
-    X8 = w.X8.view(torch.float8_e4m3fn).view(N, 2 * H).cpu().double()
+    dG8 = w.dG8[1].view(torch.float8_e4m3fn).view(N, 8 * H).cpu().double()
+    X8 = w.X8[1].view(torch.float8_e4m3fn).view(N, 2 * H).cpu().double()
     print("dG8 finite", bool(torch.isfinite(dG8).all()), "absmax", dG8.abs().max().item(),
           "X8 finite", bool(torch.isfinite(X8).all()), "absmax", X8.abs().max().item())
     ref = (dG8.t() @ X8) * eng.g8w[1][1].item()
@@ -40,7 +40,7 @@ def main():
     C = torch.empty(8 * H, 2 * H, device="cuda")
     nb = l.mlvae_gemm_fp8_tn_workspace_size(8 * H, 2 * H, N)
     ws = torch.empty(nb // 4 + 1, device="cuda")
-    check(l.mlvae_gemm_fp8_tn(8 * H, 2 * H, N, w.dG8.data_ptr(), 8 * H, w.X8.data_ptr(), 2 * H, C.data_ptr(), 2 * H,
+    check(l.mlvae_gemm_fp8_tn(8 * H, 2 * H, N, w.dG8[1].data_ptr(), 8 * H, w.X8[1].data_ptr(), 2 * H, C.data_ptr(), 2 * H,
                               eng.g8w[1].data_ptr() + 4, ws.data_ptr(), nb, torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     Cd = C.cpu().double()
