@@ -78,16 +78,22 @@ def lstm_launch_bytes(B, T, H, gate_bytes=4, dg_bytes=4, dy_bytes=4):
     return B * T * (8 * H * gate_bytes + 2 * H * 4 + 2 * H * dy_bytes + 8 * H * dg_bytes)
 
 
-def lstm_fwd_launch_bytes(B, T, H, L, gate_bytes=2, h_bytes=2, drop=True, fp8=False, zin=0):
-    """Algorithmic HBM bytes of one forward-recurrence launch (both directions), averaged over
-    the L layers' launches (the HIP-event timer averages them too).  Per frame: read the input
-    projection [8H] (gate_bytes: 2 = fp16 on the wide path), write the activated gates [8H]
-    (same width), c [2H] fp32 and h [2H] (h_bytes: 2 = the bf16 GEMM operand); layers below the
-    top also write dropout(h) [2H] bf16 (drop) and, in fp8 mode, its e4m3 copy [2H].  zin > 0:
-    layer 0 computes its projection itself (mlvae_lstm_fwd_z) and reads the bf16 latent [zin]."""
-    per = [(zin * 2 if (zin and l == 0) else 8 * H * gate_bytes) + 8 * H * gate_bytes + 2 * H * 4 + 2 * H * h_bytes +
-           ((2 * H * 2 + (2 * H if fp8 else 0)) if (drop and l < L - 1) else 0) for l in range(L)]
-    return B * T * sum(per) / L
+def lstm_fwd_layer_bytes(B, T, H, L, gate_bytes=2, h_bytes=2, drop=True, fp8=False, zin=0):
+    """Algorithmic HBM bytes of each layer's forward-recurrence launch (both directions).  Per
+    frame: read the input projection [8H] (gate_bytes: 2 = fp16 on the wide path), write the
+    activated gates [8H] (same width), c [2H] fp32 and h [2H] (h_bytes: 2 = the bf16 GEMM
+    operand); layers below the top also write dropout(h) [2H] bf16 (drop) and, in fp8 mode, its
+    e4m3 copy [2H].  zin > 0: layer 0 computes its projection itself (mlvae_lstm_fwd_z) and
+    reads the bf16 latent [zin]."""
+    return [B * T * ((zin * 2 if (zin and l == 0) else 8 * H * gate_bytes) + 8 * H * gate_bytes + 2 * H * 4 +
+                     2 * H * h_bytes + ((2 * H * 2 + (2 * H if fp8 else 0)) if (drop and l < L - 1) else 0))
+            for l in range(L)]
+
+
+def lstm_fwd_launch_bytes(*args, **kw):
+    """The layers' forward launches averaged (the HIP-event timer averages them too)."""
+    per = lstm_fwd_layer_bytes(*args, **kw)
+    return sum(per) / len(per)
 
 
 def lstm_launch_flops(B, T, H):
@@ -120,12 +126,12 @@ def conv_fwd_bytes(N, F, E):
     return N * 4 * (F + 3 * E)
 
 
-def conv_bwd_bytes(N, F, E, fused=True):
+def conv_bwd_bytes(N, F, E):
     """The Conv1d backward region below the top layer (fp32 activations): the layer-2 input
-    gradient dE1 = conv^T(dE2) * lrelu'(E1) and the layer-1 weight gradient dE1^T x.  Fused
-    (mlvae_conv1d_bwd2) dE1 stays on chip: read dE2, E1, x.  As two kernels: + write and read
-    dE1.  (Through round 4 this counted 5E + F per frame for the two kernels -- one E too many.)"""
-    return N * 4 * ((2 * E + F) if fused else (4 * E + F))
+    gradient dE1 = conv^T(dE2) * lrelu'(E1) (read dE2, E1, write dE1) and the layer-1 weight
+    gradient dE1^T x (read dE1, x).  (Through round 4 this counted 5E + F per frame -- one E too
+    many.)"""
+    return N * 4 * (4 * E + F)
 
 
 def cpu_model():
@@ -193,15 +199,28 @@ def pmc_source(cfg):
     return {"file": "profiles/pmc_traffic.json", "config": cfg, **(src or {})}
 
 
-def recurrence_roofline(name, what, nbytes, flops, ms, launches, T, cfg_name, prec):
+def pmc_sum(cfg_name, roles):
+    """Summed PMC bytes per launch of the launches `roles` (one region of the step), or None."""
+    v = [pmc_traffic(f"{cfg_name}/{r}") for r in roles]
+    return None if any(x is None for x in v) else sum(v)
+
+
+def recurrence_roofline(name, what, layer_bytes, flops, ms, launches, T, cfg_name, prec):
     """HBM roofline (algorithmic bytes / HIP-event launch time) + per-step latency of one
-    persistent recurrence kernel."""
+    persistent recurrence kernel.  layer_bytes: algorithmic bytes of each layer's launch; the
+    HIP-event time averages the layers' launches, so `algorithmic_bytes_per_launch` and the PMC
+    `traffic` are the same layer means (per layer in `per_layer`: l0 = the bottom layer)."""
+    nbytes = sum(layer_bytes) / len(layer_bytes)
     dur_s = ms * 1e-3
     achieved = nbytes / dur_s / 1e9
     step_us = ms * 1e3 / T
+    per_layer = {f"l{l}": {"algorithmic_bytes": b, "traffic": pmc_traffic(f"{cfg_name}/{name}_l{l}")}
+                 for l, b in enumerate(layer_bytes)}
+    tl = [v["traffic"] for v in per_layer.values()]
+    traffic = None if any(t is None for t in tl) else sum(tl) / len(tl)
     return {"kernel": name, "what": what, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic(f"{cfg_name}/{name}"), "traffic_source": pmc_source(cfg_name),
+            "traffic": traffic, "traffic_source": pmc_source(cfg_name), "per_layer": per_layer,
             "algorithmic_bytes_per_launch": nbytes, "avg_launch_ms": ms, "launches": launches,
             "mfma_frac": flops / dur_s / 1e12 / MFMA_PEAK_TFLOPS[prec],
             "step_latency_us": step_us, "handoff_floor_us": HANDOFF_FLOOR_US,
@@ -331,19 +350,21 @@ def secondary(kern, B, T, cfg_name, dy_bytes=4):
             tf = wg_flops.get(name, gemm_flops) / (kern[name] * 1e-3) / 1e12
             out[name] = {"what": what, "bound": "mfma", "avg_launch_ms": kern[name],
                          "achieved": tf, "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
-                         "frac": tf / MFMA_PEAK_TFLOPS["bf16"]}
-    for name, nbytes, key in (("encoder_fwd", encoder_fwd_bytes(N, F, E, Z), "encoder_fwd"),
-                              ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), "encoder_bwd"),
-                              ("conv_fwd", conv_fwd_bytes(N, F, E), "conv_fwd"),
-                              ("conv_bwd", conv_bwd_bytes(N, F, E, os.environ.get("MLVAE_CONV_BWD2", "0") == "1"),
-                               "conv_bwd"),
-                              ("heads", heads_bytes(N, F, C, H, dy_bytes), "heads")):
+                         "frac": tf / MFMA_PEAK_TFLOPS["bf16"], "traffic": pmc_traffic(f"{cfg_name}/{name}")}
+    # HBM-bound regions: the timed region's launches (PMC roles, tools/pmc_summary.py) summed, beside
+    # the same region's algorithmic bytes
+    for name, nbytes, roles in (
+            ("encoder_fwd", encoder_fwd_bytes(N, F, E, Z), ["encoder_fwd"]),
+            ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), ["encoder_bwd"]),
+            ("conv_fwd", conv_fwd_bytes(N, F, E), ["conv_fwd_l1", "conv_fwd_l2"]),
+            ("conv_bwd", conv_bwd_bytes(N, F, E), ["conv_dgrad", "conv_wgrad_l1"]),
+            ("heads", heads_bytes(N, F, C, H, dy_bytes), ["heads_p1", "heads_mid", "heads_dy"])):
         if name in kern:
             gbs = nbytes / (kern[name] * 1e-3) / 1e9
             out[name] = {"bound": "hbm", "avg_launch_ms": kern[name], "achieved": gbs,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": nbytes,
-                         "traffic": pmc_traffic(f"{cfg_name}/{key}")}
+                         "traffic": pmc_sum(cfg_name, roles), "traffic_launches": roles}
     return out
 
 
@@ -374,7 +395,7 @@ def conv_standalone(cfg_name, device, iters=50):
 
     out = {}
     for name, fn, nbytes, what in (
-            ("conv_bwd", bwd, conv_bwd_bytes(N, F, E, False),
+            ("conv_bwd", bwd, conv_bwd_bytes(N, F, E),
              "layer-2 input gradient + layer-1 weight gradient (+ slab reduce), alone"),
             ("conv_fwd_layer1", fwd, N * 4 * (F + E), "layer-1 forward (+ LeakyReLU), alone")):
         for _ in range(3):
@@ -425,7 +446,8 @@ def extra_runs(args, device):
                                        if k.startswith("conv")}
                 # PMC HBM bytes per launch of each conv kernel (profiles/pmc_traffic.json[c4])
                 out[key]["pmc_bytes_per_launch"] = {k: pmc_traffic(f"{cname}/{k}") for k in
-                                                    ("conv_fwd_layer", "conv_dgrad", "conv_wgrad")}
+                                                    ("conv_fwd_l1", "conv_fwd_l2", "conv_dgrad", "conv_wgrad_l1",
+                                                     "conv_wgrad_l2")}
                 out[key]["pmc_source"] = pmc_source(cname)
                 out[key]["kernels_standalone"] = conv_standalone(cname, device)
             else:
@@ -513,12 +535,12 @@ def main():
         recs = {
             "lstm_fwd": recurrence_roofline(
                 "lstm_fwd", "persistent BiLSTM forward recurrence, both directions, one launch per layer",
-                lstm_fwd_launch_bytes(B, T, H, L, 2 if g16 else 4, 2 if bf else 4, True,
-                                      args.config in FP8 and bf, Z if (zp and g16 and bf and Z == 32) else 0),
+                lstm_fwd_layer_bytes(B, T, H, L, 2 if g16 else 4, 2 if bf else 4, True,
+                                     args.config in FP8 and bf, Z if (zp and g16 and bf and Z == 32) else 0),
                 lstm_launch_flops(B, T, H), kern["lstm_fwd"], launches["lstm_fwd"], T, args.config, args.prec),
             "lstm_bwd": recurrence_roofline(
                 "lstm_bwd", "persistent BiLSTM BPTT recurrence, both directions, one launch per layer",
-                lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if bf else 4, dyb if g16 else 4),
+                [lstm_launch_bytes(B, T, H, 2 if g16 else 4, 2 if bf else 4, dyb if g16 else 4)] * L,
                 lstm_launch_flops(B, T, H), kern["lstm_bwd"], launches["lstm_bwd"], T, args.config, args.prec),
         }
         # the bench line's roofline names the kernel with the most measured time per step (both

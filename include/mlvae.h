@@ -172,14 +172,6 @@ int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* 
                        float* cells, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
                        unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
                        void* xbuf, size_t xbytes, int* err, void* stream);
-/* As mlvae_lstm_fwd_fp8 with the recurrent product h_{t-1} W_hh^T (ref:src/modules/decoder.py:22,
- * nn.LSTM's hidden GEMM) itself on e4m3 operands where the wide kernels run their per-GPU-batch
- * <= 128 form: W_hh with one E8M0 scale per 32-element block, h at 2^8; the exchange of h stays
- * bf16.  y_drop_bf16 / y_drop_fp8 optional (the top layer has no next-layer input). */
-int mlvae_lstm_fwd_fp8r(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
-                        float* cells, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
-                        unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
-                        void* xbuf, size_t xbytes, int* err, void* stream);
 /* Wide forward of the bottom layer with its input projection fused (replaces the skinny
  * projection + mlvae_lstm_fwd_ex2 pair for ref:src/modules/decoder.py:22, nn.LSTM layer 0 whose
  * input is the 32-wide latent z): each step's gate inputs z_t W_ih^T + b_ih + b_hh are computed
@@ -301,17 +293,6 @@ int mlvae_conv1d_dgrad(int B, int T, int Cin, int Cout, int K, const float* dy, 
 size_t mlvae_conv1d_wgrad_workspace_size(int B, int T, int Cin, int Cout, int K);
 int mlvae_conv1d_wgrad(int B, int T, int Cin, int Cout, int K, const float* dy, int lddy, const float* x,
                        int ldx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
-/* The Conv1d encoder's backward below the top layer in one pass: the layer-2 input gradient
- * dE1 = conv^T(dE2) * lrelu'(E1) (as mlvae_conv1d_dgrad with aux = E1) feeds the layer-1 weight
- * and bias gradients (as mlvae_conv1d_wgrad with dy = dE1, x = the layer-1 input) through LDS:
- * dE1 is never written (dx: optional fp32 copy).  E = the encoder width (layer 2: E -> E),
- * F = the layer-1 input channels; limits of mlvae_conv1d_supported(F, E, K).  Workspace as
- * mlvae_conv1d_wgrad's for (F, E, K). */
-size_t mlvae_conv1d_bwd2_workspace_size(int B, int T, int F, int E, int K);
-int mlvae_conv1d_bwd2(int B, int T, int F, int E, int K, const float* dy, int lddy, const float* w,
-                      const float* aux, int ldaux, const float* x, int ldx, float* dx, int lddx, float* dw,
-                      float* db, void* ws, size_t ws_bytes, void* stream);
-
 /* ELBO: reparameterise + KL (ref:src/modules/vanilla_vae.py:37-45) with masked partial
  * sums; ml = [mu | log_var] rows of width 2Z (leading dim ldml). */
 int mlvae_elbo_partials_count(int B, int T, int C);

@@ -287,152 +287,6 @@ __global__ __launch_bounds__(CT) void conv_wgrad_kernel(WgArgs a) {
   }
 }
 
-// Layer-2 input gradient fused with the layer-1 weight gradient (the Conv1d encoder's backward
-// below the top layer): per 64-frame tile, dE1 = conv^T(dE2) * lrelu'(E1) is computed as in
-// conv_kernel<NT, true> and, instead of going to HBM and being read back by conv_wgrad_kernel,
-// written as bf16 straight into the weight gradient's dy image in LDS; the tile's layer-1 input
-// window is staged beside it.  dE1 is never materialised (optional copy for tests), so the pass
-// reads dE2, E1 and x once: 4 (2 E + F) bytes per frame instead of 4 (4 E + F) over two launches.
-// Same slab / reduce as conv_wgrad_kernel.  E = 16 NT (the encoder width), F = layer-1 input.
-struct Bwd2Args {
-  int T, E, F, K, CinP, Cin16, tpu, ntiles;
-  const float* dy; int lddy;   // dE2 [N][lddy]
-  const float* w;              // layer-2 weight [E][E][K] (torch layout)
-  const float* aux; int ldaux; // E1 = LeakyReLU output of layer 1 (its derivative)
-  const float* x; int ldx;     // layer-1 input [N][ldx]
-  float* dx; int lddx;         // optional fp32 dE1 (tests)
-  float* slabs;
-};
-
-template <int NT>
-__global__ __launch_bounds__(CT) void conv_bwd2_kernel(Bwd2Args a) {
-  extern __shared__ __attribute__((aligned(16))) short smem[];
-  constexpr int E = 16 * NT;
-  const int K = a.K, CinP = a.CinP, KC = K * CinP, p = (K - 1) / 2, Cin16 = a.Cin16;
-  const int ldw = KC + SKEW, ldd = CinP + SKEW, lddy = E + SKEW, ldxl = Cin16 + SKEW;
-  short* Wl = smem;                          // [E][K * CinP]: transposed, time-flipped layer-2 weights
-  short* Dl = Wl + E * ldw;                  // [BM + K - 1][CinP]: dE2 window
-  short* DYl = Dl + (BM + K - 1) * ldd;      // [BM][E]: dE1 tile (bf16), the weight gradient's dy
-  short* Xl = DYl + BM * lddy;               // [BM + K - 1][Cin16]: layer-1 input window
-  if (E < CinP) {  // padding channels [E, CinP) of every (o, tap) row: zero
-    for (int r = threadIdx.x; r < E * K; r += CT) {
-      short* dst = Wl + (r / K) * ldw + (r % K) * CinP + E;
-      for (int c = 0; c < CinP - E; ++c) dst[c] = 0;
-    }
-  }
-  for (int pr = threadIdx.x; pr < E * E; pr += CT) {  // layer (out lo, in li): product row li, column lo
-    const int lo = pr / E, li = pr - lo * E;
-    const float* wp = a.w + (size_t)pr * K;
-    short* dst = Wl + li * ldw + lo;
-    for (int j = 0; j < K; ++j) dst[(K - 1 - j) * CinP] = f2bf(wp[j]);
-  }
-  const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int f = 16 * wave + l15;  // this lane's frame in the tile
-  const int mpj = Cin16 / 16, MT = K * mpj;
-  float unused[4];
-  f32x4 win[NLW], vx[NLX], axc[NT], axn[NT];
-  auto load_tile = [&](int tile_) {
-    const int b_ = tile_ / a.tpu, t0_ = (tile_ - b_ * a.tpu) * BM, t_ = t0_ + f;
-    load_rows(win, a.dy, a.lddy, b_, a.T, t0_ - p, BM + K - 1, E, CinP);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      axn[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t_ < a.T) axn[nt] = *(const f32x4*)(a.aux + ((size_t)b_ * a.T + t_) * a.ldaux + 16 * nt + 4 * q);
-    }
-    load_rows(vx, a.x, a.ldx, b_, a.T, t0_ - p, BM + K - 1, a.F, Cin16);
-  };
-  f32x4 accw[MTW][NT];
-#pragma unroll
-  for (int u = 0; u < MTW; ++u)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) accw[u][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 bsum[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) bsum[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (blockIdx.x < a.ntiles) load_tile(blockIdx.x);
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    const int b = tile / a.tpu, t0 = (tile - b * a.tpu) * BM;
-    lds_barrier();  // weights staged / the previous tile's reads of Dl, Xl, DYl done
-    store_rows<false>(Dl, ldd, win, BM + K - 1, CinP, unused);
-    store_rows<false>(Xl, ldxl, vx, BM + K - 1, Cin16, unused);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) axc[nt] = axn[nt];
-    lds_barrier();
-    if (tile + (int)gridDim.x < a.ntiles) load_tile(tile + gridDim.x);  // in flight under the MFMAs
-    // dE1 = conv^T(dE2) (swapped operands: lane holds channels 16 nt + 4 q .. + 3 of frame f)
-    f32x4 acc[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int kc32 = CinP / 32;
-    for (int ks = 0; ks < K * kc32; ++ks) {
-      const int j = ks / kc32, c0 = (ks - j * kc32) * 32;
-      const bf16x8 xb = *(const bf16x8*)(Dl + (f + j) * ldd + c0 + 8 * q);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const bf16x8 wa = *(const bf16x8*)(Wl + (16 * nt + l15) * ldw + ks * 32 + 8 * q);
-        acc[nt] = mfma16(wa, xb, acc[nt]);
-      }
-    }
-    const int t = t0 + f;
-    const bool valid = t < a.T;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const int o = 16 * nt + 4 * q;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (valid) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] * lrelu_d(axc[nt][r]);
-        if (a.dx) *(f32x4*)(a.dx + ((size_t)b * a.T + t) * a.lddx + o) = v;
-      }
-      bsum[nt] += v;
-      *(bf16x4*)(DYl + f * lddy + o) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-    }
-    lds_barrier();  // the dE1 tile is complete
-    // dW1 += dE1^T x (as conv_wgrad_kernel)
-#pragma unroll
-    for (int kk = 0; kk < BM; kk += 32) {
-      bf16x8 bf[NT];
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) bf[nt] = trfrag(DYl, lddy, 16 * nt, kk, lane);
-#pragma unroll
-      for (int u = 0; u < MTW; ++u) {
-        const int mt = wave + 4 * u;
-        if (mt < MT) {  // wave-uniform
-          const int j = mt / mpj, i0 = (mt - j * mpj) * 16;
-          const bf16x8 af = trfrag(Xl + j * ldxl, ldxl, i0, kk, lane);
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) accw[u][nt] = mfma16(af, bf[nt], accw[u][nt]);
-        }
-      }
-    }
-  }
-  const int NW = MT * NT * 256;
-  const size_t S = (size_t)NW + E;
-  float* slab = a.slabs + (size_t)blockIdx.x * S;
-#pragma unroll
-  for (int u = 0; u < MTW; ++u) {
-    const int mt = wave + 4 * u;
-    if (mt < MT) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        *reinterpret_cast<f32x4*>(slab + ((size_t)(mt * NT + nt) * 64 + lane) * 4) = accw[u][nt];
-    }
-  }
-  // db1: every lane summed its frame's channels 16 nt + 4 q + r; the 64 frame-lanes of a channel
-  // are added in a fixed order through LDS (the images are free now)
-  float* red = reinterpret_cast<float*>(smem);  // [64 frame-lanes][E]
-  __syncthreads();
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) *reinterpret_cast<f32x4*>(red + f * E + 16 * nt + 4 * q) = bsum[nt];
-  __syncthreads();
-  if (threadIdx.x < E) {
-    float sum = 0.f;
-    for (int fl = 0; fl < BM; ++fl) sum += red[fl * E + threadIdx.x];
-    slab[(size_t)NW + threadIdx.x] = sum;
-  }
-}
-
 // The slabs are summed in two fixed-order stages (deterministic): block (column chunk, z) sums
 // slabs [z G / NZ, (z + 1) G / NZ) into part[z]; then the NZ partial rows in order.  (One pass
 // with a thread per column walked all G = 256 slabs alone: ~25 K threads, each a 256-deep chain
@@ -614,50 +468,3 @@ extern "C" int mlvae_conv1d_wgrad(int B, int T, int Cin, int Cout, int K, const 
   return 0;
 }
 
-// Layer-2 input gradient + layer-1 weight gradient in one pass (conv_bwd2_kernel): E = the encoder
-// width (layer-2 in = out channels), F = the layer-1 input channels.  dx (fp32 dE1) optional.
-extern "C" size_t mlvae_conv1d_bwd2_workspace_size(int B, int T, int F, int E, int K) {
-  return mlvae_conv1d_wgrad_workspace_size(B, T, F, E, K);
-}
-
-extern "C" int mlvae_conv1d_bwd2(int B, int T, int F, int E, int K, const float* dy, int lddy, const float* w,
-                                 const float* aux, int ldaux, const float* x, int ldx, float* dx, int lddx,
-                                 float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
-  if (B <= 0 || T <= 0) return 0;
-  if (!mlvae_conv1d_supported(F, E, K) || !dims_ok(B, T, E, E, K) || !dy || !w || !aux || !x || !dw ||
-      lddy < E || ldaux < E || ldx < F || lddy % 4 || ldaux % 4 || ldx % 4 || (dx && (lddx < E || lddx % 4 ||
-      !aligned16(dx))) || !aligned16(dy) || !aligned16(aux) || !aligned16(x) || !aligned16(w)) {
-    mlvae_set_error("mlvae_conv1d_bwd2: unsupported shape/stride/alignment (F %d E %d K %d)", F, E, K);
-    return 1;
-  }
-  if (!ws || ws_bytes < mlvae_conv1d_bwd2_workspace_size(B, T, F, E, K)) {
-    mlvae_set_error("mlvae_conv1d_bwd2: workspace too small");
-    return 1;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  Bwd2Args a{};
-  a.T = T; a.E = E; a.F = F; a.K = K; a.CinP = round_up(E, 32); a.Cin16 = round_up(F, 16);
-  a.tpu = (T + BM - 1) / BM; a.ntiles = B * a.tpu;
-  a.dy = dy; a.lddy = lddy; a.w = w; a.aux = aux; a.ldaux = ldaux; a.x = x; a.ldx = ldx;
-  a.dx = dx; a.lddx = lddx; a.slabs = static_cast<float*>(ws);
-  const int g = wgrad_grid(B, T);
-  const size_t lds = ((size_t)E * (K * a.CinP + SKEW) + (size_t)(BM + K - 1) * (a.CinP + SKEW) +
-                      (size_t)BM * (E + SKEW) + (size_t)(BM + K - 1) * (a.Cin16 + SKEW)) * 2;
-  if (lds < (size_t)BM * E * 4 || lds > 160 * 1024) {
-    mlvae_set_error("mlvae_conv1d_bwd2: LDS %zu bytes", lds);
-    return 1;
-  }
-  const int rc = E == 16 ? launch_lds(conv_bwd2_kernel<1>, g, lds, s, a)
-               : E == 32 ? launch_lds(conv_bwd2_kernel<2>, g, lds, s, a)
-                         : launch_lds(conv_bwd2_kernel<4>, g, lds, s, a);
-  if (rc) return rc;
-  const size_t S = wgrad_slab(F, E, K);
-  const int rb = (int)((S + 255) / 256);
-  float* part = static_cast<float*>(ws) + (size_t)g * S;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rb, NZ), dim3(256), 0, s, static_cast<const float*>(ws), g, S, part);
-  MLVAE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(rb), dim3(256), 0, s, static_cast<const float*>(part), S, S - E,
-                     E / 16, F, a.Cin16, K, dw, db);
-  MLVAE_CHECK_LAUNCH();
-  return 0;
-}

@@ -48,11 +48,8 @@ struct GFArgs {
   int group_m;        // > 1: tiles walk groups of group_m M-panels column-major (L2 reuse)
   int c16;            // C stored as 16-bit: 1 fp16 (epi bit EPI_OUT_F16), 2 bf16 (EPI_OUT_BF16)
   const float* alpha; // device scalar multiplying A.B (fp8 operand scales), or null
-  int stagger;        // VAR 14: realtime ticks per start phase for workgroups with fewer tiles (0: off)
   int abl;            // ablation bits (MLVAE_GEMM_ABL, timing only): 1 no MFMA, 2 no staging loads (VAR 6),
-                      // 4 the direct (unstaged) epilogue, 8 no epilogue, 64 4-column 16-bit C stores;
-                      // VAR 14: 16 start-phase
-                      // stagger of (abl >> 8) & 255 realtime ticks per phase
+                      // 4 the direct (unstaged) epilogue, 8 no epilogue, 64 4-column 16-bit C stores
   float* ws;
 };
 
@@ -790,213 +787,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   }
 }
 
-// ---- VAR 14: the ping-pong loop (VAR 12) made persistent.  One workgroup per CU walks its tiles
-// (virtual blocks wg, wg + G, ... under the same XCD-aware bijection) as ONE stream of BK-32 steps:
-// the ring stages the next tile's first steps during this tile's last ones, and a finished tile's
-// epilogue -- direct buffer stores from the accumulators, left in flight -- runs in the M slot of
-// the next tile's first step, beside the other group's MFMAs.  In the one-tile-per-launch form
-// every CU's epilogue and prologue fell together (a chip-wide 32 MB store burst, then the loads
-// of the next tiles): the projection's per-tile fixed cost was 12.8 us of 39 (tools/gemm_kscan.py,
-// 2.35 us without the epilogue).  Every vm operation of a wave is counted (its stores and bias
-// loads issue unconditionally, out-of-range ones dropped by the buffer range check), so the wait
-// for a staged step is an exact vmcnt.
-__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(<= n), n wave-uniform
-  switch (n >= 60 ? 15 : n >> 2) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
-  }
-}
-
-constexpr size_t PERSIST_LDS = FAST_LDS + 2 * 2 * 256 * sizeof(float);  // + bias rows [2 tiles][2][256]
-
-// C16: 0 fp32 C, 1 fp16, 2 bf16
-template <bool AKC, bool BKC, int C16>
-__global__ __launch_bounds__(512) void gemm256_persist_kernel(GFArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  short* lds = reinterpret_cast<short*>(smem);
-  float* bias_lds = reinterpret_cast<float*>(smem + FAST_LDS);  // [tile & 1][bias1 256 | bias2 256]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wv >> 2, wn = wv & 3, grpw = wv >> 2, w4 = wv & 3;
-  const int TM = (g.M + TBM - 1) / TBM, TN = (g.N + TBN - 1) / TBN, ntiles = TM * TN;
-  const int G = gridDim.x, wg = blockIdx.x;
-  const int ntl = wg < ntiles ? (ntiles - 1 - wg) / G + 1 : 0;
-  const int nk = (g.K + DBK - 1) / DBK;
-  const int total = ntl * nk;
-  const auto ra = make_rsrc(g.A, OOB);
-  const auto rb = make_rsrc(g.B, OOB);
-  auto tile_mn = [&](int j, int& m0_, int& n0_) {
-    const int v = wg + j * G, xcd = v % 8, local = v / 8, q = ntiles / 8, r = ntiles % 8;
-    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
-    int mt = t / TN, nt = t % TN;
-    if (g.group_m > 1) {
-      const int grp = t / (g.group_m * TN), mfirst = grp * g.group_m;
-      const int gsz = min(TM - mfirst, g.group_m), in = t - grp * g.group_m * TN;
-      mt = mfirst + in % gsz;
-      nt = in / gsz;
-    }
-    m0_ = mt * TBM;
-    n0_ = nt * TBN;
-  };
-  // the staging cursor: shares go out in step order, so the tile coordinates advance once per
-  // tile instead of being divided out at every step (per-step integer divisions cost ~50 % of
-  // the main loop's time)
-  int sh_gs = 0, sh_ks = 0, sh_j = 0, sh_m0 = 0, sh_n0 = 0;
-  if (ntl > 0) tile_mn(0, sh_m0, sh_n0);
-  auto share_next = [&]() {
-    const int buf = sh_gs & (DNB - 1), k0 = sh_ks * DBK;
-    if (grpw == 0)
-      stage32<AKC, 4>(lds + (buf * 2 + 0) * DIMG, ra, i32x4{}, g.lda, sh_m0, g.M, k0, g.K, 0, 0, w4, lane);
-    else
-      stage32<BKC, 4>(lds + (buf * 2 + 1) * DIMG, rb, i32x4{}, g.ldb, sh_n0, g.N, k0, g.K, 0, 0, w4, lane);
-    ++sh_gs;
-    if (++sh_ks == nk) {
-      sh_ks = 0;
-      if (++sh_j < ntl) tile_mn(sh_j, sh_m0, sh_n0);
-    }
-  };
-  // tile j's bias rows into LDS slot j & 1 by LDS-DMA (wave 0 bias1, wave 1 bias2; absent biases
-  // and columns past N read as zero): no register result, so no compiler wait in the loop
-  auto load_bias = [&](int j, int n0_) {
-    if (wv >= 2) return;
-    const float* bp = wv == 0 ? g.bias1 : g.bias2;
-    const auto rbs = make_rsrc(bp, bp ? (unsigned)(g.N * 4) : 0u);
-    const int col = n0_ + 4 * lane;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rbs, (lds_ptr_t)(bias_lds + ((j & 1) * 2 + wv) * 256), 16,
-                                             col < g.N ? (unsigned)(col * 4) : OOB, 0, 0, 0);
-  };
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const unsigned long long dkey = drop_key(g.dseed);
-  const auto rcs = make_rsrc(g.C, OOB);  // C < 2 GB (host-checked): out-of-range rows dropped
-  auto epilogue = [&](int j, int m0_, int n0_) {  // tile j's accumulators -> C (32 stores, none waited for)
-    const float* bl = bias_lds + (j & 1) * 2 * 256;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int lc = wn * 64 + jj * 16 + 4 * (lane >> 4), col = n0_ + lc;
-      const f32x4 b = *reinterpret_cast<const f32x4*>(bl + lc) + *reinterpret_cast<const f32x4*>(bl + 256 + lc);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = m0_ + wm * 128 + i * 16 + (lane & 15);
-        const bool ok = row < g.M && col < g.N;
-        f32x4 v = acc[i][jj] + b;
-        if (g.epi == EPI_DROPOUT) {
-          const unsigned long long rq = drop_quad(dkey, (g.doff + (size_t)(ok ? row : 0) * g.ldc + col) >> 2);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] *= drop_elem_scale(rq, r, g.dkeep, g.dscale);
-        } else if (g.epi == EPI_LRELU) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r]);
-        }
-        const unsigned e = (unsigned)row * (unsigned)g.ldc + (unsigned)col;  // < 2^30 (host-checked)
-        if constexpr (C16 == 0) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rcs, ok ? e * 4u : OOB, 0, 0);
-        } else {
-          const u32x2 h = C16 == 2
-              ? u32x2{(unsigned)(unsigned short)f2bf(v[0]) | ((unsigned)(unsigned short)f2bf(v[1]) << 16),
-                      (unsigned)(unsigned short)f2bf(v[2]) | ((unsigned)(unsigned short)f2bf(v[3]) << 16)}
-              : f2h4(v);
-          __builtin_amdgcn_raw_buffer_store_b64(h, rcs, ok ? e * 2u : OOB, 0, 0);
-        }
-      }
-    }
-  };
-
-  int cj = 0, cm0 = sh_m0, cn0 = sh_n0;  // the tile being computed
-  if (total > 0 && ((g.abl & 16) || (g.stagger > 0 && ntl < (ntiles + G - 1) / G))) {
-    // start phases spread over 16 slots so the workgroups' epilogue store bursts do not all
-    // coincide: g.stagger ticks (10 ns) per slot, only on workgroups with one tile fewer than
-    // the most loaded (they have a tile of slack); timing probe (MLVAE_GEMM_ABL bit 16): every
-    // workgroup, ((abl >> 8) & 255) ticks per slot
-    const int per = (g.abl & 16) ? ((g.abl >> 8) & 255) : g.stagger;
-    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() +
-                                     (unsigned long long)((wg >> 3) & 15) * (unsigned long long)per;
-    while (__builtin_amdgcn_s_memrealtime() < t_end) __builtin_amdgcn_s_sleep(8);
-  }
-  if (total > 0) {
-    load_bias(0, cn0);
-    const int npre = min(3, total);
-    for (int it = 0; it < npre; ++it) share_next();
-    vm_wait(4 * (npre - 1));
-  }
-  __builtin_amdgcn_s_barrier();
-  if (grpw == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one slot behind
-  bf16x8 af[8], bfr[4];
-  int ks = 0;
-  for (int gs = 0; gs < total; ++gs) {
-    if (ks == 0 && gs > 0) {  // the previous tile is complete: its stores, this tile's bias rows
-      epilogue(cj, cm0, cn0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ++cj;
-      tile_mn(cj, cm0, cn0);
-      load_bias(cj, cn0);
-    }
-    {
-      const short* As = lds + ((gs & (DNB - 1)) * 2 + 0) * DIMG;
-      const short* Bs = lds + ((gs & (DNB - 1)) * 2 + 1) * DIMG;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag32<BKC>(Bs, wn * 64 + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = frag32<AKC>(As, wm * 128 + i * 16, lane);
-    }
-    if (gs + 3 < total) share_next();
-    if (gs + 1 < total) {
-      // the wave's vm operations issued after step gs+1's share: steps gs+2, gs+3 and the
-      // epilogue of slot gs-1 or gs (at most one of them: nk >= 4); 32 stores + at most one
-      // bias DMA, waited as 32 (one more op than needed on waves 0-1)
-      const bool ep = (ks == 0 && gs > 0) || (ks == 1 && gs > 1);
-      const bool a2 = gs + 2 < total, a3 = gs + 3 < total;
-      if (ep) {
-        if (a3) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-        else if (a2) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      } else {
-        if (a3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (a2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    if (++ks == nk) ks = 0;
-  }
-  if (grpw == 0) __builtin_amdgcn_s_barrier();  // both groups pass the same number of barriers
-  if (total > 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's last bias-row DMA ...
-    __builtin_amdgcn_s_barrier();                      // ... and every other wave's
-    epilogue(cj, cm0, cn0);
-  }
-}
 
 __global__ __launch_bounds__(256) void splitk_reduce_fast(GFArgs g) {
   const size_t MN = (size_t)g.M * g.N;
@@ -1037,29 +827,6 @@ int launch_fast_v(const GFArgs& g, dim3 grid, hipStream_t s) {
   }
   k<<<grid, 512, FAST_LDS, s>>>(g);
   return 0;
-}
-
-template <bool AKC, bool BKC, int C16>
-int launch_persist_c(const GFArgs& g, int grid, hipStream_t s) {
-  auto k = gemm256_persist_kernel<AKC, BKC, C16>;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)PERSIST_LDS) != hipSuccess) {
-      mlvae_set_error("gemm_bf16: cannot reserve %zu B LDS", PERSIST_LDS);
-      return 2;
-    }
-    attr = true;
-  }
-  k<<<grid, 512, PERSIST_LDS, s>>>(g);
-  return 0;
-}
-
-template <bool AKC, bool BKC>
-int launch_persist(const GFArgs& g, int grid, hipStream_t s) {
-  return g.c16 == 2 ? launch_persist_c<AKC, BKC, 2>(g, grid, s)
-       : g.c16 == 1 ? launch_persist_c<AKC, BKC, 1>(g, grid, s)
-                    : launch_persist_c<AKC, BKC, 0>(g, grid, s);
 }
 
 int gemm_cus() {
@@ -1216,7 +983,6 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     return e ? atoi(e) : 0;
   }();
   g.abl = abl;
-  g.stagger = 0;
   int s, kc;
   fast_plan(M, N, K, batch, &s, &kc);
   if (s > 1 && (N % 4 != 0 || !ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
@@ -1243,31 +1009,7 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
   // 1469 vs 1236), the same with register-double-buffered fragments (proj 1.38 vs 1.31 ms), the
   // staging pieces spread one per 8 MFMAs (+-1 %)
   const int var = gemm_variant();
-  // the persistent ping-pong loop (VAR 14, opt-in: MLVAE_GEMM_VAR=14; k-contiguous A, one batch,
-  // no split, no beta / aux / time shift, C < 2 GB).  Measured slower than the per-tile VAR 12 in
-  // the step (same box: c3 11.16 -> 11.35-11.48 ms/step, the projection 1.10 -> 1.25-1.26 ms;
-  // tools/gemm_kscan.py: 1.77 vs 1.59 us per 64-deep K-step, fixed per-tile cost 15.4 vs 12.3 us):
-  // the finished tile's stores cost the same overlapped as in the per-tile epilogue
-  const size_t esz = c16 ? 2 : 4;
-  const bool persist = var == 14 && akc && batch == 1 && s == 1 && beta == 0.f &&
-                       (epi == EPI_NONE || epi == EPI_DROPOUT || epi == EPI_LRELU) && !aux && kshift == 0 &&
-                       kshift_bstep == 0 && K >= 4 * DBK && N % 4 == 0 && ldc % 4 == 0 &&
-                       ((uintptr_t)C % (c16 ? 8 : 16)) == 0 && ((uintptr_t)bias1 % 16) == 0 &&
-                       ((uintptr_t)bias2 % 16) == 0 && ((size_t)(M - 1) * ldc + N) * esz < OOB &&
-                       ((size_t)(M - 1) * ldc + N) < (1u << 30);
-  if (persist) {
-    // start-phase stagger of the workgroups with a tile of slack: 1/16 of a tile per slot,
-    // a tile ~ K / 32 BK-32 steps of ~0.8 us = K / 32 x 80 ticks.  MLVAE_GEMM_STAGGER=0: off
-    static const int stag_on = [] {
-      const char* e = getenv("MLVAE_GEMM_STAGGER");
-      return e ? atoi(e) : 1;
-    }();
-    g.stagger = stag_on ? (K / DBK) * 80 / 16 : 0;
-    const int ntiles = grid.x;
-    int G = ntiles < gemm_cus() ? ntiles : gemm_cus();
-    if (G >= 8) G &= ~7;
-    rc = bkc ? launch_persist<true, true>(g, G, st) : launch_persist<true, false>(g, G, st);
-  } else if (akc && bkc) rc = launch_fast<true, true>(g, grid, st, var);
+  if (akc && bkc) rc = launch_fast<true, true>(g, grid, st, var);
   else if (akc) rc = launch_fast<true, false>(g, grid, st, var);
   else if (bkc) rc = launch_fast<false, true>(g, grid, st, var);
   else rc = launch_fast<false, false>(g, grid, st, var);
@@ -1340,7 +1082,7 @@ extern "C" int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, co
   g.bias1 = nullptr; g.bias2 = nullptr; g.epi = EPI_NONE; g.aux = nullptr; g.ldaux = 0;
   g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
   g.dseed = 0; g.doff = 0; g.dkeep = 1.f; g.dscale = 1.f;
-  g.ws = ws; g.alpha = alpha; g.abl = 0; g.stagger = 0;
+  g.ws = ws; g.alpha = alpha; g.abl = 0;
   g.splits = s; g.kchunk = kc;
   g.group_m = 1;
   g.c16 = 0;
@@ -1410,7 +1152,7 @@ extern "C" int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, co
   g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
   g.dseed = drop_seed; g.doff = drop_offset; g.dkeep = 1.f - drop_p;
   g.dscale = drop_p < 1.f ? 1.f / (1.f - drop_p) : 0.f;
-  g.ws = nullptr; g.alpha = alpha; g.abl = 0; g.stagger = 0;
+  g.ws = nullptr; g.alpha = alpha; g.abl = 0;
   g.splits = 1; g.kchunk = ((g.K + TBK - 1) / TBK) * TBK;
   if (g.K == 0) g.kchunk = TBK;
   static const int group_m = [] {

@@ -1235,27 +1235,6 @@ extern "C" int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, cons
   return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, y, xbuf, xbytes,
              err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
 }
-// fp8 mode forward with the recurrent product on e4m3 operands (F8R: where the wide kernels run
-// the asymmetric TPW-1 form -- per-GPU batches <= 128 -- elsewhere as mlvae_lstm_fwd_fp8's
-// bf16 recurrence); the e4m3 / bf16 dropout(h) outputs are optional here (the top layer).
-extern "C" int mlvae_lstm_fwd_fp8r(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
-                                   void* gates, float* cells, void* y_bf16, void* y_drop_bf16,
-                                   void* y_drop_fp8, float x8_scale, unsigned long long drop_seed,
-                                   unsigned long long drop_offset, float drop_p, void* xbuf,
-                                   size_t xbytes, int* err, void* stream) {
-  if (!use_wide(B, H, PREC_BF16) || (y_drop_fp8 && (!y_drop_bf16 || !(x8_scale > 0.f)))) {
-    mlvae_set_error("lstm_fwd_fp8r: wide-batch shapes; an e4m3 dropout output needs the bf16 one and a scale");
-    return 1;
-  }
-  WideExtra ex;
-  ex.ydb = static_cast<unsigned short*>(y_drop_bf16);
-  ex.seed = drop_seed; ex.off = drop_offset; ex.p = drop_p;
-  ex.f8.y8 = static_cast<unsigned char*>(y_drop_fp8);
-  ex.f8.x8scale = x8_scale;
-  ex.f8.rec8 = 1;
-  return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, nullptr,
-             xbuf, xbytes, err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
-}
 extern "C" int mlvae_lstm_bwd_fp8_ex(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                                      void* gates, const float* cells, const void* dy, int dy_bf16,
                                      void* dg_bf16, float* dbias_rows, void* dg_fp8,
@@ -1375,12 +1354,10 @@ extern "C" int mlvae_lstm_set_debug(void* buf) {
 // bit3 reserves 100 KB LDS per recurrence workgroup, bit4 polls with s_sleep 1 instead of 4,
 // bits 5-10 delay the first poll sweep of every step by that many s_sleep 1, bit 11 times the
 // batch-group kernels without their prefetch, bit 12 runs the wide-batch kernels at any batch,
-// bit 22 runs the wide forward as two interleaved chains per workgroup (lstm_fwd_il_kernel),
 // bit 23 stamps the forward pollers' publish acknowledgement, bit 24 makes the wide kernels
 // cycle through all NSLOT exchange slots instead of 2 (A/B: 2 slots keep the BPTT's partial
 // tiles in L2 -- PMC 5.34 -> 3.45 GB per launch at c3, 1.53 -> 1.46 ms standalone).
 extern "C" int mlvae_lstm_set_debug_mode(int mode) {
   g_dbg_mode = mode;
-  lstm_wide_set_mode(mode);
   return 0;
 }

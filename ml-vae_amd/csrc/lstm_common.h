@@ -49,7 +49,6 @@ struct LstmArgs {
   const float* g8scale;
   unsigned* g8amax;
   const unsigned short* dYb;  // wide BPTT, optional: dY as bf16 [B*T, 2H] instead of Y (fp32)
-  int rec8;                   // fp8 mode, wide forward at TPW 1: h W_hh on e4m3 operands (F8R)
   // wide forward, optional (ZP): the layer input z (bf16 [B*T rows, ldz], 32 wide) whose
   // projection z W_ih^T + b_ih + b_hh the kernel computes itself -- G then only receives the
   // activated gates (no 8H-wide fp16 projection written and read back)
@@ -211,7 +210,6 @@ struct WideFp8 {  // the fp8 mode's fused outputs of the wide kernels (LstmArgs 
   unsigned char* dg8 = nullptr;
   const float* g8scale = nullptr;
   unsigned* g8amax = nullptr;
-  int rec8 = 0;  // forward: h W_hh on e4m3 operands (F8R)
 };
 struct WideZ {  // the wide forward's fused layer-0 input projection (LstmArgs Zb ... bz)
   const unsigned short* zb = nullptr;
@@ -226,8 +224,6 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   unsigned long long dseed, unsigned long long doff, float dp,
                   unsigned long long* dbg, int dbg_mode, const WideFp8& f8 = WideFp8(),
                   const unsigned short* dyb = nullptr, const WideZ& wz = WideZ());
-// debug-mode bits the wide plans read (bit 21: one workgroup per CU, no two-per-CU plan)
-void lstm_wide_set_mode(int mode);
 // exchange bytes the wide kernels need at (B, H), or 0 when they do not apply
 size_t lstm_wide_xbytes(int B, int H, bool fwd);
 // the wide kernels address one batch group's rows through 32-bit buffer offsets: T bound

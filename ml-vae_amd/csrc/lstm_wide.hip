@@ -57,6 +57,15 @@ __device__ __forceinline__ void publish(__amdgpu_buffer_rsrc_t r, unsigned byte_
 // 16-byte slot of row `utt` in an XOR-swizzled LDS image (conflict-free B/A-fragment reads)
 __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15); }
 
+// f(integral_constant<int, I>) for I = 0 .. N-1 (compile-time indices: register arrays stay registers)
+template <int N, int I = 0, class Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
@@ -75,15 +84,11 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // c2 0.954 -> 0.863, c5 (B = 64) 0.979 -> 0.872, c4 3.95 -> 3.49 ms (profiles/ab/r04_as.txt);
 // the default at TPW 1, debug bit 8 restores equal shares.  At TPW 2 the pollers' 3 tiles
 // spilled 46 VGPRs.
-// F8R (fp8 mode, with AS at TPW 1): h W_hh on the block-scaled 16x16x128 e4m3 MFMA -- W_hh in
-// registers as e4m3 with one E8M0 scale per lane's 32-element k-block (half the VGPRs of bf16),
-// h converted to e4m3 at 2^8 (|h| < 1) as the pollers write it into the LDS image; a quarter of
-// the MFMAs at twice the cycles each.  The exchange stays bf16.
 // ZP: the layer-0 input projection fused (a.Zb): io wave 4 DMAs the step's 16 z rows (64 B each)
 // into the gx ring's space and each tile's gate inputs are one v_mfma_f32_16x16x32_bf16 of the
 // resident W_ih fragment (K = 32 = the latent width) onto the tile's b_ih + b_hh -- instead of
 // reading 8 KB of fp16 projection per utterance and step that a separate kernel wrote.
-template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool F8R = false, bool ZP = false>
+template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool ZP = false>
 __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
@@ -95,10 +100,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;
   constexpr int NC8 = 16 * HJ / 8;            // 8-unit chunks of h per step
   // k-chunks whose A-fragments live in LDS (VGPR budget; at TPW 1 one tile's 16 fit in registers)
-  constexpr int KLF = ((TPW == 1 && !AS) || F8R) ? 0 : FWD_KLF;
-  static_assert(!F8R || (AS && TPW == 1 && NKC % 4 == 0), "fp8 recurrence: the asymmetric TPW-1 form");
-  constexpr int K8 = NKC / 4;                 // F8R: 128-deep k-chunks
-  constexpr int ROW8 = H;                     // F8R: bytes of one e4m3 h-image row
+  constexpr int KLF = (TPW == 1 && !AS) ? 0 : FWD_KLF;
   constexpr int KR = NKC - KLF;               // ... and in registers
   constexpr int HB = 4;                       // B-fragments (h) read ahead per batch
   constexpr int NQ = 16 * 4 * HJ / 4;         // 16-byte quads of gx / gates per step
@@ -293,37 +295,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     constexpr int MT = IO ? TPI : TPP;         // this wave's tiles
     constexpr int MTA = MT > 0 ? MT : 1;       // (array extent)
     const int m0 = IO ? 4 * TPP + (wave - 4) * TPI : wave * TPP;
-    bf16x8 wreg[F8R ? 1 : MTA][F8R ? 1 : KR];
-    i32x8 w8[F8R ? MTA : 1][F8R ? K8 : 1];
-    int w8s[F8R ? MTA : 1][F8R ? K8 : 1];
-    if constexpr (F8R) {
-      // lane (row bi, k-block q): 32 consecutive k of each 128-deep chunk, scaled by 2^(8 - e)
-      // where max |w| of the block = m 2^e, m in [0.5, 1): |w 2^(8-e)| < 256 <= 448
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const int m = m0 + t;
-        const float* wrow = W + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * H;
-#pragma unroll
-        for (int kc = 0; kc < K8; ++kc) {
-          f32x4 v[8];
-          float am = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            v[e] = *reinterpret_cast<const f32x4*>(wrow + kc * 128 + 32 * q + 4 * e);
-            am = fmaxf(am, fmaxf(fmaxf(fabsf(v[e][0]), fabsf(v[e][1])), fmaxf(fabsf(v[e][2]), fabsf(v[e][3]))));
-          }
-          // am = m 2^ex, m in [0.5, 1) (normal am; a zero / denormal block gets scale 1)
-          const int ex = am >= 1.17549435e-38f ? (int)((__float_as_uint(am) >> 23) & 255u) - 126 : 8;
-          const float sc = __uint_as_float((unsigned)(127 + 8 - ex) << 23);  // 2^(8 - ex)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) w8[t][kc][e] = (int)pack4_fp8(v[e][0] * sc, v[e][1] * sc, v[e][2] * sc, v[e][3] * sc);
-          w8s[t][kc] = 127 + ex - 8;  // E8M0: the block's values are w8 x 2^(ex - 8)
-          __builtin_amdgcn_sched_barrier(0);  // (one chunk's 32 floats live at a time)
-        }
-      }
-    } else {
-      load_w(wreg, m0, MT);
-    }
+    bf16x8 wreg[MTA][KR];
+    load_w(wreg, m0, MT);
     // ZP: the tiles' W_ih fragments (row bi: gate bi & 3, unit 4 m + (bi >> 2); k = 8 q .. 8 q + 7)
     // and b_ih + b_hh in the accumulator layout (element g: gate g of unit 4 m + q)
     bf16x8 wz[ZP ? MTA : 1];
@@ -434,26 +407,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           }
           LSTAMP(1);
           RTS(8 + wave);
-          if constexpr (F8R) {
-            // e4m3 image [16 utt][H bytes]: 16-byte chunk c of row bi at slot c ^ bi; this lane's
-            // 8 units are half q & 1 of chunk 2 (wave PL + i) + q / 2
 #pragma unroll
-            for (int i = 0; i < PL; ++i) {
-              float f[8];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                f[2 * e] = __uint_as_float(hv[i][e] << 16) * 256.f;
-                f[2 * e + 1] = __uint_as_float(hv[i][e] & 0xffff0000u) * 256.f;
-              }
-              const int c8 = 2 * (wave * PL + i) + (q >> 1);
-              *reinterpret_cast<u32x2*>(hb + bi * ROW8 + ((c8 ^ bi) << 4) + 8 * (q & 1)) =
-                  u32x2{pack4_fp8(f[0], f[1], f[2], f[3]), pack4_fp8(f[4], f[5], f[6], f[7])};
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < PL; ++i)
-              *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
-          }
+          for (int i = 0; i < PL; ++i)
+            *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
         }
         LWSTAMP();
         __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
@@ -477,24 +433,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // (AS: the pollers, owning most tiles, go first)
         const bool first = AS ? !IO : IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
         if (first) __builtin_amdgcn_s_setprio(1);
-        if constexpr (F8R) {
-          // B-fragments: lane (utt bi, k-block q) reads 32 e4m3 of h at k = 128 kc + 32 q + j
-          i32x8 hf8[K8];
-#pragma unroll
-          for (int kc = 0; kc < K8; ++kc) {
-            const int c8 = 8 * kc + 2 * q;
-            const u32x4 lo = *reinterpret_cast<const u32x4*>(hb + bi * ROW8 + ((c8 ^ bi) << 4));
-            const u32x4 hi = *reinterpret_cast<const u32x4*>(hb + bi * ROW8 + (((c8 + 1) ^ bi) << 4));
-            hf8[kc] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int kc = 0; kc < K8; ++kc)
-#pragma unroll
-            for (int t = 0; t < MT; ++t)  // h at E8M0 119 = 2^-8
-              acc[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w8[t][kc], hf8[kc], acc[t], 0, 0, 0,
-                                                                        w8s[t][kc], 0, 119);
-        } else
 #pragma unroll
         for (int k0 = 0; k0 < NKC; k0 += HB) {
           bf16x8 hfrag[HB];
@@ -608,319 +546,28 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// forward, two chains per workgroup (interleaved)
-// ---------------------------------------------------------------------------------------
-// A workgroup owns the same HJ units of TWO batch groups (chains) of one direction and
-// alternates between them: while chain A's h_t travels to the other workgroups of its group,
-// the workgroup computes chain B's step, so the inter-CU hand-off overlaps MFMA work instead
-// of idling the CU.  The W_hh fragments (registers + LDS) serve both chains.  Sub-step (s, c):
-//   pollers (waves 0-3)  poll chain c's h_{t-1} into its LDS image          | barrier |
-//   every wave           MFMA over the image, cell update (chain c's state), publish h_t,
-//                        chain c's step-s outputs into its out ring
-//   loaders (waves 4-5)  after the barrier: LDS-DMA of chain c's gx(s+1); after publish: the
-//                        dropout keep bits of chain c's step s
-//   storers (waves 6-7)  after publish: the previous sub-step's outputs LDS -> HBM
-// Loaders issue a fixed number of DMAs per sub-step (padded rows read a clamped valid row), so
-// a counted vmcnt waits for chain c's gx without waiting for the other chain's; storers never
-// wait on their stores.  The number of batch groups is padded to even (a padded group runs on
-// zeros and stores nothing).
-template <int TPW, int NKC>
-__global__ __launch_bounds__(512, 2) void lstm_fwd_il_kernel(LstmArgs a) {
-  constexpr int HJ = WW * TPW * 4;
-  constexpr int H = NKC * 32;
-  constexpr int PL = NKC / 4;                 // poll loads (k-chunks) per lane, waves 0-3
-  constexpr int ROWB = H * 2;
-  constexpr int HIMG = 16 * ROWB;             // one chain's h image (single-buffered)
-  constexpr int GXU = 4 * HJ + 8;             // gx halfs per utterance: [gate][unit] + 16 B
-  constexpr int GXS = 16 * GXU;               // halfs per gx slot
-  constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;  // gates fp16 | c fp32 | h fp32 | 16 B
-  constexpr int NC8 = 16 * HJ / 8;
-  constexpr int KLF = 2;
-  constexpr int KR = NKC - KLF;
-  constexpr int UPL = 16 / 2;                 // utterances (DMAs) per loader wave and sub-step
-  static_assert(NC8 <= 128, "one keep-bit chunk per loader / storer thread");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* himg = smem;                                                         // [2 ch][HIMG]
-  unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2 ch][2 slot][GXS]
-  char* outr = reinterpret_cast<char*>(gxr + 4 * GXS);                      // [2 ch][16][OUB]
-  bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUB);            // [wave][TPW][KLF][lane]
-  unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);   // [2 ch][NC8]
-  __shared__ int abort_flag;
-
-  const int NBe = (a.NB + 1) & ~1, npair = NBe / 2;
-  const int ngroups = 2 * npair, gstride = (ngroups + 7) & ~7;
-  const int gid = blockIdx.x % gstride, js = blockIdx.x / gstride;
-  if (gid >= ngroups) return;
-  const int dir = gid / npair, pr = gid % npair;
-  const int T = a.T, j0 = js * HJ;
-  const int tid = threadIdx.x, lane = tid & 63;
-  // exchange slots in use: 2 (every member of a group is producer and consumer of every other,
-  // so a slot is rewritten only after all its readers have loaded it); bit 24: all NSLOT
-  const int nlg = (a.dbg_mode & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const float* W = dir ? a.W1 : a.W0;
-  const int bi = lane & 15, q = lane >> 4;
-
-  bf16x8 wreg[TPW][KR];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int m = wave * TPW + t;
-    const float* wrow = W + (size_t)((bi & 3) * H + j0 + 4 * m + (bi >> 2)) * H;
-#pragma unroll
-    for (int kc = 0; kc < NKC; ++kc) {
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q);
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(wrow + kc * 32 + 8 * q + 4);
-      bf16x8 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] = f2bf(w0[e]); v[4 + e] = f2bf(w1[e]); }
-      if (kc < KR) wreg[t][kc < KR ? kc : 0] = v;
-      else wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane] = v;
-    }
-  }
-  __shared__ int placement;
-  const bool same_xcd = group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement) &&
-                        !(a.dbg_mode & 32768);
-  if (tid == 0) abort_flag = 0;
-
-  const size_t xslot = (size_t)BG * H;
-  short* const xbase = reinterpret_cast<short*>(a.xbuf);
-  // chain c = batch group 2 pr + c of this direction: its own exchange (the wide layout)
-  auto xrc = [&](int c) {
-    return make_rsrc(xbase + (size_t)(dir * NBe + 2 * pr + c) * NSLOT * xslot,
-                     (unsigned)(NSLOT * xslot * sizeof(short)));
-  };
-  const auto xr0 = xrc(0), xr1 = xrc(1);
-
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
-  const int role = wave < 4 ? 0 : (wave < 6 ? 1 : 2);  // poller / loader / storer (uniform)
-  const int lw = wave - 4, sw = tid - 384;             // loader wave 0-1, storer thread 0-127
-  auto io_load = [&](int c, int s_) {  // chain c's gx of step s_ -> slot s_ & 1 (fixed DMA count)
-    const int sc = s_ < T ? s_ : T - 1;
-    const int t_ = dir ? T - 1 - sc : sc;
-#pragma unroll
-    for (int i = 0; i < UPL; ++i) {
-      const int u = lw * UPL + i;
-      const int b = min((2 * pr + c) * BG + u, a.B - 1);  // padded rows: a clamped valid row
-      const auto rs = make_rsrc(G16 + (size_t)b * T * 8 * H, (unsigned)((size_t)T * 8 * H * 2));
-      const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
-      const unsigned off = (unsigned)(((size_t)t_ * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
-      unsigned short* dst = gxr + (c * 2 + (s_ & 1)) * GXS + u * GXU;
-      if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
-    }
-  };
-  auto drop_bits = [&](int c, int s_, int c8) -> unsigned {
-    const int u = c8 / (HJ / 8), uu = (c8 % (HJ / 8)) * 8;
-    const int t_ = dir ? T - 1 - s_ : s_;
-    const size_t o = ((size_t)((2 * pr + c) * BG + u) * T + t_) * 2 * H + dir * H + j0 + uu;
-    const unsigned long long k = drop_key(a.dseed);
-    const unsigned long long r0 = drop_quad(k, (a.doff + o) >> 2), r1 = drop_quad(k, (a.doff + o + 4) >> 2);
-    unsigned bits = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      bits |= (drop_elem_scale(r0, e, a.dkeep, 1.f) != 0.f ? 1u : 0u) << e;
-      bits |= (drop_elem_scale(r1, e, a.dkeep, 1.f) != 0.f ? 1u : 0u) << (4 + e);
-    }
-    return bits;
-  };
-  auto io_store = [&](int c, int s_) {  // chain c's saved step-s_ activations (storer threads)
-    if (a.dbg_mode & 1) return;
-    const int t_ = dir ? T - 1 - s_ : s_;
-    const char* src = outr + c * 16 * OUB;
-    const int g0 = (2 * pr + c) * BG;
-    constexpr int NG8 = 16 * 4 * HJ / 8;
-    for (int ci = sw; ci < NG8; ci += 128) {
-      const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
-      const int u = row >> 2, g = row & 3, b = g0 + u;
-      if (b >= a.B) continue;
-      *reinterpret_cast<u32x4*>(G16 + ((size_t)b * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
-          *reinterpret_cast<const u32x4*>(src + u * OUB + (g * HJ + uu) * 2);
-    }
-    constexpr int NQ2 = 16 * HJ / 4;
-    for (int qi = sw; qi < NQ2; qi += 128) {
-      const int u = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4, b = g0 + u;
-      if (b >= a.B) continue;
-      const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
-      const float* cf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ);
-      *reinterpret_cast<f32x4*>(a.Cs + o) = *reinterpret_cast<const f32x4*>(cf + uu);
-      if (a.Y) *reinterpret_cast<f32x4*>(a.Y + o) = *reinterpret_cast<const f32x4*>(cf + HJ + uu);
-    }
-    if (sw < NC8) {  // h (bf16) and dropout(h) (bf16) of one 8-unit chunk per thread
-      const int u = sw / (HJ / 8), uu = (sw % (HJ / 8)) * 8, b = g0 + u;
-      if (b < a.B) {
-        const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
-        const size_t o = ((size_t)b * T + t_) * 2 * H + dir * H + j0 + uu;
-        if (a.Yb)
-          *reinterpret_cast<bf16x8*>(a.Yb + o) =
-              bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
-                     f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
-        if (a.Ydb) {
-          const unsigned bits = dbl[c * NC8 + sw];
-          f32x4 d0, d1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            d0[e] = (bits >> e) & 1 ? v0[e] * a.dscale : 0.f;
-            d1[e] = (bits >> (4 + e)) & 1 ? v1[e] * a.dscale : 0.f;
-          }
-          *reinterpret_cast<bf16x8*>(a.Ydb + o) =
-              bf16x8{f2bf(d0[0]), f2bf(d0[1]), f2bf(d0[2]), f2bf(d0[3]),
-                     f2bf(d1[0]), f2bf(d1[1]), f2bf(d1[2]), f2bf(d1[3])};
-        }
-      }
-    }
-  };
-
-  auto run = [&](auto role_tag) {
-    constexpr int ROLE = decltype(role_tag)::value;
-    if (ROLE == 1) {
-      io_load(0, 0); io_load(0, 1); io_load(1, 0); io_load(1, 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    float cst[2][TPW];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) cst[c][t] = 0.f;
-    int pend_c = -1, pend_s = 0;  // storers: the last completed sub-step not yet stored
-    bool aborted = false;
-    for (int s = 0; s < T && !aborted; ++s) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        // step 0 has no poll / barrier: one here orders chain 0's out ring before its store
-        if (s == 0 && c == 1) __syncthreads();
-        STAMP(c * 8 + 0);
-        char* hb = himg + c * HIMG;
-        const auto xr = c ? xr1 : xr0;
-        const bool valid = (2 * pr + c) * BG + bi < a.B;
-        f32x4 acc[TPW];
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        float gxv[TPW][4];
-        auto read_gx = [&]() {
-          const unsigned short* gx = gxr + (c * 2 + (s & 1)) * GXS + bi * GXU;
-#pragma unroll
-          for (int t = 0; t < TPW; ++t) {
-            const int u = 4 * (wave * TPW + t) + q;
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = h2f(gx[g4 * HJ + u]);
-          }
-        };
-        if (s == 0) read_gx();
-        if (s > 0) {
-          if (ROLE == 1) {
-            // chain c's gx(s) was issued two sub-steps ago; younger than it: this wave's TPW
-            // publishes of chain c, the other chain's UPL = 8 DMAs and (but at the last step)
-            // its TPW publishes -- at least 8 + TPW ops, so vmcnt(8 + TPW) covers gx(s)
-            if constexpr (TPW == 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-          } else if (ROLE == 0) {
-            const unsigned tag = step_tag_lg(s - 1, nlg);
-            const unsigned ebase = (unsigned)(((s - 1) & nmask) * xslot) + bi * H + wave * PL * 32 + 8 * q;
-            u32x4 hv[PL];
-            unsigned spins = 0;
-            while (true) {
-#pragma unroll
-              for (int i = 0; i < PL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * 32) * sizeof(short));
-              bool ok = true;
-#pragma unroll
-              for (int i = 0; i < PL; ++i) ok &= tags_ok(hv[i], tag, true, true);
-              if (__all(ok)) break;
-              if (++spins > SPIN_LIMIT) {
-                if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
-                break;
-              }
-              __builtin_amdgcn_s_sleep(2);
-            }
-            STAMP(c * 8 + 1);
-#pragma unroll
-            for (int i = 0; i < PL; ++i)
-              *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
-          }
-          __syncthreads();
-          STAMP(c * 8 + 2);
-          if (abort_flag) { aborted = true; break; }
-          if (ROLE == 1) io_load(c, s + 1);
-          read_gx();
-#pragma unroll
-          for (int kc = 0; kc < NKC; ++kc) {
-            const bf16x8 hfrag = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, kc * 4 + q) * 16);
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) {
-              const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
-                                        : wlds[((wave * TPW + t) * KLF + (kc - KR)) * 64 + lane];
-              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag, acc[t], 0, 0, 0);
-            }
-          }
-          STAMP(c * 8 + 3);
-        }
-        float hvals[TPW], gates[TPW][4];
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const float ig = sigmoid_fast(acc[t][0] + gxv[t][0]);
-          const float fg = sigmoid_fast(acc[t][1] + gxv[t][1]);
-          const float gg = tanh_fast(acc[t][2] + gxv[t][2]);
-          const float og = sigmoid_fast(acc[t][3] + gxv[t][3]);
-          cst[c][t] = valid ? fg * cst[c][t] + ig * gg : 0.f;
-          hvals[t] = valid ? og * tanh_fast(cst[c][t]) : 0.f;
-          gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
-        }
-        if (s + 1 < T) {
-          const unsigned tag = step_tag_lg(s, nlg);
-          const size_t row = (size_t)(s & nmask) * xslot + (size_t)bi * H + j0;
-#pragma unroll
-          for (int t = 0; t < TPW; ++t) {
-            const unsigned hu = __float_as_uint(hvals[t]);
-            const unsigned x1 = __builtin_amdgcn_permlane16_swap(hu, hu, false, false)[1];
-            const unsigned x2 = __builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1];
-            const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];
-            if (q == 0)
-              publish(xr, (unsigned)((row + 4 * (wave * TPW + t)) * sizeof(short)),
-                      pack_bf16(hvals[t], __uint_as_float(x1), __uint_as_float(x2), __uint_as_float(x3), tag),
-                      same_xcd);
-          }
-        }
-        STAMP(c * 8 + 4);
-        if (ROLE == 2 && pend_c >= 0) io_store(pend_c, pend_s);
-        char* ob = outr + c * 16 * OUB + bi * OUB;
-        unsigned short* og = reinterpret_cast<unsigned short*>(ob);
-        float* of = reinterpret_cast<float*>(ob + 8 * HJ);
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const int u = 4 * (wave * TPW + t) + q;
-          og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
-          og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
-          of[u] = cst[c][t]; of[HJ + u] = hvals[t];
-        }
-        if (ROLE == 1 && a.Ydb && (tid - 256) < NC8) dbl[c * NC8 + (tid - 256)] = drop_bits(c, s, tid - 256);
-        pend_c = c; pend_s = s;
-      }
-    }
-    __syncthreads();
-    if (ROLE == 2) io_store(pend_c, pend_s);
-    if (ROLE == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA left in flight at exit
-  };
-  if (role == 0) run(std::integral_constant<int, 0>{});
-  else if (role == 1) run(std::integral_constant<int, 1>{});
-  else run(std::integral_constant<int, 2>{});
-}
-
-// ---------------------------------------------------------------------------------------
 // backward (BPTT), reduce-scatter form
 // ---------------------------------------------------------------------------------------
 // F8: the fp8 mode's e4m3 dG copy + amax (a separate instantiation: the bf16 path's registers
 // stay as they are)
 // DYB: dY (the layer output's gradient) arrives as bf16 (a.dYb) instead of fp32 (a.Y): half the
 // bytes in the cell-input stream (and in the producers' epilogues)
-template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false, bool DBG = false>  // HJ = 32 * TPW, H = 32 * NKC
+// NB: no workgroup barrier in the step (round 5).  The MFMA's K (the 4 HJ gate rows of the
+// workgroup's units) is ordered so that k-chunk c (32 rows) holds gates i,f,g,o of units
+// 8c .. 8c+7 -- the cell-update output of WPC = 8 / KC waves.  A wave that has written its rows of
+// the A-image sets its LDS flag to s + 1; every wave multiplies the chunks whose waves have flagged,
+// as they become ready, so the MFMAs of the early waves' chunks overlap the slowest wave's poll
+// (r04 stamps: the barrier followed the reduce by 1,724 ticks of a 5,524-tick step at B = 256).
+// Debug bit 11: the pre-round-5 form (one __syncthreads per step, same k order).
+template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false, bool DBG = false, bool NB = true>  // HJ = 32 * TPW, H = 32 * NKC
 __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = 32 * TPW;
   constexpr int H = NKC * 32;
   constexpr int NJ = H / HJ;                  // workgroups per (dir, group) = producers = consumers
   constexpr int NTW = NKC / 4;                // N-tiles (16 units) per wave: 8 waves cover H
   constexpr int KC = 4 * HJ / 32;             // k-chunks of the own-dG operand (K = 4 HJ)
+  constexpr int WPC = WW / KC;                // waves whose cell outputs make one k-chunk
+  static_assert(WPC >= 1 && WPC * KC == WW && HJ / 8 == KC, "k-chunk c = units 8c .. 8c+7");
   // k-chunks whose B-fragments live in LDS (VGPR budget at TPW 2; TPW 1 keeps all of them in
   // registers).  The <2,16> build reloads ~11 spilled dwords once, in the prologue (not in the
   // step loop: checked in the ISA)
@@ -929,7 +576,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   // k-chunks per batch of fragment reads: all 4 at TPW 1 (c2 BPTT 0.999 -> 0.966 ms, c5 1.10 ->
   // 1.04); at TPW 2 one per batch, the compiler's own order (4: c3 1.230 -> 1.249 ms)
   constexpr int BKB = TPW == 1 ? 4 : 1;
-  constexpr bool BWL = false;                 // ... with the LDS B-fragments (VGPR budget at TPW 2)
   constexpr int ROWB = 4 * HJ * 2;            // bytes of one A-image row
   constexpr int AIMG = 16 * ROWB;
   constexpr int NPL = NJ / 8;                 // producers per lane in the reduce-scatter
@@ -951,6 +597,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int CUTT = CG_B + CF_B + CD_B;    // bytes per utterance
   char* cst = smem + 2 * AIMG + (size_t)8 * NTW * KLB * 64 * 16;  // [2][16][CUTT]
   __shared__ int abort_flag;
+  __shared__ __attribute__((aligned(16))) unsigned wflag[WW];  // NB: wave w's A-image rows (and staged cell inputs) of step s: s + 1
+  typedef __attribute__((address_space(3))) unsigned lds_u32;
+  typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+  lds_u32* const wflag_lds = (lds_u32*)(wflag);
 
   // group slots padded to a multiple of 8 (idle slots exit at once): members gid + k * gstride
   // then share one XCD under round-robin dispatch at every batch size (B = 32: 4 groups)
@@ -968,7 +618,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const int bi = lane & 15, q = lane >> 4;
 
   // resident B-fragments: tile nt -> global units n = (wave*NTW + nt)*16 + col;
-  // B[k][n] = W_hh[g*H + j0 + u][n], k = g*HJ + u
+  // B[k][n] = W_hh[g*H + j0 + u][n], k = 32 c + 8 g + e <-> gate g, unit u = 8 c + e
   bf16x8 wreg[NTW][KR];
   static_assert(KLB > 0 || KR == KC, "");
 #pragma unroll
@@ -979,8 +629,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       bf16x8 v;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int k = kc * 32 + 8 * q + e;
-        v[e] = f2bf(W[(size_t)((k / HJ) * H + j0 + (k % HJ)) * H + n]);
+        v[e] = f2bf(W[(size_t)(q * H + j0 + 8 * kc + e) * H + n]);  // gate q, unit 8 kc + e
       }
       if (kc < KR) wreg[nt][kc < KR ? kc : 0] = v;
       else wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane] = v;
@@ -990,6 +639,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * NJ, NJ, js, &placement) &&
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) abort_flag = 0;
+  if (tid < WW) wflag[tid] = 0;
   __syncthreads();
 
   // exchange: [slot][consumer][producer][HJ units][16 utterances] bf16
@@ -1217,54 +867,131 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
       cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
       bsum[ci][0] += d0; bsum[ci][1] += d1; bsum[ci][2] += d2; bsum[ci][3] += d3;
+      // k-chunk u / 8, gate g: A-image slot 4 (u / 8) + g, element u % 8 (k = 32 (u / 8) + 8 g + u % 8)
       const int u = uc[ci], r = cu[ci];
       const float dg[4] = {d0, d1, d2, d3};
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int k = g * HJ + u;
-        *reinterpret_cast<short*>(ab + r * ROWB + swz(r, k >> 3) * 16 + (k & 7) * 2) = f2bf(dg[g]);
-      }
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<short*>(ab + r * ROWB + swz(r, (u >> 3) * 4 + g) * 16 + (u & 7) * 2) = f2bf(dg[g]);
     }
-    __syncthreads();  // double-buffered A-image: one barrier per step
+    constexpr unsigned FULL = (1u << KC) - 1;
+    // NB: chunks whose WPC waves have all flagged step s (LDS flags, one broadcast read)
+    // (through an LDS-typed pointer: a volatile generic one compiled to flat sc0 sc1 accesses
+    // with an s_waitcnt vmcnt(0) behind every flag -- an HBM round trip per step -- and flat
+    // stores are not ordered with the ds_write of the A-image rows; the asm memory clobbers keep
+    // the plain loads in the spin loop and the store behind the rows)
+    auto ready_mask = [&]() -> unsigned {
+      asm volatile("" ::: "memory");
+      const u32x4 f0 = *reinterpret_cast<const lds_u32x4*>(wflag_lds);
+      const u32x4 f1 = *reinterpret_cast<const lds_u32x4*>(wflag_lds + 4);
+      const unsigned f[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
+      unsigned m = 0;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        bool ok = true;
+#pragma unroll
+        for (int w = 0; w < WPC; ++w) ok &= __builtin_amdgcn_readfirstlane(f[c * WPC + w]) > (unsigned)s;
+        m |= ok ? 1u << c : 0u;
+      }
+      asm volatile("" ::: "memory");  // the flag read precedes the A-image reads it licenses
+      return m;
+    };
+    const bool nb = NB && !(a.dbg_mode & 2048);
+    if (nb) {
+      // this wave's A-image rows (and its stage_cell(s + 1) writes, issued earlier) are in the
+      // LDS queue ahead of the flag: LDS processes one wave's accesses in order
+      asm volatile("" ::: "memory");
+      if (lane == 0) wflag_lds[wave] = (unsigned)s + 1u;
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();  // double-buffered A-image: one barrier per step
+    }
     if (late_pf) load_cell(s + 2);
     LSTAMP(3);
     if (abort_flag) return false;
+    // wait (NB) until the chunks not yet in `done` are ready, in snapshots
+    unsigned done = 0;
+    auto wait_ready = [&]() -> unsigned {
+      unsigned spins = 0;
+      while (true) {
+        const unsigned m = ready_mask() & ~done;
+        if (m) return m;
+        if (abort_flag) return 0;
+        if (++spins > SPIN_LIMIT) {
+          if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
+          return 0;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
     if (s + 1 < T) {
       f32x4 acc[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // The A-fragments (and, with BWL, the batch's LDS-resident B-fragments) of a batch of BKB
-      // k-chunks are read before its MFMAs: left to itself the compiler issued each read one
-      // k-chunk ahead and waited for it (5 exposed LDS round trips per step at TPW 1)
+      auto wfrag = [&](int nt, int kc) -> bf16x8 {
+        return kc < KR ? wreg[nt][kc < KR ? kc : 0] : wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
+      };
+      // NB, debug bit 22: a fixed per-wave order (own chunk first, then the next ones cyclically),
+      // each chunk waited for in turn -- the accumulation order, and so every bit of the result,
+      // is the same in every run (the dynamic order below rounds the partial sums in whatever
+      // order the chunks became ready)
+      if (nb && (a.dbg_mode & (1 << 22))) {
+        bool failed = false;
+        static_for<KC>([&](auto R) {
+          if (wave / WPC != decltype(R)::value) return;
+          static_for<KC>([&](auto I) {
+            constexpr int kc = (decltype(R)::value + decltype(I)::value) % KC;
+            while (!failed && !(done & (1u << kc))) {
+              const unsigned m = wait_ready();
+              if (!m) failed = true;
+              done |= m;
+            }
+            if (failed) return;
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, kc * 4 + q) * 16);
 #pragma unroll
-      for (int k0 = 0; k0 < KC; k0 += BKB) {
+            for (int nt = 0; nt < NTW; ++nt)
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wfrag(nt, kc), acc[nt], 0, 0, 0);
+          });
+        });
+        if (failed) return false;
+        done = FULL;
+      }
+      // NB: the chunks ready so far, one at a time, while any is still outstanding
+      while (nb && done != FULL) {
+        const unsigned m = wait_ready();
+        if (!m) return false;
+        if ((m | done) == FULL) break;  // everything left is ready: the batched loop below
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc)
+          if (m & (1u << kc)) {  // (wave-uniform)
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, kc * 4 + q) * 16);
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt)
+              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wfrag(nt, kc), acc[nt], 0, 0, 0);
+          }
+        done |= m;
+      }
+      // The A-fragments of a batch of BKB k-chunks are read before its MFMAs: left to itself the
+      // compiler issued each read one k-chunk ahead and waited for it (5 exposed LDS round trips
+      // per step at TPW 1).  (NB: only the chunks not done above -- all ready now.)
+#pragma unroll
+      for (int k0 = 0; k0 < KC && done != FULL; k0 += BKB) {
         bf16x8 afr[BKB];
-        bf16x8 wl[BWL ? NTW : 1][BWL ? BKB : 1];
 #pragma unroll
         for (int i = 0; i < BKB; ++i)
-          afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
-        if constexpr (BWL) {
-#pragma unroll
-          for (int i = 0; i < BKB; ++i)
-            if (k0 + i >= KR)
-#pragma unroll
-              for (int nt = 0; nt < NTW; ++nt)
-                wl[nt][i] = wlds[((wave * NTW + nt) * KLB + (k0 + i - KR)) * 64 + lane];
-        }
+          if (!(done & (1u << (k0 + i))))
+            afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
         __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
 #pragma unroll
         for (int i = 0; i < BKB; ++i) {
           const int kc = k0 + i;
+          if (done & (1u << kc)) continue;
 #pragma unroll
-          for (int nt = 0; nt < NTW; ++nt) {
-            bf16x8 wf;
-            if (kc < KR) wf = wreg[nt][kc < KR ? kc : 0];
-            else if constexpr (BWL) wf = wl[nt][i];
-            else wf = wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wf, acc[nt], 0, 0, 0);
-          }
+          for (int nt = 0; nt < NTW; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wfrag(nt, kc), acc[nt], 0, 0, 0);
         }
       }
+      done = FULL;
       const unsigned tag = step_tag_lg(s, nlg);
       const size_t sb = (size_t)(s & nmask) * xslot;
 #pragma unroll
@@ -1279,16 +1006,25 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     }
     LSTAMP(4);
     // dG of this step for the weight-gradient GEMMs: 16-byte rows out of the A-image
-    // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|)
+    // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|).  A wave's 64
+    // slots are 8 consecutive 16-byte slots (one gate, 64 units: whole 128-byte lines) of each of
+    // its utterance rows.  Every chunk is ready (NB: the MFMA loop waited for all of them; the
+    // last step, which has no MFMAs, waits here).
+    while (nb && done != FULL) {
+      const unsigned m = wait_ready();
+      if (!m) return false;
+      done |= m;
+    }
     if (!(a.dbg_mode & 1)) {
       constexpr int NSL = 16 * 4 * HJ / 8;  // 16-byte slots
       const int t = dir ? s : T - 1 - s;
       for (int sl = tid; sl < NSL; sl += 512) {
-        const int r = sl / (4 * HJ / 8), kslot = sl % (4 * HJ / 8);
+        // row r, slot j = g (HJ / 8) + c: gate g, units 8 c .. 8 c + 7 (A-image slot 4 c + g)
+        const int r = sl / (4 * HJ / 8), j = sl % (4 * HJ / 8);
+        const int g = j / (HJ / 8), c = j % (HJ / 8), kslot = 4 * c + g, u = 8 * c;
         const int b = grp * BG + r;
-        if (b >= a.B) continue;
-        const int k = kslot * 8, g = k / HJ, u = k % HJ;
         const u32x4 v = *reinterpret_cast<const u32x4*>(ab + r * ROWB + swz(r, kslot) * 16);
+        if (b < a.B) {
         const size_t o = ((size_t)b * T + t) * 8 * H + dir * 4 * H + g * H + j0 + u;
         *reinterpret_cast<u32x4*>(a.dGb + o) = v;  // G is fp16 here: dG always goes to dGb
         if constexpr (F8) {
@@ -1304,6 +1040,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
             *reinterpret_cast<u32x2*>(a.dG8 + o) =
                 u32x2{pack4_fp8(f[0] * g8s, f[1] * g8s, f[2] * g8s, f[3] * g8s),
                       pack4_fp8(f[4] * g8s, f[5] * g8s, f[6] * g8s, f[7] * g8s)};
+        }
         }
       }
     }
@@ -1349,15 +1086,7 @@ struct WidePlan {
   int tpw, nkc, NB, NJ, HJ;
   size_t lds, xbytes, xtab_off;
   bool ok;
-  bool il;  // forward: two chains (batch groups) per workgroup, lstm_fwd_il_kernel
 };
-
-// Interleaved forward (lstm_fwd_il_kernel): MLVAE_WIDE_IL=0/1 (default off until measured),
-// MLVAE_IL_TPW=1/2 its units per workgroup (HJ = 32 / 64)
-int il_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 int wide_cus() {
   int dev = 0, cus = 256;
@@ -1378,38 +1107,16 @@ size_t wide_lds(int H, int hj, bool fwd) {
          (size_t)2 * 16 * ((4 * hj * 2 + 16) + 2 * (hj * 4 + 32));  // + staged cell inputs
 }
 
-int g_wide_mode = 0;  // lstm_wide_set_mode (debug bits; none read by the plans at present)
-
 WidePlan wide_plan(int B, int H, bool fwd) {
   WidePlan p{};
   p.ok = false;
-  p.il = false;
   if (H != 512) return p;  // the decoder's H (c2-c5); other H run the batch-group kernels
   p.nkc = H / 32;
   p.NB = (B + BG - 1) / BG;
-  static const int il = il_env("MLVAE_WIDE_IL", 0), il_tpw = il_env("MLVAE_IL_TPW", 2) == 1 ? 1 : 2;
-  if (fwd && (il || (g_wide_mode & (1 << 22)))) {
-    const int npair = (p.NB + 1) / 2, NBe = 2 * npair;
-    for (int tpw = il_tpw; tpw >= 1; --tpw) {
-      const int hj = 32 * tpw, nj = H / hj;
-      if (2 * npair * nj > wide_cus()) continue;
-      p.tpw = tpw; p.HJ = hj; p.NJ = nj; p.ok = true; p.il = true;
-      const int gxs = 16 * (4 * hj + 8);
-      p.lds = (size_t)2 * 16 * H * 2 + (size_t)4 * gxs * 2 + (size_t)2 * 16 * (4 * hj * 2 + 2 * hj * 4 + 16) +
-              (size_t)8 * tpw * 2 * 64 * 16 + (size_t)2 * (16 * hj / 8) * 4;
-      if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;
-      p.xbytes = (size_t)2 * NBe * NSLOT * BG * H * 2;
-      p.xtab_off = p.xbytes;
-      p.xbytes += (size_t)2 * NBe * p.NJ * sizeof(unsigned);
-      return p;
-    }
-  }
   const int cus = wide_cus();
-  static const int tpw0 = [] {  // MLVAE_WIDE_TPW=2: start at HJ = 64 units per workgroup (A/B)
-    const char* e = getenv("MLVAE_WIDE_TPW");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  for (int tpw = tpw0; tpw <= 2; ++tpw) {
+  // HJ = 32 units per workgroup where the grid fits the chip (it beat HJ = 64 at every shard,
+  // round 2: 7.94 vs 8.02, 5.58 vs 6.34, 4.72 vs 5.68 ms/step); HJ = 64 at B = 256
+  for (int tpw = 1; tpw <= 2; ++tpw) {
     if (fwd && tpw * p.nkc * 4 > 128) break;   // resident A-fragments <= 128 VGPRs
     const int hj = 32 * tpw, nj = H / hj;
     if (!fwd && (nj < 8 || nj % 8)) continue;   // reduce-scatter: NJ multiple of 8
@@ -1438,13 +1145,11 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   // train step's form (bf16 dY, no fp8 copy)
   const bool dbg = a.dbg != nullptr;
   const bool as = TPW == 1 && !(a.dbg_mode & (1 << 8));   // the asymmetric split; bit 8: equal shares
-  const bool f8r = as && a.rec8 && !dbg;    // fp8 mode: e4m3 h W_hh (the asymmetric TPW-1 form only)
-  const bool zp = a.Zb != nullptr;          // fused layer-0 projection (checked: no DBG / F8R with it)
+  const bool zp = a.Zb != nullptr;          // fused layer-0 projection (checked: no DBG with it)
   auto k = fwd ? (dbg ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, true>)
-                      : (f8r ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, TPW == 1>
-                             : zp ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, false, true>
-                                        : lstm_fwd_wide_kernel<TPW, NKC, OCC, false, false, false, true>)
-                             : as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
+                      : (zp ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, true>
+                                  : lstm_fwd_wide_kernel<TPW, NKC, OCC, false, false, true>)
+                            : as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? (dbg ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true, true>
@@ -1460,22 +1165,7 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   return 0;
 }
 
-template <int TPW, int NKC>
-int launch_il(const LstmArgs& a, const WidePlan& p, hipStream_t s) {
-  auto k = lstm_fwd_il_kernel<TPW, NKC>;
-  if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess) {
-    mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
-    return 2;
-  }
-  const int npair = (p.NB + 1) / 2;
-  k<<<dim3(((2 * npair + 7) & ~7) * p.NJ), 512, p.lds, s>>>(a);
-  MLVAE_CHECK_LAUNCH();
-  return 0;
-}
-
 }  // namespace
-
-void lstm_wide_set_mode(int mode) { g_wide_mode = mode; }
 
 bool lstm_wide_t_ok(int T, int H) {
   return (size_t)BG * T * 8 * H * 2 <= 0xffffffffull && (size_t)BG * T * 2 * H * 4 <= 0xffffffffull;
@@ -1484,7 +1174,7 @@ bool lstm_wide_t_ok(int T, int H) {
 int lstm_wide_workgroups(int B, int H, bool fwd) {
   WidePlan p = wide_plan(B, H, fwd);
   if (!p.ok) return 0;
-  return p.il ? ((p.NB + 1) / 2) * 2 * p.NJ : 2 * p.NB * p.NJ;
+  return 2 * p.NB * p.NJ;
 }
 
 size_t lstm_wide_xbytes(int B, int H, bool fwd) {
@@ -1517,20 +1207,19 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
   a.dbg = dbg; a.dbg_mode = dbg_mode; a.xcd_local = 0; a.Yb = yb; a.dGb = dgb;
   a.dbias = dbias; a.Ydb = ydb; a.dseed = dseed; a.doff = doff; a.dkeep = 1.f - dp;
   a.Y8 = f8.y8; a.x8scale = f8.x8scale; a.dG8 = f8.dg8; a.g8scale = f8.g8scale; a.g8amax = f8.g8amax;
-  a.rec8 = f8.rec8;
   a.dYb = fwd ? nullptr : dyb;
   if (wz.zb) {
-    if (!fwd || p.il || dbg || f8.rec8 || !wz.w0 || !wz.w1 || !wz.b[0] || !wz.b[1] || !wz.b[2] || !wz.b[3] ||
+    if (!fwd || dbg || !wz.w0 || !wz.w1 || !wz.b[0] || !wz.b[1] || !wz.b[2] || !wz.b[3] ||
         wz.ldz < 32 || wz.ldz % 8 || ((uintptr_t)wz.zb % 16)) {
-      mlvae_set_error("lstm_wide: the fused z projection needs the plain forward (no stamps / fp8 recurrence), "
+      mlvae_set_error("lstm_wide: the fused z projection needs the plain forward (no stamps), "
                       "both W_ih and all four biases, a 16-byte aligned z with ldz >= 32, ldz %% 8 == 0");
       return 1;
     }
     a.Zb = wz.zb; a.ldz = wz.ldz; a.Wz0 = wz.w0; a.Wz1 = wz.w1;
     for (int i = 0; i < 4; ++i) a.bz[i] = wz.b[i];
   }
-  if (a.Y8 && (!ydb || p.il)) {
-    mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one (one-group forward)");
+  if (a.Y8 && !ydb) {
+    mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one");
     return 1;
   }
   if (a.dG8 && (!a.g8scale || !a.g8amax)) {
@@ -1544,6 +1233,5 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
     mlvae_set_error("lstm_wide: memset failed");
     return 2;
   }
-  if (p.il) return p.tpw == 2 ? launch_il<2, 16>(a, p, st) : launch_il<1, 16>(a, p, st);
   return p.tpw == 2 ? launch_wide<2, 16, 2>(fwd, a, p, st) : launch_wide<1, 16, 2>(fwd, a, p, st);
 }

@@ -50,9 +50,7 @@ _SIGS = {
     "mlvae_conv1d_fwd": [I, I, I, I, I, P, I, P, P, I, P, I, P],
     "mlvae_conv1d_dgrad": [I, I, I, I, I, P, I, P, P, I, P, I, P],
     "mlvae_conv1d_wgrad_workspace_size": [I, I, I, I, I],
-    "mlvae_conv1d_bwd2_workspace_size": [I, I, I, I, I],
     "mlvae_conv1d_wgrad": [I, I, I, I, I, P, I, P, I, P, P, P, SZ, P],
-    "mlvae_conv1d_bwd2": [I, I, I, I, I, P, I, P, P, I, P, I, P, I, P, P, P, SZ, P],
     "mlvae_boundary_fwd": [SZ, P, P, P, P, U64, U64, P, P, P, P],
     "mlvae_boundary_bwd": [SZ, P, P, P, P, U64, U64, P, P, P, P, P, P],
     "mlvae_lstm1_fwd": [I, I, I, I, P, P, P, P, P, P, SZ, P, P],
@@ -110,7 +108,6 @@ _SIGS = {
     "mlvae_lstm_set_debug": [P],
     "mlvae_lstm_set_debug_mode": [I],
     "mlvae_lstm_fwd_fp8": [I, I, I, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
-    "mlvae_lstm_fwd_fp8r": [I, I, I, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_fwd_z": [I, I, I, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_bwd_fp8": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_fp8_ex": [I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, SZ, P, P],
@@ -126,7 +123,6 @@ _SIGS = {
 _RESTYPE = {
     "mlvae_last_error": C.c_char_p,
     "mlvae_conv1d_wgrad_workspace_size": SZ,
-    "mlvae_conv1d_bwd2_workspace_size": SZ,
     "mlvae_skinny_dzw_workspace_size": SZ,
     "mlvae_fp8_scale_workspace_size": SZ,
     "mlvae_gemm_fp8_tn_workspace_size": SZ,

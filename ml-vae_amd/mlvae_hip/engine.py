@@ -353,15 +353,12 @@ class VAEEngine:
         self.wih_t = {}
         # bf16 mode: the heads run as one fused kernel (heads.hip) when the shape is supported
         self.fused_heads = (cfg.prec == "bf16" and bool(lib().mlvae_heads_supported(cfg.C, cfg.F, 2 * cfg.H)))
-        # fused heads: in-kernel bias sums + bf16 saved intermediates (MLVAE_HEADS_BSUM=0: the
-        # colsum passes over fp32 intermediates, for same-box A/B)
-        self.heads_bias_sums = os.environ.get("MLVAE_HEADS_BSUM", "1") != "0"
+        # fused heads: in-kernel bias sums + bf16 saved intermediates (False: the colsum passes
+        # over fp32 intermediates; same box 12.30 -> 12.17 ms/step with them)
+        self.heads_bias_sums = True
         # dY (the layer outputs' gradients) in bf16 where its producers can write it: the heads'
-        # split form and the bf16 dgrad, into the wide-batch BPTT (mlvae_lstm_bwd_ex3 /
-        # _fp8_ex); the fp8 dgrad's epilogue writes fp32, so that layer's dY stays fp32.
-        # MLVAE_DY_BF16=0: fp32 everywhere (A/B)
-        self.dy_bf16 = (cfg.prec == "bf16" and os.environ.get("MLVAE_DY_BF16", "1") != "0"
-                        and os.environ.get("MLVAE_HEADS_FUSED", "0") in ("", "0"))
+        # split form and the bf16 dgrad, into the wide-batch BPTT (mlvae_lstm_bwd_ex3 / _fp8_ex)
+        self.dy_bf16 = cfg.prec == "bf16"
         self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
                      if self.fused_heads else None)
         # bf16 mode: the encoder (+ reparameterisation + KL) runs as two fused kernels
@@ -382,12 +379,8 @@ class VAEEngine:
                 self.g8 = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
                 self.g8_amax = {li: torch.zeros(2, device=self.device, dtype=torch.int32) for li in range(1, cfg.L)}
                 # the fp8 weight gradient dW_ih = dG^T X (e4m3 dG and layer input): alpha =
-                # 1 / (q_dG * x-scale); MLVAE_FP8_WGRAD=0 keeps it in bf16 (A/B)
-                self.fp8_wgrad = os.environ.get("MLVAE_FP8_WGRAD", "1") != "0"
-                # ... and, opt-in (MLVAE_FP8_REC=1), the forward recurrence's h W_hh on e4m3
-                # operands (mlvae_lstm_fwd_fp8r): measured slower at the c5 shard (same box: forward
-                # 0.893 -> 0.936 ms per launch, step 4.94 -> 5.05 ms), so off by default
-                self.fp8_rec = os.environ.get("MLVAE_FP8_REC", "0") == "1"
+                # 1 / (q_dG * x-scale) (False: bf16)
+                self.fp8_wgrad = True
                 self.x8s = torch.tensor([x8_scale(cfg.dropout)], device=self.device)
                 self.g8w = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
                 self.g8_ready = False  # a previous step's amax exists (the first step's dgrad is bf16)
@@ -403,32 +396,22 @@ class VAEEngine:
         self._T = 0
         self._pool = _Pool(self.device)
         # weight-gradient GEMMs on a side stream, unless the recurrences fill the chip
-        # (_full_chip; env MLVAE_OVERLAP=0/1 forces the choice for A/B runs)
-        env = os.environ.get("MLVAE_OVERLAP")
-        self._env_overlap = None if env is None else env != "0"
+        # (_full_chip; force_overlap True / False overrides the choice)
+        self.force_overlap = None
         self.overlap = True
         # split-K workgroup targets of the weight-gradient GEMMs (mlvae_gemm_bf16): those that
-        # overlap a recurrence / those in the step's tail (env overrides for A/B sweeps)
-        self.split_overlap = int(os.environ.get("MLVAE_SPLIT_OVERLAP", "128"))
-        self.split_tail = int(os.environ.get("MLVAE_SPLIT_TAIL", "160"))
-        # layer-0 input projection (K = latent width) on skinny_proj instead of the 256² GEMM
-        self.skinny_proj = os.environ.get("MLVAE_PROJ0", "skinny") == "skinny"
-        # ... or fused into the layer-0 forward recurrence (mlvae_lstm_fwd_z: the 8H-wide fp16
-        # projection is never written; MLVAE_ZPROJ=0: the skinny kernel + mlvae_lstm_fwd_ex2, A/B)
-        self.zproj = os.environ.get("MLVAE_ZPROJ", "1") != "0"
-        # Conv1d encoder: the layer-2 input gradient and layer-1 weight gradient as one pass
-        # (mlvae_conv1d_bwd2), opt-in MLVAE_CONV_BWD2=1: it reads 38 % fewer bytes but standalone
-        # at configs[3] takes 65.7 us against the two kernels' 62.5 (one workgroup per CU runs
-        # the dgrad and weight-gradient phases back to back; profiles/ab/r04_conv_standalone.txt)
-        self.conv_bwd2 = os.environ.get("MLVAE_CONV_BWD2", "0") == "1"
-        # full-chip steps, opt-in (MLVAE_TAIL_OVERLAP=1): the tail after the last BPTT overlaps its
-        # weight gradient -- measured slower at c3, 10.26 -> 10.39 ms/step: the 160-CU GEMM holds
-        # the encoder backward off the chip (0.105 -> 0.279 ms), profiles/ab/r04_tail_overlap.txt
-        self.tail_overlap = os.environ.get("MLVAE_TAIL_OVERLAP", "0") == "1"
-        # layer 0's dZ and dW_ih_l0 from one pass over dG (MLVAE_DZW=0: the NT + TN pair, A/B)
-        self.dzw = os.environ.get("MLVAE_DZW", "1") != "0"
-        # wide recurrence writes dropout(h) itself (MLVAE_FUSE_DROP=0: separate dropout pass, A/B)
-        self._fuse_drop = os.environ.get("MLVAE_FUSE_DROP", "1") != "0"
+        # overlap a recurrence / those in the step's tail
+        self.split_overlap = 128
+        self.split_tail = 160
+        # layer-0 input projection (K = latent width) fused into the layer-0 forward recurrence
+        # (mlvae_lstm_fwd_z: the 8H-wide fp16 projection is never written); where that form does
+        # not apply, on the skinny projection kernel (skinny_proj False: the 256² GEMM)
+        self.zproj = True
+        self.skinny_proj = True
+        # layer 0's dZ and dW_ih_l0 from one pass over dG (False: the NT + TN pair)
+        self.dzw = True
+        # the wide recurrence writes dropout(h) itself (False: a separate dropout pass)
+        self._fuse_drop = True
         self.side_stream = torch.cuda.Stream(self.device)
         # the step's critical path (recurrences, dgrads) runs on a high-priority stream so the
         # dispatcher prefers its workgroups over the side stream's weight-gradient GEMMs
@@ -737,7 +720,7 @@ class VAEEngine:
             w.layer_in.append((xin, xin_bf, din, ldx))
             # layer 0 on the 32-wide latent: the projection inside the recurrence (below)
             zproj = bool(li == 0 and self.zproj and w.bf and w.g16 and din == 32 and ldx % 8 == 0 and
-                         xin_bf is not None and not (cfg.fp8 and self.fp8_rec))
+                         xin_bf is not None)
             if zproj:
                 pass
             elif w.bf and din <= 32 and din % 8 == 0 and self.skinny_proj:
@@ -793,9 +776,6 @@ class VAEEngine:
                         and 2 * H % 16 == 0)
             x8_ptr = w.X8[li + 1].data_ptr() if x8_fused else None
             w.__dict__.setdefault("x8_fused", {})[li + 1] = x8_fused
-            # fp8 mode, opt-in: the recurrent product h W_hh^T on e4m3 operands too
-            # (mlvae_lstm_fwd_fp8r; the wide kernels' per-GPU-batch <= 128 form)
-            rec8 = bool(cfg.fp8 and w.g16 and not need_y and self.fp8_rec)
             with self._timed("lstm_fwd"):
                 if zproj:
                     rp = lambda n: self._ptr(f"decoder.rnn.{n}")
@@ -809,14 +789,6 @@ class VAEEngine:
                                              x8_scale(cfg.dropout) if x8_fused else 0.0, seed, self._drop_off,
                                              cfg.dropout if fuse_drop else 0.0, _p(w.xbuf), w.xbuf.numel(),
                                              _p(self.err), s), "lstm_fwd_z")
-                elif rec8:
-                    check(l.mlvae_lstm_fwd_fp8r(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
-                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                                _p(w.Cs[li]), _pb(w.Yb[li]),
-                                                _pb(w.Ydb[li]) if fuse_drop else None,
-                                                x8_ptr, x8_scale(cfg.dropout),
-                                                seed, self._drop_off, cfg.dropout if fuse_drop else 0.0,
-                                                _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd_fp8r")
                 elif x8_fused:
                     check(l.mlvae_lstm_fwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
@@ -942,8 +914,8 @@ class VAEEngine:
         """True when this batch's BPTT launch fills (>= 3/4 of) the chip: a side-stream GEMM
         would then only hold CUs the recurrence's co-resident workgroups wait for (measured at
         B = 256: 17.7 ms/step overlapped vs 15.3 serialised with whole-chip split-K plans)."""
-        if self._env_overlap is not None:
-            return not self._env_overlap
+        if self.force_overlap is not None:
+            return not self.force_overlap
         wgs = lib().mlvae_lstm_launch_workgroups(B, self.cfg.H, PREC[self.cfg.prec], 0)
         return wgs >= 0.75 * _lib.device_cus()
 
@@ -1132,13 +1104,6 @@ class VAEEngine:
             # this GEMM).  Below the bottom layer nothing waits on the dgrad: its weight
             # gradients, the step's longest tail, go first.
             if li == 0:
-                if full and self.tail_overlap and self._env_overlap is None:
-                    # The last BPTT is queued: nothing in the step's tail waits on co-resident
-                    # recurrence workgroups any more, so dW_hh_l0 goes to the side stream on
-                    # 160 CUs beside the dZ / encoder backward / dW_ih_l0 chain (as below a full
-                    # chip) instead of ahead of it (opt-in, measured slower: see __init__)
-                    self.overlap = True
-                    split_tail = self.split_tail
                 self._defer_side(pending, wgl)
             dx = w.dZs if li == 0 else w.dY[li - 1]
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
@@ -1248,15 +1213,9 @@ class VAEEngine:
                       "conv1d_wgrad")
             self._side(lambda: wgc(E, w.dE2, _p(w.E1), 2, w.conv_ws[1]))
             with self._timed("conv_bwd"):
-                if self.conv_bwd2:
-                    # layer-2 input gradient -> layer-1 weight gradient through LDS (dE1 never written)
-                    check(l.mlvae_conv1d_bwd2(B, T, Fd, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1), E,
-                                              _p(w.x), Fd, None, 0, gp(f"{ep}.0.weight"), gp(f"{ep}.0.bias"),
-                                              _p(w.conv_ws[0]), w.conv_ws[0].numel() * 4, s), "conv1d_bwd2")
-                else:
-                    check(l.mlvae_conv1d_dgrad(B, T, E, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1),
-                                               E, _p(w.dE1), E, s), "conv1d_dgrad")
-                    wgc(Fd, w.dE1, _p(w.x), 0, w.conv_ws[0])
+                check(l.mlvae_conv1d_dgrad(B, T, E, E, K, _p(w.dE2), E, self._ptr(f"{ep}.2.weight"), _p(w.E1),
+                                           E, _p(w.dE1), E, s), "conv1d_dgrad")
+                wgc(Fd, w.dE1, _p(w.x), 0, w.conv_ws[0])
             self._join_side()
             return
 

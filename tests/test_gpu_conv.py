@@ -84,38 +84,6 @@ def test_conv1d_weight_gradient(B, T, Cin, Cout, K):
     assert torch.equal(dw, dw2)
 
 
-@pytest.mark.parametrize("B,T,F,E,K", [(3, 70, 80, 64, 5), (2, 130, 48, 32, 3), (2, 5, 16, 16, 9), (1, 2000, 80, 64, 5)])
-def test_conv1d_fused_backward_matches_two_kernels(B, T, F, E, K):
-    """mlvae_conv1d_bwd2 (layer-2 input gradient feeding the layer-1 weight gradient through LDS)
-    against mlvae_conv1d_dgrad + mlvae_conv1d_wgrad on the same inputs: the same products in the
-    same order, so dE1 and dW1 are bit-identical; db1 sums the same fp32 values in another order."""
-    need_gpu()
-    torch.manual_seed(B * 5 + T + F)
-    dy = torch.randn(B, T, E).cuda()
-    w = (torch.randn(E, E, K) / (E * K) ** 0.5).cuda()
-    aux = torch.randn(B, T, E).cuda()
-    x = torch.randn(B, T, F).cuda()
-    dx_ref = torch.empty(B, T, E, device="cuda")
-    check(lib().mlvae_conv1d_dgrad(B, T, E, E, K, P(dy), E, P(w), P(aux), E, P(dx_ref), E, stream()))
-    nb = lib().mlvae_conv1d_wgrad_workspace_size(B, T, F, E, K)
-    assert lib().mlvae_conv1d_bwd2_workspace_size(B, T, F, E, K) == nb
-    ws = torch.empty(nb // 4 + 1, device="cuda")
-    dw_ref, db_ref = torch.empty(E, F, K, device="cuda"), torch.empty(E, device="cuda")
-    check(lib().mlvae_conv1d_wgrad(B, T, F, E, K, P(dx_ref), E, P(x), F, P(dw_ref), P(db_ref), P(ws), nb, stream()))
-    dx, dw, db = torch.empty_like(dx_ref), torch.full_like(dw_ref, float("nan")), torch.empty_like(db_ref)
-    check(lib().mlvae_conv1d_bwd2(B, T, F, E, K, P(dy), E, P(w), P(aux), E, P(x), F, P(dx), E, P(dw), P(db),
-                                  P(ws), nb, stream()))
-    dw2, db2 = torch.empty_like(dw_ref), torch.empty_like(db_ref)
-    check(lib().mlvae_conv1d_bwd2(B, T, F, E, K, P(dy), E, P(w), P(aux), E, P(x), F, None, 0, P(dw2), P(db2),
-                                  P(ws), nb, stream()))
-    torch.cuda.synchronize()
-    assert torch.equal(dx, dx_ref)
-    assert torch.equal(dw, dw_ref) and torch.equal(dw2, dw)
-    assert torch.equal(db2, db) and norm_rel(db, db_ref) < 1e-5
-    assert lib().mlvae_conv1d_bwd2(B, T, F, E, K, P(dy), E, P(w), P(aux), E, P(x), F, None, 0, P(dw2), P(db2),
-                                   P(ws), nb - 4, stream()) != 0
-
-
 def _encoder_bf16_operands(p, x, eps):
     """oracle.vae_cpu.encoder_forward in fp64 with every matrix-product operand rounded to bf16
     as the kernels round them (activations, weights; biases and the reparameterisation stay

@@ -1,7 +1,6 @@
 """Standalone timing of the Conv1d encoder's backward kernels at configs[3] (B=64, T=2000, F=80,
 E=64, K=5), outside the train step (where they share the chip with the side-stream weight-gradient
-GEMMs): the fused pass (mlvae_conv1d_bwd2) against mlvae_conv1d_dgrad + mlvae_conv1d_wgrad, and the
-forward layers.  Algorithmic HBM bytes as bench.py (fp32 activations).
+GEMMs): mlvae_conv1d_dgrad + mlvae_conv1d_wgrad and the forward layers.  Algorithmic HBM bytes as bench.py (fp32 activations).
 usage: python tools/conv_bench.py [iters]"""
 import os
 import sys
@@ -48,10 +47,6 @@ def main():
     ws = torch.empty(nb // 4 + 1, device="cuda")
     y1 = torch.empty(N, E, device="cuda")
 
-    def fused():
-        check(l.mlvae_conv1d_bwd2(B, T, F, E, K, P(de2), E, P(w2), P(e1), E, P(x), F, None, 0, P(dw1), P(db1),
-                                  P(ws), nb, s))
-
     def two():
         check(l.mlvae_conv1d_dgrad(B, T, E, E, K, P(de2), E, P(w2), P(e1), E, P(de1), E, s))
         check(l.mlvae_conv1d_wgrad(B, T, F, E, K, P(de1), E, P(x), F, P(dw1), P(db1), P(ws), nb, s))
@@ -59,8 +54,7 @@ def main():
     def fwd1():
         check(l.mlvae_conv1d_fwd(B, T, F, E, K, P(x), F, P(w1), P(b1), 1, P(y1), E, s))
 
-    for name, fn, nbytes in (("conv backward fused (bwd2)", fused, N * 4 * (2 * E + F)),
-                             ("conv backward dgrad + wgrad", two, N * 4 * (4 * E + F)),
+    for name, fn, nbytes in (("conv backward dgrad + wgrad", two, N * 4 * (4 * E + F)),
                              ("conv forward layer 1", fwd1, N * 4 * (F + E))):
         ms = timed(fn, iters)
         gbs = nbytes / (ms * 1e-3) / 1e9
