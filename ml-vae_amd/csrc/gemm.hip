@@ -121,6 +121,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     for (int j = 0; j < NB; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+  // fp32 parity mode: two-level accumulation over long K (the weight gradients sum over B*T
+  // frames).  The MFMA chain runs over KBLK = 256 of K, then folds into `tot`: a sequential fp32
+  // chain of kc / 2 accumulations (kc = 10,667 at B = 256) rounds ~sqrt(kc / 256) times worse
+  // than the fp32 oracle's blocked sums (round 5, fp64-anchored whole-step test: dW_ih_l1 3.5x
+  // the oracle's error at B = 32 before, tests/test_gpu_trajectory.py)
+  constexpr int KBLK = 256;
+  f32x16 tot[PREC == PREC_F32 ? MB : 1][PREC == PREC_F32 ? NB : 1];
+  if constexpr (PREC == PREC_F32) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) tot[i][j][v] = 0.f;
+  }
 
   // K-contiguous operand: float4 chunks along k (NC per thread).
   // M-contiguous operand (stored [K][rows]): 4k x 4r blocks, transposed in registers so the
@@ -201,6 +216,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
             for (int j = 0; j < NB; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][e], b4[j][e], acc[i][j], 0, 0, 0);
       }
+      if ((k0 - kbeg + BK) % KBLK == 0 || k0 + BK >= kend) {  // fold the block (uniform)
+#pragma unroll
+        for (int i = 0; i < MB; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) { tot[i][j][v] += acc[i][j][v]; acc[i][j][v] = 0.f; }
+      }
     } else {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 16) {
@@ -221,6 +244,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
+  if constexpr (PREC == PREC_F32) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = tot[i][j];
+  }
   // epilogue: C/D layout col = lane&31, row = (v&3) + 8*(v>>2) + 4*(lane>>5)
   const bool split = g.splits > 1;
   float* wsz = split ? g.ws + (size_t)blockIdx.z * g.M * g.N : nullptr;

@@ -57,15 +57,6 @@ __device__ __forceinline__ void publish(__amdgpu_buffer_rsrc_t r, unsigned byte_
 // 16-byte slot of row `utt` in an XOR-swizzled LDS image (conflict-free B/A-fragment reads)
 __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15); }
 
-// f(integral_constant<int, I>) for I = 0 .. N-1 (compile-time indices: register arrays stay registers)
-template <int N, int I = 0, class Fn>
-__device__ __forceinline__ void static_for(Fn&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<N, I + 1>(f);
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
@@ -552,22 +543,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
 // stay as they are)
 // DYB: dY (the layer output's gradient) arrives as bf16 (a.dYb) instead of fp32 (a.Y): half the
 // bytes in the cell-input stream (and in the producers' epilogues)
-// NB: no workgroup barrier in the step (round 5).  The MFMA's K (the 4 HJ gate rows of the
-// workgroup's units) is ordered so that k-chunk c (32 rows) holds gates i,f,g,o of units
-// 8c .. 8c+7 -- the cell-update output of WPC = 8 / KC waves.  A wave that has written its rows of
-// the A-image sets its LDS flag to s + 1; every wave multiplies the chunks whose waves have flagged,
-// as they become ready, so the MFMAs of the early waves' chunks overlap the slowest wave's poll
-// (r04 stamps: the barrier followed the reduce by 1,724 ticks of a 5,524-tick step at B = 256).
-// Debug bit 11: the pre-round-5 form (one __syncthreads per step, same k order).
-template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false, bool DBG = false, bool NB = true>  // HJ = 32 * TPW, H = 32 * NKC
+template <int TPW, int NKC, int OCC, bool F8 = false, bool DYB = false, bool DBG = false>  // HJ = 32 * TPW, H = 32 * NKC
 __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int HJ = 32 * TPW;
   constexpr int H = NKC * 32;
   constexpr int NJ = H / HJ;                  // workgroups per (dir, group) = producers = consumers
   constexpr int NTW = NKC / 4;                // N-tiles (16 units) per wave: 8 waves cover H
   constexpr int KC = 4 * HJ / 32;             // k-chunks of the own-dG operand (K = 4 HJ)
-  constexpr int WPC = WW / KC;                // waves whose cell outputs make one k-chunk
-  static_assert(WPC >= 1 && WPC * KC == WW && HJ / 8 == KC, "k-chunk c = units 8c .. 8c+7");
   // k-chunks whose B-fragments live in LDS (VGPR budget at TPW 2; TPW 1 keeps all of them in
   // registers).  The <2,16> build reloads ~11 spilled dwords once, in the prologue (not in the
   // step loop: checked in the ISA)
@@ -597,10 +579,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   constexpr int CUTT = CG_B + CF_B + CD_B;    // bytes per utterance
   char* cst = smem + 2 * AIMG + (size_t)8 * NTW * KLB * 64 * 16;  // [2][16][CUTT]
   __shared__ int abort_flag;
-  __shared__ __attribute__((aligned(16))) unsigned wflag[WW];  // NB: wave w's A-image rows (and staged cell inputs) of step s: s + 1
-  typedef __attribute__((address_space(3))) unsigned lds_u32;
-  typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-  lds_u32* const wflag_lds = (lds_u32*)(wflag);
 
   // group slots padded to a multiple of 8 (idle slots exit at once): members gid + k * gstride
   // then share one XCD under round-robin dispatch at every batch size (B = 32: 4 groups)
@@ -618,7 +596,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const int bi = lane & 15, q = lane >> 4;
 
   // resident B-fragments: tile nt -> global units n = (wave*NTW + nt)*16 + col;
-  // B[k][n] = W_hh[g*H + j0 + u][n], k = 32 c + 8 g + e <-> gate g, unit u = 8 c + e
+  // B[k][n] = W_hh[g*H + j0 + u][n], k = g*HJ + u
   bf16x8 wreg[NTW][KR];
   static_assert(KLB > 0 || KR == KC, "");
 #pragma unroll
@@ -629,7 +607,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       bf16x8 v;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        v[e] = f2bf(W[(size_t)(q * H + j0 + 8 * kc + e) * H + n]);  // gate q, unit 8 kc + e
+        const int k = kc * 32 + 8 * q + e;
+        v[e] = f2bf(W[(size_t)((k / HJ) * H + j0 + (k % HJ)) * H + n]);
       }
       if (kc < KR) wreg[nt][kc < KR ? kc : 0] = v;
       else wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane] = v;
@@ -639,7 +618,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * NJ, NJ, js, &placement) &&
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) abort_flag = 0;
-  if (tid < WW) wflag[tid] = 0;
   __syncthreads();
 
   // exchange: [slot][consumer][producer][HJ units][16 utterances] bf16
@@ -867,131 +845,44 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
       cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
       bsum[ci][0] += d0; bsum[ci][1] += d1; bsum[ci][2] += d2; bsum[ci][3] += d3;
-      // k-chunk u / 8, gate g: A-image slot 4 (u / 8) + g, element u % 8 (k = 32 (u / 8) + 8 g + u % 8)
       const int u = uc[ci], r = cu[ci];
       const float dg[4] = {d0, d1, d2, d3};
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<short*>(ab + r * ROWB + swz(r, (u >> 3) * 4 + g) * 16 + (u & 7) * 2) = f2bf(dg[g]);
-    }
-    constexpr unsigned FULL = (1u << KC) - 1;
-    // NB: chunks whose WPC waves have all flagged step s (LDS flags, one broadcast read)
-    // (through an LDS-typed pointer: a volatile generic one compiled to flat sc0 sc1 accesses
-    // with an s_waitcnt vmcnt(0) behind every flag -- an HBM round trip per step -- and flat
-    // stores are not ordered with the ds_write of the A-image rows; the asm memory clobbers keep
-    // the plain loads in the spin loop and the store behind the rows)
-    auto ready_mask = [&]() -> unsigned {
-      asm volatile("" ::: "memory");
-      const u32x4 f0 = *reinterpret_cast<const lds_u32x4*>(wflag_lds);
-      const u32x4 f1 = *reinterpret_cast<const lds_u32x4*>(wflag_lds + 4);
-      const unsigned f[8] = {f0[0], f0[1], f0[2], f0[3], f1[0], f1[1], f1[2], f1[3]};
-      unsigned m = 0;
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        bool ok = true;
-#pragma unroll
-        for (int w = 0; w < WPC; ++w) ok &= __builtin_amdgcn_readfirstlane(f[c * WPC + w]) > (unsigned)s;
-        m |= ok ? 1u << c : 0u;
+      for (int g = 0; g < 4; ++g) {
+        const int k = g * HJ + u;
+        *reinterpret_cast<short*>(ab + r * ROWB + swz(r, k >> 3) * 16 + (k & 7) * 2) = f2bf(dg[g]);
       }
-      asm volatile("" ::: "memory");  // the flag read precedes the A-image reads it licenses
-      return m;
-    };
-    const bool nb = NB && !(a.dbg_mode & 2048);
-    if (nb) {
-      // this wave's A-image rows (and its stage_cell(s + 1) writes, issued earlier) are in the
-      // LDS queue ahead of the flag: LDS processes one wave's accesses in order
-      asm volatile("" ::: "memory");
-      if (lane == 0) wflag_lds[wave] = (unsigned)s + 1u;
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();  // double-buffered A-image: one barrier per step
     }
+    __syncthreads();  // double-buffered A-image: one barrier per step
     if (late_pf) load_cell(s + 2);
     LSTAMP(3);
     if (abort_flag) return false;
-    // wait (NB) until the chunks not yet in `done` are ready, in snapshots
-    unsigned done = 0;
-    auto wait_ready = [&]() -> unsigned {
-      unsigned spins = 0;
-      while (true) {
-        const unsigned m = ready_mask() & ~done;
-        if (m) return m;
-        if (abort_flag) return 0;
-        if (++spins > SPIN_LIMIT) {
-          if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
-          return 0;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    };
     if (s + 1 < T) {
       f32x4 acc[NTW];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      auto wfrag = [&](int nt, int kc) -> bf16x8 {
-        return kc < KR ? wreg[nt][kc < KR ? kc : 0] : wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
-      };
-      // NB, debug bit 22: a fixed per-wave order (own chunk first, then the next ones cyclically),
-      // each chunk waited for in turn -- the accumulation order, and so every bit of the result,
-      // is the same in every run (the dynamic order below rounds the partial sums in whatever
-      // order the chunks became ready)
-      if (nb && (a.dbg_mode & (1 << 22))) {
-        bool failed = false;
-        static_for<KC>([&](auto R) {
-          if (wave / WPC != decltype(R)::value) return;
-          static_for<KC>([&](auto I) {
-            constexpr int kc = (decltype(R)::value + decltype(I)::value) % KC;
-            while (!failed && !(done & (1u << kc))) {
-              const unsigned m = wait_ready();
-              if (!m) failed = true;
-              done |= m;
-            }
-            if (failed) return;
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, kc * 4 + q) * 16);
-#pragma unroll
-            for (int nt = 0; nt < NTW; ++nt)
-              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wfrag(nt, kc), acc[nt], 0, 0, 0);
-          });
-        });
-        if (failed) return false;
-        done = FULL;
-      }
-      // NB: the chunks ready so far, one at a time, while any is still outstanding
-      while (nb && done != FULL) {
-        const unsigned m = wait_ready();
-        if (!m) return false;
-        if ((m | done) == FULL) break;  // everything left is ready: the batched loop below
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc)
-          if (m & (1u << kc)) {  // (wave-uniform)
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, kc * 4 + q) * 16);
-#pragma unroll
-            for (int nt = 0; nt < NTW; ++nt)
-              acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wfrag(nt, kc), acc[nt], 0, 0, 0);
-          }
-        done |= m;
-      }
       // The A-fragments of a batch of BKB k-chunks are read before its MFMAs: left to itself the
       // compiler issued each read one k-chunk ahead and waited for it (5 exposed LDS round trips
-      // per step at TPW 1).  (NB: only the chunks not done above -- all ready now.)
+      // per step at TPW 1).  (Round 5, measured and dropped: per-wave LDS flags instead of this
+      // barrier, each wave multiplying the k-chunks whose cell outputs were ready -- BPTT 1.36 ->
+      // 1.72 ms per launch at c3, 0.97 -> 1.19 at c2; profiles/r05_bptt_flags_stamps.txt)
 #pragma unroll
-      for (int k0 = 0; k0 < KC && done != FULL; k0 += BKB) {
+      for (int k0 = 0; k0 < KC; k0 += BKB) {
         bf16x8 afr[BKB];
 #pragma unroll
         for (int i = 0; i < BKB; ++i)
-          if (!(done & (1u << (k0 + i))))
-            afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
+          afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
         __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
 #pragma unroll
         for (int i = 0; i < BKB; ++i) {
           const int kc = k0 + i;
-          if (done & (1u << kc)) continue;
 #pragma unroll
-          for (int nt = 0; nt < NTW; ++nt)
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wfrag(nt, kc), acc[nt], 0, 0, 0);
+          for (int nt = 0; nt < NTW; ++nt) {
+            const bf16x8 wf = kc < KR ? wreg[nt][kc < KR ? kc : 0] : wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wf, acc[nt], 0, 0, 0);
+          }
         }
       }
-      done = FULL;
       const unsigned tag = step_tag_lg(s, nlg);
       const size_t sb = (size_t)(s & nmask) * xslot;
 #pragma unroll
@@ -1006,25 +897,16 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     }
     LSTAMP(4);
     // dG of this step for the weight-gradient GEMMs: 16-byte rows out of the A-image
-    // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|).  A wave's 64
-    // slots are 8 consecutive 16-byte slots (one gate, 64 units: whole 128-byte lines) of each of
-    // its utterance rows.  Every chunk is ready (NB: the MFMA loop waited for all of them; the
-    // last step, which has no MFMAs, waits here).
-    while (nb && done != FULL) {
-      const unsigned m = wait_ready();
-      if (!m) return false;
-      done |= m;
-    }
+    // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|)
     if (!(a.dbg_mode & 1)) {
       constexpr int NSL = 16 * 4 * HJ / 8;  // 16-byte slots
       const int t = dir ? s : T - 1 - s;
       for (int sl = tid; sl < NSL; sl += 512) {
-        // row r, slot j = g (HJ / 8) + c: gate g, units 8 c .. 8 c + 7 (A-image slot 4 c + g)
-        const int r = sl / (4 * HJ / 8), j = sl % (4 * HJ / 8);
-        const int g = j / (HJ / 8), c = j % (HJ / 8), kslot = 4 * c + g, u = 8 * c;
+        const int r = sl / (4 * HJ / 8), kslot = sl % (4 * HJ / 8);
         const int b = grp * BG + r;
+        if (b >= a.B) continue;
+        const int k = kslot * 8, g = k / HJ, u = k % HJ;
         const u32x4 v = *reinterpret_cast<const u32x4*>(ab + r * ROWB + swz(r, kslot) * 16);
-        if (b < a.B) {
         const size_t o = ((size_t)b * T + t) * 8 * H + dir * 4 * H + g * H + j0 + u;
         *reinterpret_cast<u32x4*>(a.dGb + o) = v;  // G is fp16 here: dG always goes to dGb
         if constexpr (F8) {
@@ -1040,7 +922,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
             *reinterpret_cast<u32x2*>(a.dG8 + o) =
                 u32x2{pack4_fp8(f[0] * g8s, f[1] * g8s, f[2] * g8s, f[3] * g8s),
                       pack4_fp8(f[4] * g8s, f[5] * g8s, f[6] * g8s, f[7] * g8s)};
-        }
         }
       }
     }

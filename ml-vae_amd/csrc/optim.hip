@@ -165,7 +165,13 @@ __global__ __launch_bounds__(256) void colsum_partial(int N, int C, const void* 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (c < C) {
     if (vec && c + 3 < C) {
-      for (int r = r0 + rl; r < r1; r += 16) acc += load4<BF>(in, (size_t)r * ld + c);
+      // two-level: blocks of 16 rows per thread (256 rows of the chunk) folded into acc
+      for (int rb = r0 + rl; rb < r1; rb += 256) {
+        f32x4 blk = {0.f, 0.f, 0.f, 0.f};
+        const int re = min(r1, rb + 256);
+        for (int r = rb; r < re; r += 16) blk += load4<BF>(in, (size_t)r * ld + c);
+        acc += blk;
+      }
     } else {
       for (int r = r0 + rl; r < r1; r += 16)
         for (int e = 0; e < 4; ++e)
@@ -188,9 +194,15 @@ __global__ __launch_bounds__(256) void colsum_final(int C, int R, const float* _
                                                     float beta) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
+  // two-level fixed-order sum (blocks of 16 chunks): a 256-long sequential chain rounded ~4x worse
+  // than the fp32 oracle's pairwise sums (round 5, fp64-anchored parity test)
   float s = 0.f;
-#pragma unroll 8
-  for (int r = 0; r < R; ++r) s += part[(size_t)r * C + c];
+  for (int r0 = 0; r0 < R; r0 += 16) {
+    float b = 0.f;
+    const int r1 = min(R, r0 + 16);
+    for (int r = r0; r < r1; ++r) b += part[(size_t)r * C + c];
+    s += b;
+  }
   out[c] = beta != 0.f ? beta * out[c] + s : s;
   if (out2) out2[c] = out[c];
 }

@@ -656,16 +656,23 @@ class VAEEngine:
         N, E, Z, H, C, Fd = w.N, cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
         X = _p(x)
+        prep_ev = None
         if self.flat_bf is not None:  # this step's weights as bf16 GEMM operands
             check(l.mlvae_cast_bf16(self.layout.total, _p(self.flat), _pb(self.flat_bf), s), "cast_bf16")
-            if train and self.w1_t is not None:
-                check(l.mlvae_cast_bf16_t(2 * cfg.C, 2 * cfg.H, self._ptr("decoder.mean_fc.blocks.0.weight"),
-                                          _pb(self.w1_t), s), "cast_bf16_t")
-            if train:
-                for li, dst in self.wih_t.items():
-                    check(l.mlvae_cast_bf16_t(8 * cfg.H, cfg.Z if li == 0 else 2 * cfg.H,
-                                              self._ptr(f"decoder.rnn.weight_ih_l{li}"), _pb(dst), s),
-                          "cast_bf16_t")
+            # the transposed / fp8 weight copies the layer-1 projection, the heads and the backward
+            # read: beside the encoder and the layer-0 forward recurrence on the side stream when
+            # that recurrence leaves CUs free (off the critical path), else in line
+            if not self._full_chip(B):
+                self._on_side = True
+                self.side_stream.wait_event(self._mark())
+                try:
+                    self._weight_prep(train)
+                finally:
+                    self._on_side = False
+                prep_ev = torch.cuda.Event()
+                prep_ev.record(self.side_stream)
+            else:
+                self._weight_prep(train)
         wb = self._wb
         count = None
         if self.world > 1:
@@ -717,6 +724,9 @@ class VAEEngine:
         xin, xin_bf, din, ldx = w.Zs, (w.Zb if w.bf else None), Z, w.ZA
         w.layer_in = []
         for li in range(cfg.L):
+            if li == 1 and prep_ev is not None:  # the layer-1 weight copies (side stream) are done
+                torch.cuda.current_stream(self.device).wait_event(prep_ev)
+                prep_ev = None
             w.layer_in.append((xin, xin_bf, din, ldx))
             # layer 0 on the 32-wide latent: the projection inside the recurrence (below)
             zproj = bool(li == 0 and self.zproj and w.bf and w.g16 and din == 32 and ldx % 8 == 0 and
@@ -735,14 +745,7 @@ class VAEEngine:
                 # W_ih: 448 / max|W_ih|), block-scaled MFMA, alpha = 1 / (2^8 q_w) (fp8.hip)
                 xs = x8_scale(cfg.dropout)
                 with self._timed(f"proj_l{li}"):
-                    wih = self._ptr(f"decoder.rnn.weight_ih_l{li}")
-                    check(l.mlvae_fp8_scale(8 * H * din, wih, xs, _p(self.w8s[li]), _p(self.f8ws),
-                                            self.f8ws.numel() * 4, s), "fp8_scale")
-                    check(l.mlvae_cast_fp8(8 * H * din, wih, 0, _p(self.w8s[li]), 0.0, self.w8[li].data_ptr(), s),
-                          "cast_fp8")
-                    if train and li in self.wih_t:  # the fp8 dgrad's W_ih^T, same scale
-                        check(l.mlvae_cast_fp8(8 * H * din, _pb(self.wih_t[li]), 1, _p(self.w8s[li]), 0.0,
-                                               self.w8t[li].data_ptr(), s), "cast_fp8")
+                    # (W_ih's e4m3 copies and scale: _weight_prep)
                     if not w.__dict__.get("x8_fused", {}).get(li):  # else the recurrence wrote it
                         check(l.mlvae_cast_fp8(N * din, _pb(xin_bf), 1, None, xs, w.X8[li].data_ptr(), s), "cast_fp8")
                     check(l.mlvae_gemm_fp8(N, 8 * H, din, w.X8[li].data_ptr(), din, self.w8[li].data_ptr(), din,
@@ -810,6 +813,8 @@ class VAEEngine:
                     w.__dict__.setdefault("_drop_seed", {})[li] = (seed, None)
                 else:
                     self._dropout(w, li, w.Y[li], xin, dropout_masks)
+        if prep_ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(prep_ev)
         w.rnn_out = w.Y[cfg.L - 1]
         w.rnn_out_bf = w.Yb[cfg.L - 1] if w.bf else None
         # ---- heads (ref:src/modules/decoder.py:24-25, FCBlock ref:src/modules/fc_block.py:9-16)
@@ -872,6 +877,30 @@ class VAEEngine:
         check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.pr), w.nr, _p(lens), count, B, T, Z, Fd,
                                     w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
         return w
+
+    def _weight_prep(self, train):
+        """This step's derived weight copies (after cast_bf16 of the flat buffer): the k-contiguous
+        transposes the heads' split form and the dgrads read (train), and in fp8 mode W_ih_l{>=1}
+        as e4m3 with its per-tensor scale (448 / max|W_ih|) and, for the fp8 dgrad, its
+        transpose with the same scale (fp8.hip)."""
+        cfg, l, s = self.cfg, lib(), self._stream()
+        if train and self.w1_t is not None:
+            check(l.mlvae_cast_bf16_t(2 * cfg.C, 2 * cfg.H, self._ptr("decoder.mean_fc.blocks.0.weight"),
+                                      _pb(self.w1_t), s), "cast_bf16_t")
+        if train:
+            for li, dst in self.wih_t.items():
+                check(l.mlvae_cast_bf16_t(8 * cfg.H, cfg.Z if li == 0 else 2 * cfg.H,
+                                          self._ptr(f"decoder.rnn.weight_ih_l{li}"), _pb(dst), s), "cast_bf16_t")
+        if cfg.fp8 and cfg.prec == "bf16":
+            n = 8 * cfg.H * 2 * cfg.H
+            for li in self.w8:
+                wih = self._ptr(f"decoder.rnn.weight_ih_l{li}")
+                check(l.mlvae_fp8_scale(n, wih, x8_scale(cfg.dropout), _p(self.w8s[li]), _p(self.f8ws),
+                                        self.f8ws.numel() * 4, s), "fp8_scale")
+                check(l.mlvae_cast_fp8(n, wih, 0, _p(self.w8s[li]), 0.0, self.w8[li].data_ptr(), s), "cast_fp8")
+                if train and li in self.wih_t:  # the fp8 dgrad's W_ih^T, same scale
+                    check(l.mlvae_cast_fp8(n, _pb(self.wih_t[li]), 1, _p(self.w8s[li]), 0.0,
+                                           self.w8t[li].data_ptr(), s), "cast_fp8")
 
     def loss_weights(self):
         return float(self.cfg.kld_weight), float(self.cfg.recon_weight)
