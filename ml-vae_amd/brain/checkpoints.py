@@ -146,6 +146,7 @@ class Checkpointer:
     # ------------------------------------------------------------------ recover
     def recover_if_possible(self, max_key=None, min_key=None, device=None):
         d = self.find_checkpoint(max_key=max_key, min_key=min_key)
+        self.recovered_meta = None
         if d is None:
             logger.info("no checkpoint to recover in %s", self.checkpoints_dir)
             return None
@@ -153,6 +154,7 @@ class Checkpointer:
         for c, m in self.list_checkpoints():
             if c == d:
                 eoe = m["end_of_epoch"]
+                self.recovered_meta = dict(m["meta"], end_of_epoch=eoe)
         for k, obj in self.recoverables.items():
             path = os.path.join(d, k + PARAMFILE_EXT)
             if not os.path.exists(path):

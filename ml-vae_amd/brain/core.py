@@ -66,8 +66,16 @@ class Brain:
 
     def on_fit_start(self):
         self.init_optimizers()
+        self._resume_batches = 0
         if self.checkpointer is not None:
             self.checkpointer.recover_if_possible(device=torch.device(self.device))
+            # an intra-epoch checkpoint (--ckpt_interval_minutes): the EpochCounter re-runs that
+            # epoch, whose first `batches_done` batches were already trained -- they are skipped
+            # (SpeechBrain resumes through its saveable dataloader's position; here the dataset's
+            # batch order is reproducible per epoch, so skipping the same count is the same thing)
+            meta = getattr(self.checkpointer, "recovered_meta", None) or {}
+            if INTRA_EPOCH_CKPT_FLAG in meta:
+                self._resume_batches = int(meta.get("batches_done", 0))
 
     def init_optimizers(self):
         if self.opt_class is not None:
@@ -152,7 +160,11 @@ class Brain:
             self.step = 0
             acc = None
             last_ckpt = time.time()
-            for batch in train_set:
+            skip, self._resume_batches = self._resume_batches, 0
+            self._batches_skipped = skip
+            for i, batch in enumerate(train_set):
+                if i < skip:  # trained before the intra-epoch checkpoint this run resumed from
+                    continue
                 self.step += 1
                 loss = self.fit_batch(batch)
                 acc = self.update_average(loss, acc)
@@ -187,7 +199,8 @@ class Brain:
 
     def _save_intra_epoch_ckpt(self):
         self.checkpointer.save_and_keep_only(
-            end_of_epoch=False, num_to_keep=1, meta={INTRA_EPOCH_CKPT_FLAG: True},
+            end_of_epoch=False, num_to_keep=1,
+            meta={INTRA_EPOCH_CKPT_FLAG: True, "batches_done": self.step + self._batches_skipped},
             ckpt_predicate=lambda meta: INTRA_EPOCH_CKPT_FLAG in meta)
 
     def evaluate(self, test_set, max_key=None, min_key=None, progressbar=None,

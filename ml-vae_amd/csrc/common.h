@@ -12,6 +12,7 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));  // fp8 MFMA operand (32 e4m3 per lane)
+typedef int i32x4 __attribute__((ext_vector_type(4)));  // raw buffer-resource words (asm operands)
 
 // Compute precision of a matrix product (operands; accumulation is always fp32).
 enum MlvaePrec { PREC_F32 = 0, PREC_BF16 = 1 };

@@ -60,7 +60,6 @@ constexpr int EPI_OUT_BF16 = 32; // flag bit of the ABI's epi: C is bf16 (staged
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(3))) bf16x4* lds_b4_t;
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // The raw words of make_rsrc()'s buffer descriptor (stride 0, flags 0x00020000) for inline asm.
 __device__ __forceinline__ i32x4 rsrc_words(const void* base, unsigned bytes) {

@@ -240,3 +240,50 @@ def test_weight_for_matches_reference_fixture():
             total = MDModel.compute_and_save_losses(
                 fake, {k: torch.tensor(v) for k, v in zip(case["keys"], case["values"])})
         assert abs(float(total) - case["total"]) <= 1e-6 * abs(case["total"]), case
+
+
+def test_resume_from_intra_epoch_checkpoint_skips_trained_batches(tmp_path, monkeypatch):
+    """resuming from an intra-epoch checkpoint re-runs that epoch (EpochCounter saved
+    - 1) but must not train its first batches a second time: the checkpoint records how many
+    batches of the epoch were done, and fit() skips them."""
+    import brain.core as core
+    from brain import Checkpointer, EpochCounter
+    from brain.core import Brain, Stage
+
+    clock = [1000.0]
+    monkeypatch.setattr(core.time, "time", lambda: clock[0])
+    data = [torch.full((3, 4), float(i)) for i in range(6)]
+
+    class Toy(Brain):
+        def compute_forward(self, batch, stage):
+            return self.modules["lin"](batch)
+
+        def compute_objectives(self, out, batch, stage):
+            clock[0] += 40.0
+            return out.pow(2).mean()
+
+        def fit_batch(self, batch):
+            self.trained.append(int(batch[0, 0].item()))
+            if len(self.trained) == self.crash_after:
+                raise KeyboardInterrupt   # the run dies after this batch
+            return self.compute_objectives(self.compute_forward(batch, Stage.TRAIN), batch, Stage.TRAIN).detach()
+
+    def make(crash_after):
+        lin = torch.nn.Linear(4, 2)
+        ec = EpochCounter(1)
+        ck = Checkpointer(tmp_path, {"lin": lin, "epoch_counter": ec})
+        b = Toy(modules={"lin": lin}, opt_class=lambda p: torch.optim.SGD(p, lr=0.1),
+                run_opts={"device": "cpu", "ckpt_interval_minutes": 1.0}, checkpointer=ck)
+        b.trained, b.crash_after = [], crash_after
+        return b, ec
+
+    b, ec = make(crash_after=5)
+    try:
+        b.fit(ec, data)
+    except KeyboardInterrupt:
+        pass
+    # 40 s per batch, a checkpoint every 60 s: after batches 2 and 4 (the later one kept)
+    assert b.trained == [0, 1, 2, 3, 4]
+    b2, ec2 = make(crash_after=-1)
+    b2.fit(ec2, data)
+    assert b2.trained == [4, 5]   # batches 0-3 were in the checkpoint; 4 was lost with the crash
