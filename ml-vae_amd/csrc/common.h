@@ -43,6 +43,15 @@ __device__ __forceinline__ float tanh_fast(float x) {
   // tanh(x) = 1 - 2/(1+e^{2x}); saturates cleanly for |x| large
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
 }
+// The fp32 parity mode's cell math: libm-accurate.  tanh_fast loses relative accuracy near 0
+// (1 - 2/(2 + 2x) cancels: |err| ~ 1e-7 absolute, not relative), which made the fp32 mode's
+// rnn_out 6x further from fp64 than the fp32 oracle's (round 5, tools/parity_heads_dw1.py).
+template <int PREC> __device__ __forceinline__ float sigmoid_p(float x) {
+  if constexpr (PREC == PREC_F32) return 1.f / (1.f + expf(-x)); else return sigmoid_fast(x);
+}
+template <int PREC> __device__ __forceinline__ float tanh_p(float x) {
+  if constexpr (PREC == PREC_F32) return tanhf(x); else return tanh_fast(x);
+}
 
 // bf16 round-to-nearest-even, NaN-preserving (plain cast -> v_cvt_pk_bf16_f32).
 __device__ __forceinline__ short f2bf(float x) {

@@ -277,12 +277,12 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
     if (owner) {
       if (valid) {
         // acc[q'] = recurrent part of gate q' for unit jj, utterance bi
-        ig = sigmoid_fast(acc[0] + gx[0]);
-        fg = sigmoid_fast(acc[1] + gx[1]);
-        gg = tanh_fast(acc[2] + gx[2]);
-        og = sigmoid_fast(acc[3] + gx[3]);
+        ig = sigmoid_p<PREC>(acc[0] + gx[0]);
+        fg = sigmoid_p<PREC>(acc[1] + gx[1]);
+        gg = tanh_p<PREC>(acc[2] + gx[2]);
+        og = sigmoid_p<PREC>(acc[3] + gx[3]);
         c = fg * c + ig * gg;
-        hv = og * tanh_fast(c);
+        hv = og * tanh_p<PREC>(c);
       }
       if (s + 1 < T) {
         // gather 4 (bf16) / 2 (fp32) consecutive units of one utterance into one granule;
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
       dG[u][0] = dG[u][1] = dG[u][2] = dG[u][3] = 0.f;
       if (bvalid && cj + 16 * u < HJ) {
         const float dh = sdy[u] + dhrec[u];
-        const float tc = tanh_fast(scc[u]);
+        const float tc = tanh_p<PREC>(scc[u]);
         const float d_o = dh * tc;
         const float dcs = dc[u] + dh * sgo[u] * (1.f - tc * tc);
         const float di = dcs * sgg[u], dgg = dcs * sgi[u], df = dcs * scp[u];

@@ -57,42 +57,6 @@ __device__ __forceinline__ void publish(__amdgpu_buffer_rsrc_t r, unsigned byte_
 // 16-byte slot of row `utt` in an XOR-swizzled LDS image (conflict-free B/A-fragment reads)
 __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15); }
 
-// The forward's io waves (round 5).  An io wave's gx LDS-DMA for step s+1 and its stores of the
-// saved activations count on the same in-order vmcnt; waiting for the DMA with vmcnt(0) waited
-// for the stores too -- the io waves reached the barrier 1,660 ticks after the pollers at B = 256
-// (r04 stamps).  The DMA is issued from asm (a buffer_load ... lds builtin is a pending LDS write
-// to the compiler, which then drains vmcnt(0) before the next barrier or LDS read) and waited for
-// with a counted vmcnt (io_wait: the vm instructions the wave issued after it); the step barrier
-// is an LDS-only one (a __syncthreads() fence also waits for the stores).
-__device__ __forceinline__ i32x4 rsrc_words(const void* base, unsigned bytes) {
-  const unsigned long long b = (unsigned long long)(uintptr_t)base;
-  return i32x4{(int)(unsigned)b, (int)((unsigned)(b >> 32) & 0xffffu), (int)bytes, 0x00020000};
-}
-// 16 bytes per lane into LDS at dst + 16 lane (nt: read-once stream); m0 set in the same statement
-// (the kernels use m0 for nothing else)
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void dma16_nt(i32x4 rw, const void* dst, unsigned off) {
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds"
-               :: "v"(off), "s"(rw), "s"(la) : "memory", "m0");
-}
-#pragma clang diagnostic pop
-// s_waitcnt vmcnt(<= n), n wave-uniform (the younger vm instructions may stay in flight)
-__device__ __forceinline__ void vm_wait_le(int n) {
-  switch (n >= 8 ? 8 : n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
@@ -205,7 +169,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
   const auto rgx = make_rsrc(G16 + (size_t)grp * BG * T * 8 * H, 0xffffffffu);
-  const i32x4 rgx_w = rsrc_words(G16 + (size_t)grp * BG * T * 8 * H, 0xffffffffu);
   // debug bit 10 (timing probe only, outputs wrong): the saved activations and the gx loads
   // addressed time-major (row t * B + b) -- one step's rows of all utterances contiguous in HBM
   const bool tmaj = (a.dbg_mode & 1024) != 0;
@@ -215,12 +178,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // ZP: z rows [16 utt][32] bf16 per ring slot, lane-linear (lane 4 u + c: 16 B chunk c of utt u)
   unsigned short* zr = gxr;
   const auto rz = make_rsrc(a.Zb, (unsigned)min((size_t)a.B * T * a.ldz * 2, (size_t)0x7fffffff));
-  const i32x4 rz_w = rsrc_words(a.Zb, (unsigned)min((size_t)a.B * T * a.ldz * 2, (size_t)0x7fffffff));
-  // counted DMA waits (above): for full batch groups outside the timing probes -- a ragged group's
-  // waves may skip a store instruction whole, so their count is not known: vmcnt(0) there
-  const bool cw = grp * BG + BG <= a.B && !(a.dbg_mode & (1 | 1024 | 8192 | 16384));
-  int io_after = 0;       // (io waves) vm instructions issued since this wave's last gx DMA
-  bool io_dma = false;    // ... and whether it issued one
   auto io_load = [&](int s_) {  // input projection of step s_ into gx ring slot s_ & 1
     if (s_ >= T || (s_ > 0 && (a.dbg_mode & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
@@ -228,10 +185,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (wave == 4) {
         const int u = lane >> 2, b = grp * BG + u;
         const unsigned off = b < a.B ? (unsigned)((((size_t)b * T + t_) * a.ldz + 8 * (lane & 3)) * 2) : 0x80000000u;
-        if (cw) dma16_nt(rz_w, zr + (s_ & 1) * 16 * 32, off);
-        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_ptr_t)(zr + (s_ & 1) * 16 * 32), 16, off, 0, 0, NT_AUX);
-        io_after = 0;
-        io_dma = true;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_ptr_t)(zr + (s_ & 1) * 16 * 32), 16, off, 0, 0, NT_AUX);
       }
       return;
     }
@@ -249,26 +203,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       const auto rs = tmaj ? rgx_abs : rgx;
       unsigned short* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
       // nt: read-once stream, kept from displacing the hand-off lines in L2
-      if (cw) {
-        if (lane < HJ / 2) dma16_nt(rgx_w, dst, off);
-      } else if (lane < HJ / 2) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
-      }
-      io_after = 0;
-      io_dma = true;
+      if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
     }
   };
-  // store instructions of one io_store call by this wave (full groups: every lane stores)
-  const int io_nst = [&] {
-    constexpr int NG8c = 16 * 4 * HJ / 8, NQ2c = 16 * HJ / 4;
-    const int w0 = (wave - 4) * 64;  // this wave's first io thread
-    int n = NG8c / 256;              // gates
-    if (w0 < NQ2c) n += a.Y ? 2 : 1; // c (+ fp32 h)
-    const bool d8 = w0 >= NC8;
-    const int c8 = d8 ? w0 - NC8 : w0;
-    if (c8 < NC8 && (d8 ? a.Ydb != nullptr : a.Yb != nullptr)) n += (d8 && a.Y8) ? 2 : 1;
-    return n;
-  }();
   // dropout keep bits (bit e = element e) of h chunk c8 (8 units) at step s_: one mask quad per
   // 4 aligned elements, as dropout_scale in common.h
   auto drop_bits = [&](int s_, int c8) -> unsigned {
@@ -287,7 +224,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   };
   auto io_store = [&](int s_) {  // saved activations of step s_ from out ring slot s_ & 1
     if (s_ < 0 || s_ >= T || (a.dbg_mode & 1)) return;
-    io_after += io_nst;
     const int t_ = dir ? T - 1 - s_ : s_;
     const char* src = outr + (s_ & 1) * 16 * OUB;
     // activated gates (fp16 in the ring already): 16 utt x 4 gates x HJ/8 chunks, LDS -> HBM
@@ -418,12 +354,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (s == 0) read_gx();
       if (s > 0) {
         if (IO) {
-          // this wave's gx(s) LDS-DMA has landed (its younger stores may stay in flight)
-          if (cw) {
-            if (io_dma) vm_wait_le(io_after);
-          } else if (!(a.dbg_mode & 16384)) {  // bit 14: timing without the wait
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
+          if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
           IOSTAMP(1);
         } else {
           // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
@@ -471,9 +403,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
         }
         LWSTAMP();
-        // h image of step s complete; gx ring slot s & 1 landed (LDS-only barrier: the io waves'
-        // stores stay in flight)
-        lds_barrier();
+        __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
         LSTAMP(2);
         if (abort_flag) break;
         // gx of step s+1 right behind the barrier (it lands before barrier s+1)
@@ -562,7 +492,6 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             publish(xr, cell * sizeof(short), gr[0], same_xcd);
           }
         }
-        if constexpr (IO && MT > 0 && !AS) io_after += 1;  // (the publish store: one instruction)
       }
       LSTAMP(4);
       RTS(wave);

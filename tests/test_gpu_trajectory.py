@@ -188,7 +188,16 @@ def test_fp32_mode_whole_step_at_bench_sizes(B_, seed):
     the same parameters, inputs and randomness.  Pre-registered bound (round 5): for the ELBO, the
     encoder / decoder outputs and every gradient tensor, the engine's norm-relative error to fp64
     is <= 3x the fp32 oracle's (floored at the fp32 epsilon); plus the absolute bounds of the
-    earlier test (ELBO 1e-4 relative -- the north star -- and the Adam update checks)."""
+    earlier test (ELBO 1e-4 relative -- the north star -- and the Adam update checks).
+
+    Round 5: the B=256 gradient excess of round 4 (1e-4 to 1e-5 in both the engine and the fp32
+    oracle) was LeakyReLU-derivative flips -- a heads first-layer pre-activation within rounding of
+    0 whose sign fp32 gets wrong takes the 0.01 slope instead of 1, and that one entry of dP1 moves
+    every gradient behind it.  The oracle has one such flip (log_var head) at this seed; the engine
+    had one in the mean head while its fp32 recurrence used the hardware tanh (1 - 2/(1+e^2x),
+    relatively inaccurate near 0: rnn_out 1.2e-6 from fp64).  With libm cell math in the fp32 mode
+    the engine has none (tools/parity_heads_dw1.py counts them) and every row is within 4e-7 of
+    fp64: asserted as an absolute 1e-6 bound too."""
     need_gpu()
     from mlvae_hip.engine import VAEConfig
     from step_parity import oracle_fp64
@@ -221,5 +230,6 @@ def test_fp32_mode_whole_step_at_bench_sizes(B_, seed):
     print(f"[fp32 mode B={B_}] worst engine/oracle ratio {worst[1] / max(worst[2], FP32_EPS):.2f} ({worst[0]})")
     for k, a, b in rows:
         assert a <= 3.0 * max(b, FP32_EPS), (k, a, b)
+        assert a <= 1e-6, (k, a, b)
     assert e["loss"] <= 1e-4 and e["recon_loss"] <= 1e-4 and e["kld_loss"] <= 1e-4, e
     assert e["update_sign"] >= 0.999 and e["update_err"] <= 1e-2, e

@@ -1,8 +1,11 @@
 """Diagnostic (round 5): where the fp32 mode's mean-head first-layer gradient error at B = 256
-comes from (the fp64-anchored whole-step test: engine 2.4e-5 / 2.0e-5 vs the fp32 oracle's
+came from (the fp64-anchored whole-step test: engine 2.4e-5 / 2.0e-5 vs the fp32 oracle's
 3.7e-7 / 1.1e-7 for mean_fc.blocks.0.weight / bias).  Runs the engine's fp32 step, then sums the
-engine's own saved dP1 and rnn_out in fp64 on the host: if those sums match the fp64 oracle, the
-error is in the engine's reductions; if not, in dP1 / rnn_out themselves.
+engine's own saved dP1 and rnn_out in fp64 on the host (equal to the engine's: the reductions were
+exact), and counts the LeakyReLU-derivative flips of the heads' first layer against fp64.
+Result: one flip in the engine's mean head (hardware tanh in the fp32 recurrence, rnn_out 1.2e-6
+from fp64), one in the oracle's log_var head; with libm cell math the engine has none
+(profiles/r05_fp32_mode_vs_fp64_B256.txt).
 usage: python tools/parity_heads_dw1.py [B] [T]"""
 import os
 import sys
@@ -46,6 +49,21 @@ def main():
               f"host-fp64(engine dP1, R) {nr(hw, gw64):.2e}  oracle32 {nr(gw32, gw64):.2e}  |g| {gw64.norm():.3e}")
         print(f"{name}: bias    engine {nr(g[f'decoder.{name}.blocks.0.bias'], gb64):.2e}  "
               f"host-fp64(engine dP1) {nr(hb, gb64):.2e}  oracle32 {nr(gb32, gb64):.2e}  |g| {gb64.norm():.3e}")
+    # LeakyReLU derivative flips: first-layer pre-activations whose sign differs from fp64's, on
+    # the valid frames (the padded ones carry no gradient)
+    R64 = r64["out"]["dec"]["rnn_out"].reshape(B * T, -1)
+    R32 = rec["out"]["dec"]["rnn_out"].reshape(B * T, -1).float()
+    P1e = w.P1.detach().cpu().double()
+    from oracle.vae_cpu import length_to_mask
+    m = length_to_mask(rec["inputs"][1], T).reshape(-1) > 0
+    for name, sl in (("mean_fc", slice(0, C)), ("log_var_fc", slice(C, 2 * C))):
+        W = params[f"decoder.{name}.blocks.0.weight"]
+        b = params[f"decoder.{name}.blocks.0.bias"]
+        p64 = R64 @ W.double().t() + b.double()
+        p32 = R32 @ W.t() + b
+        fe = ((P1e[:, sl] > 0) != (p64 > 0))[m].sum().item()
+        fo = ((p32 > 0) != (p64 > 0))[m].sum().item()
+        print(f"{name}: lrelu' flips vs fp64 on {int(m.sum())} frames x {C}: engine {fe}  oracle32 {fo}")
     print("rnn_out engine vs fp64", nr(R.view(B, T, -1), r64["out"]["dec"]["rnn_out"]),
           " oracle32 vs fp64", nr(rec["out"]["dec"]["rnn_out"], r64["out"]["dec"]["rnn_out"]))
 
