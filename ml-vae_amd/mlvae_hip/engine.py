@@ -418,6 +418,7 @@ class VAEEngine:
         self.prioritize = False   # measured no gain at c2 (8.44 vs 8.39 ms); kept as an option
         self.main_stream = torch.cuda.Stream(self.device, priority=-1)
         self._on_side = False
+        self.side_prep = True      # weight prep beside the layer-0 recurrence (when it leaves CUs free)
         self.kernel_timers = None   # {name: [(start_event, end_event), ...]} when profiling
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
@@ -662,7 +663,7 @@ class VAEEngine:
             # the transposed / fp8 weight copies the layer-1 projection, the heads and the backward
             # read: beside the encoder and the layer-0 forward recurrence on the side stream when
             # that recurrence leaves CUs free (off the critical path), else in line
-            if not self._full_chip(B):
+            if self.side_prep and not self._full_chip(B):
                 self._on_side = True
                 self.side_stream.wait_event(self._mark())
                 try:
