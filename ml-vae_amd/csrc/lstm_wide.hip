@@ -416,7 +416,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         if (IO && (PURE_IO || !late_dma_s)) io_load(s + 1);
         if (PURE_IO && s > 0) io_store(s - 1);  // (out ring slot s-1 & 1 complete at barrier s)
         IOSTAMP(3);
-        read_gx();
+        if constexpr (!ZP || MT == 0) read_gx();  // (ZP: inside the first k-batch below)
         // The io waves' MFMAs at priority 1: the io wave of each SIMD finishes its MFMAs first
         // and its cell update (VALU / transcendental) overlaps the poller's MFMAs, instead of both
         // waves' cells following both MFMA streams (same box, alternating: c3 12.06 -> 11.99,
@@ -424,20 +424,43 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // (AS: the pollers, owning most tiles, go first)
         const bool first = AS ? !IO : IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
         if (first) __builtin_amdgcn_s_setprio(1);
+        // k-chunks in the order KR .. NKC-1, 0 .. KR-1: the chunks whose A-fragments live in LDS
+        // first, their fragment reads (and ZP's z-row read) issued with the first batch's h
+        // reads right behind the barrier, where one LDS round trip is exposed anyway -- read
+        // inside the chain they had one or two MFMAs of cover each
+        constexpr int KLA = KLF > 0 ? KLF : 1;
+        bf16x8 wl[MTA][KLA];
+        bf16x8 zf;
 #pragma unroll
         for (int k0 = 0; k0 < NKC; k0 += HB) {
           bf16x8 hfrag[HB];
 #pragma unroll
           for (int i = 0; i < HB; ++i)
-            hfrag[i] = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
+            hfrag[i] = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, ((k0 + i + KR) % NKC) * 4 + q) * 16);
+          if (k0 == 0) {
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+              for (int j = 0; j < KLF; ++j) wl[t][j] = wlds[((m0 + t) * KLF + j) * 64 + lane];
+            if constexpr (ZP) zf = *reinterpret_cast<const bf16x8*>(zr + (s & 1) * 16 * 32 + bi * 32 + 8 * q);
+          }
           __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
+          if constexpr (ZP) {
+            if (k0 == 0) {
+#pragma unroll
+              for (int t = 0; t < MT; ++t) {
+                const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wz[t], zf, bz4[t], 0, 0, 0);
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = r[g4];
+              }
+            }
+          }
 #pragma unroll
           for (int i = 0; i < HB; ++i) {
-            const int kc = k0 + i;
+            const int kc = (k0 + i + KR) % NKC;
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
-              const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0]
-                                        : wlds[((m0 + t) * KLF + (kc - KR)) * 64 + lane];
+              const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0] : wl[t][kc >= KR ? kc - KR : 0];
               acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag[i], acc[t], 0, 0, 0);
             }
           }
