@@ -113,12 +113,14 @@ def encoder_bwd_bytes(N, F, E, Z):
     return N * (4 * Z + 4 * 2 * Z + 4 * Z + 2 * 2 * E + 4 * F)
 
 
-def heads_bytes(N, F, C, H, dy_bytes=4):
+def heads_bytes(N, F, C, H, dy_bytes=4, wg_fused=False):
     """The heads (train, the engine's fused mode): reads h (2H bf16) and x (F fp32); writes
     mu_x, log_var_x (F each, fp32), dY (2H; dy_bytes 2 = bf16, the engine's bf16 step) and, as
     bf16 (the weight-gradient GEMMs' operand precision), P1 (2C), P2m, P2v (C each), d mu_x,
-    d log_var_x (F each), dP2m, dP2v (C each), dP1 (2C)."""
-    return N * (2 * 2 * H + 4 * F + 4 * 2 * F + dy_bytes * 2 * H + 2 * (2 * C + 2 * C + 2 * F + 2 * C + 2 * C))
+    d log_var_x (F each), dP2m, dP2v (C each), dP1 (2C).  wg_fused (round 5, the heads' dW3 / dW2
+    inside the heads kernel): P2, d mu_x, d log_var_x and dP2 are no longer written."""
+    saved = 2 * C + 2 * C if wg_fused else 2 * C + 2 * C + 2 * F + 2 * C + 2 * C
+    return N * (2 * 2 * H + 4 * F + 4 * 2 * F + dy_bytes * 2 * H + 2 * saved)
 
 
 def conv_fwd_bytes(N, F, E):
@@ -331,9 +333,10 @@ def timed_run(eng, x, lens, steps, warmup, world, timers=None, norm=None):
     return dt, loss
 
 
-def secondary(kern, B, T, cfg_name, dy_bytes=4):
+def secondary(kern, B, T, cfg_name, dy_bytes=4, wg_fused=False):
     """Per-kernel rooflines of the timed secondary launches (HIP events, main stream); dy_bytes:
-    the width of dY the engine's heads write (2 = bf16)."""
+    the width of dY the engine's heads write (2 = bf16); wg_fused: the heads computed their small
+    weight gradients in-kernel (VAEEngine.heads_wgrad)."""
     F, E, Z, H, L, C, _, _, _ = CONFIGS[cfg_name]
     N = B * T
     out = {}
@@ -358,7 +361,7 @@ def secondary(kern, B, T, cfg_name, dy_bytes=4):
             ("encoder_bwd", encoder_bwd_bytes(N, F, E, Z), ["encoder_bwd"]),
             ("conv_fwd", conv_fwd_bytes(N, F, E), ["conv_fwd_l1", "conv_fwd_l2"]),
             ("conv_bwd", conv_bwd_bytes(N, F, E), ["conv_dgrad", "conv_wgrad_l1"]),
-            ("heads", heads_bytes(N, F, C, H, dy_bytes), ["heads_p1", "heads_mid", "heads_dy"])):
+            ("heads", heads_bytes(N, F, C, H, dy_bytes, wg_fused), ["heads_p1", "heads_mid", "heads_dy"])):
         if name in kern:
             gbs = nbytes / (kern[name] * 1e-3) / 1e9
             out[name] = {"bound": "hbm", "avg_launch_ms": kern[name], "achieved": gbs,
@@ -442,7 +445,7 @@ def extra_runs(args, device):
             kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}
             if cname in ENC_CONV:
                 out[key]["encoder"] = f"Conv1d K={ENC_CONV[cname]} [{F},{E},{E}]"
-                out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname, dyb).items()
+                out[key]["kernels"] = {k: v for k, v in secondary(kern, B, T, cname, dyb, getattr(eng, 'heads_wgrad', False)).items()
                                        if k.startswith("conv")}
                 # PMC HBM bytes per launch of each conv kernel (profiles/pmc_traffic.json[c4])
                 out[key]["pmc_bytes_per_launch"] = {k: pmc_traffic(f"{cname}/{k}") for k in
@@ -451,7 +454,7 @@ def extra_runs(args, device):
                 out[key]["pmc_source"] = pmc_source(cname)
                 out[key]["kernels_standalone"] = conv_standalone(cname, device)
             else:
-                sec = secondary(kern, B, T, cname, dyb)
+                sec = secondary(kern, B, T, cname, dyb, getattr(eng, 'heads_wgrad', False))
                 if cname in FP8:  # against the fp8 (block-scaled) MFMA peak
                     what = {"proj_l1": "layer-1 input projection on fp8 e4m3 operands (incl. the W_ih "
                                        "scale + casts; the input arrives as e4m3 from the recurrence)",
@@ -526,6 +529,7 @@ def main():
     launches = {k: len(v) for k, v in timers.items()}
     dyb = 2 if getattr(eng, "dy_bf16", False) else 4   # dY width the engine's bf16 step used
     zp = bool(getattr(eng, "zproj", False))             # layer 0's projection inside its forward
+    wgf = bool(getattr(eng, "heads_wgrad", False))      # the heads' small weight gradients in-kernel
     del eng
     torch.cuda.empty_cache()
     if rank == 0:
@@ -572,7 +576,7 @@ def main():
             "train_tflops": value * 6 * macs_per_frame(F, E, Z, H, L, C) / 1e12,
             "roofline": recs[dom],
             "recurrences": recs,
-            "kernels": secondary(kern, B, T, args.config, dyb) if args.prec == "bf16" else {},
+            "kernels": secondary(kern, B, T, args.config, dyb, wgf) if args.prec == "bf16" else {},
             "kernel_ms": kern,
         }
         if world == 1 and not args.no_extra:

@@ -352,6 +352,27 @@ int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int 
                          float* partials, float* bias_ws, size_t bias_ws_bytes, float* db3m,
                          float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
                          void* stream);
+/* mlvae_heads_fused_ex plus, when wg_ws is given, the four small weight gradients of the heads
+ * (ref:src/modules/fc_block.py:9-16 blocks.2 / blocks.4 of mean_fc and log_var_fc, the products
+ * autograd forms for decoder.py:24-25): dw3m / dw3v = dOUT_h^T P2_h [F, C] and dw2m / dw2v =
+ * dP2_h^T P1_h [C, C], accumulated inside the heads' middle kernel over its 64-frame tiles (the
+ * frame rows as K, read transposed from the LDS images it already holds), per-workgroup slabs
+ * reduced in a fixed order -- replacing four split-K GEMM launches over the saved intermediates.
+ * Needs the split form (train, bias_ws, saved_bf16 bit 0) and wg_ws_bytes >=
+ * mlvae_heads_wgrad_workspace_size(B, T, F, C); under mse (loss_type 1) dw3v / dw2v may be NULL
+ * and are not written.  P2 / dOUT / dP2 (p2m, p2v, dmux, dlvx, dp2m, dp2v) are then not written. */
+size_t mlvae_heads_wgrad_workspace_size(int B, int T, int F, int C);
+int mlvae_heads_fused_ex2(int B, int T, int F, int C, int H2, int loss_type, int train,
+                          const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
+                          const float* w2m, const float* b2m, const float* w3m, const float* b3m,
+                          const float* w2v, const float* b2v, const float* w3v, const float* b3v,
+                          const float* x, const float* lens, const int* count, float rec_scale,
+                          float* p1, float* p2m, float* p2v, float* mux, float* lvx, float* dmux,
+                          float* dlvx, float* dp2m, float* dp2v, float* dp1, float* dy,
+                          float* partials, float* bias_ws, size_t bias_ws_bytes, float* db3m,
+                          float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
+                          float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
+                          float* dw2v, void* stream);
 /* Skinny products of the bottom LSTM layer (bf16; one side is the latent width):
  * mlvae_skinny_nt: C [M, N] (fp32, ldc) = A [M, K] . Bt [N, K]^T, bf16 k-contiguous operands,
  *   N in {16, 32, 48, 64}, K % 32 == 0: dZ = dG W_ih over the k-contiguous W_ih^T copy.

@@ -44,6 +44,7 @@ struct HeadArgs {
   int sbf;         // the saved intermediates (P1, P2, dOUT, dP2, dP1) are bf16 (packed rows)
   float* bias_ws;  // train, optional: per-workgroup column sums [gridDim.x][NBS] of dOUT_m | dOUT_v |
                    // dP2_m | dP2_v | dP1 (the five bias gradients before the workgroup sum)
+  float* wg_ws;    // split form, optional: per-workgroup partial dW3 / dW2 slabs (heads_mid_kernel<.., true>)
 };
 
 // bias-gradient column sums per workgroup: [dOUT_m F | dOUT_v F | dP2_m C | dP2_v C | dP1 2C]
@@ -65,6 +66,22 @@ __device__ __forceinline__ void rows16_to_lds(f32x4 v, float* dst, int lane) {
 }
 
 __device__ __forceinline__ bf16x8 lds8(const short* p) { return *reinterpret_cast<const bf16x8*>(p); }
+typedef __attribute__((address_space(3))) bf16x4* lds_b4h_p;
+// MFMA operand fragment (m or n = base + (lane & 15), k = kk + 8 (lane >> 4) + e) of an LDS image
+// stored [k rows][ld], read transposed by ds_read_b64_tr_b16: the weight gradients below take
+// the frame rows as K
+__device__ __forceinline__ bf16x8 trk(const short* img, int ld, int base, int kk, int lane) {
+  const int g = lane >> 4, i4 = lane & 15, qq = i4 >> 2, pp = i4 & 3;
+  const int r1 = kk + 8 * g + qq, r2 = r1 + 4;
+  const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4h_p)(img + r1 * ld + base + 4 * pp));
+  const bf16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4h_p)(img + r2 * ld + base + 4 * pp));
+  return bf16x8{v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+}
+// weight-gradient tiles (16 x 16) of the fused form: dW3 of both heads [F x C], then dW2 [C x C]
+template <int C, int F> constexpr int nt3() { return 2 * (F / 16) * (C / 16); }
+template <int C, int F> constexpr int nt2() { return 2 * (C / 16) * (C / 16); }
+// floats of one workgroup's slab (fragment order: ((tile * 64 + lane) * 4 + r))
+template <int C, int F> constexpr int wg_slab() { return (nt3<C, F>() + nt2<C, F>()) * 256; }
 __device__ __forceinline__ void st4bf(short* p, f32x4 v) {
   *reinterpret_cast<bf16x4*>(p) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
 }
@@ -382,7 +399,12 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
 //      registers while the current one computes
 //   3. dY = dP1 W1             fp32       gemm256 (k-contiguous dP1 and W1^T)
 // The partial sums and bias column sums keep the fused kernel's per-tile layout.
-template <int C, int F>
+// WG: the four small weight gradients (dW3 = dOUT^T P2, dW2 = dP2^T P1 per head) accumulated here
+// over the workgroup's tiles, K = the 64 frame rows of a tile read transposed from the LDS images
+// the stages already hold -- instead of four split-K GEMM launches (+ their reduces) re-reading
+// the saved P2 / dOUT / dP2 from HBM, which are then not written at all.  Each wave owns a quarter
+// of the 16 x 16 output tiles; per-workgroup slabs, reduced in a fixed order (heads_wg_reduce*).
+template <int C, int F, bool WG>
 __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
   constexpr int C2 = 2 * C, FK = (F + 31) / 32 * 32;
   constexpr int LC = C + 8, LF = FK + 8, L2C = C2 + 8;
@@ -455,6 +477,16 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
   __syncthreads();
 
   const int lrow = 16 * wave + l15;
+  constexpr int NT3W = nt3<C, F>() / 4, NT2W = nt2<C, F>() / 4;  // tiles per wave
+  static_assert(nt3<C, F>() % 4 == 0 && nt2<C, F>() % 4 == 0, "tiles split over 4 waves");
+  f32x4 aw3[WG ? NT3W : 1], aw2[WG ? NT2W : 1];
+  if constexpr (WG) {
+#pragma unroll
+    for (int i = 0; i < NT3W; ++i) aw3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NT2W; ++i) aw2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr bool SAVE = !WG;  // P2 / dOUT / dP2 have no other reader than the weight gradients
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int grow = tile * RT + lrow;
     const bool rv = grow < a.N;
@@ -493,7 +525,7 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc2[h][j][r] = lrelu(acc2[h][j][r] + a.b2[h][col + r]);
         st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc2[h][j]);
-        if (rv) st_saved(a.P2[h], (size_t)grow * C + col, acc2[h][j], 1);
+        if (SAVE && rv) st_saved(a.P2[h], (size_t)grow * C + col, acc2[h][j], 1);
       }
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc3[h][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -547,13 +579,29 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
       rows16_to_lds(gv, &bred[wave][F + 16 * j], lane);
       st4bf(sm + O_DO + lrow * LF + col, gm);
       st4bf(sm + O_DO + RT * LF + lrow * LF + col, gv);
-      if (rv) {
+      if (SAVE && rv) {
         st_saved(a.dOUT[0], (size_t)grow * F + col, gm, 1);
         if (lik) st_saved(a.dOUT[1], (size_t)grow * F + col, gv, 1);
       }
     }
     lsum = wave_sum(lsum);
     if (lane == 0) red[wave] = lsum;
+    if constexpr (WG) {
+      // dW3_h += dOUT_h^T P2_h over the tile's 64 rows (every wave's rows: a barrier before, and
+      // one after -- stage 5 overwrites the P2 images with dP2)
+      lds_barrier();
+#pragma unroll
+      for (int i = 0; i < NT3W; ++i) {
+        const int t = wave * NT3W + i, h = t / ((F / 16) * NC), fb = (t / NC) % (F / 16), cb = t % NC;
+        if (h < nh) {
+#pragma unroll
+          for (int kk = 0; kk < RT; kk += 32)
+            aw3[i] = mfma(trk(sm + O_DO + h * RT * LF, LF, 16 * fb, kk, lane),
+                          trk(sm + O_P2 + h * RT * LC, LC, 16 * cb, kk, lane), aw3[i]);
+        }
+      }
+      lds_barrier();
+    }
 
     // ---- stages 5-6 per head: dP2 = (dOUT W3) * lrelu'(P2), dP1_h = (dP2 W2) * lrelu'(P1_h);
     // every image a wave reads here is its own rows: no workgroup barrier until the sums
@@ -577,7 +625,7 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
         for (int r = 0; r < 4; ++r) acc5[j][r] *= lrelu_d(acc2[h][j][r]);
         rows16_to_lds(acc5[j], &bred[wave][2 * F + h * C + 16 * j], lane);
         st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc5[j]);
-        if (rv && h < nh) st_saved(a.dP2[h], (size_t)grow * C + col, acc5[j], 1);
+        if (SAVE && rv && h < nh) st_saved(a.dP2[h], (size_t)grow * C + col, acc5[j], 1);
       }
       f32x4 acc6[NC];
 #pragma unroll
@@ -606,7 +654,30 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
     for (int c = tid; c < NBS; c += 256)
       a.bias_ws[(size_t)tile * NBS + c] = (bred[0][c] + bred[1][c]) + (bred[2][c] + bred[3][c]);
     if (tid == 0) a.partials[tile] = red[0] + red[1] + red[2] + red[3];
+    if constexpr (WG) {
+      // dW2_h += dP2_h^T P1_h (the dP2 images of every wave are complete at the barrier above;
+      // the next tile rewrites them and the P1 image only after the one below)
+#pragma unroll
+      for (int i = 0; i < NT2W; ++i) {
+        const int t = wave * NT2W + i, h = t / (NC * NC), ob = (t / NC) % NC, ib = t % NC;
+        if (h < nh) {
+#pragma unroll
+          for (int kk = 0; kk < RT; kk += 32)
+            aw2[i] = mfma(trk(sm + O_P2 + h * RT * LC, LC, 16 * ob, kk, lane),
+                          trk(sm + O_P1, L2C, h * C + 16 * ib, kk, lane), aw2[i]);
+        }
+      }
+    }
     lds_barrier();  // bred / red are rewritten by the next tile
+  }
+  if constexpr (WG) {  // this workgroup's slab, in fragment order (16-byte stores, lane-contiguous)
+    float* slab = a.wg_ws + (size_t)blockIdx.x * wg_slab<C, F>();
+#pragma unroll
+    for (int i = 0; i < NT3W; ++i)
+      *reinterpret_cast<f32x4*>(slab + ((size_t)(wave * NT3W + i) * 64 + lane) * 4) = aw3[i];
+#pragma unroll
+    for (int i = 0; i < NT2W; ++i)
+      *reinterpret_cast<f32x4*>(slab + ((size_t)(nt3<C, F>() + wave * NT2W + i) * 64 + lane) * 4) = aw2[i];
   }
 }
 
@@ -666,12 +737,28 @@ int launch_heads(const HeadArgs& a, hipStream_t st) {
   return 0;
 }
 
-template <int C, int F>
+int heads_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+// persistent heads_mid grid: one workgroup per CU (the LDS holds one), ~8 tiles each at c3
+int mid_grid(int N) {
+  const int ntiles = (N + RT - 1) / RT, cus = heads_cus();
+  return ntiles < cus ? ntiles : cus;
+}
+
+template <int C, int F, bool WG>
 int launch_mid(const HeadArgs& a, hipStream_t st) {
   constexpr int FK = (F + 31) / 32 * 32, LC = C + 8, LF = FK + 8, L2C = 2 * C + 8;
   constexpr size_t lds = (size_t)(2 * C * LC * 2 + 2 * F * LC + 2 * C * LF + RT * L2C + 2 * RT * LC +
                                   2 * RT * LF) * sizeof(short);
-  auto k = heads_mid_kernel<C, F>;
+  auto k = heads_mid_kernel<C, F, WG>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -681,13 +768,53 @@ int launch_mid(const HeadArgs& a, hipStream_t st) {
     }
     attr = true;
   }
-  // persistent: one workgroup per CU (the LDS holds one), ~8 tiles each at c3
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  const int ntiles = (a.N + RT - 1) / RT;
-  k<<<ntiles < cus ? ntiles : cus, 256, lds, st>>>(a);
+  k<<<mid_grid(a.N), 256, lds, st>>>(a);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// the fused weight gradients' slabs: stage 1 sums slice z of the workgroups (fixed order) per
+// element, stage 2 the WG_NZ slices in order and scatters fragment order to the four matrices
+constexpr int WG_NZ = 16;
+__global__ __launch_bounds__(256) void heads_wg_reduce1(const float* __restrict__ slabs, int G, int S,
+                                                        float* __restrict__ part) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= S) return;
+  const int z = blockIdx.y, g0 = z * G / WG_NZ, g1 = (z + 1) * G / WG_NZ;
+  float v = 0.f;
+#pragma unroll 8  // loads in flight; the adds keep their order
+  for (int g = g0; g < g1; ++g) v += slabs[(size_t)g * S + e];
+  part[(size_t)z * S + e] = v;
+}
+template <int C, int F>
+__global__ __launch_bounds__(256) void heads_wg_reduce2(const float* __restrict__ part, float* dw3m,
+                                                        float* dw3v, float* dw2m, float* dw2v) {
+  constexpr int S = wg_slab<C, F>(), NC = C / 16, NF = F / 16;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= S) return;
+  float v = 0.f;
+#pragma unroll
+  for (int z = 0; z < WG_NZ; ++z) v += part[(size_t)z * S + e];
+  const int r = e & 3, lane = (e >> 2) & 63, tp = e >> 8;
+  const int m = 4 * (lane >> 4) + r, n = lane & 15;
+  if (tp < nt3<C, F>()) {
+    const int h = tp / (NF * NC), fb = (tp / NC) % NF, cb = tp % NC;
+    float* d = h ? dw3v : dw3m;
+    if (d) d[(16 * fb + m) * C + 16 * cb + n] = v;
+  } else {
+    const int t = tp - nt3<C, F>(), h = t / (NC * NC), ob = (t / NC) % NC, ib = t % NC;
+    float* d = h ? dw2v : dw2m;
+    if (d) d[(16 * ob + m) * C + 16 * ib + n] = v;
+  }
+}
+template <int C, int F>
+int launch_wg_reduce(const HeadArgs& a, float* dw3m, float* dw3v, float* dw2m, float* dw2v, hipStream_t st) {
+  constexpr int S = wg_slab<C, F>();
+  const int G = mid_grid(a.N);
+  float* part = a.wg_ws + (size_t)G * S;
+  heads_wg_reduce1<<<dim3((S + 255) / 256, WG_NZ), 256, 0, st>>>(a.wg_ws, G, S, part);
+  MLVAE_CHECK_LAUNCH();
+  heads_wg_reduce2<C, F><<<(S + 255) / 256, 256, 0, st>>>(part, dw3m, dw3v, dw2m, dw2v);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
@@ -742,6 +869,13 @@ extern "C" size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C) {
   return (size_t)((B * T + RT - 1) / RT + RSL) * (2 * F + 4 * C) * sizeof(float);
 }
 
+// the fused small weight gradients (mlvae_heads_fused_ex2): per-workgroup slabs + WG_NZ partials
+extern "C" size_t mlvae_heads_wgrad_workspace_size(int B, int T, int F, int C) {
+  if (C != 64 || (F != 64 && F != 80) || B <= 0 || T <= 0) return 0;
+  const size_t S = F == 80 ? wg_slab<64, 80>() : wg_slab<64, 64>();
+  return ((size_t)mid_grid(B * T) + WG_NZ) * S * sizeof(float);
+}
+
 static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int train,
                       const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
                       const float* b1, const float* w2m, const float* b2m,
@@ -752,7 +886,8 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                       float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
                       float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
                       float* db3m, float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
-                      void* stream);
+                      float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
+                      float* dw2v, void* stream);
 
 extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int train,
                                  const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
@@ -766,7 +901,7 @@ extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_ty
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
-                    nullptr, 0, stream);
+                    nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
@@ -783,7 +918,30 @@ extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
-                    db1, saved_bf16, stream);
+                    db1, saved_bf16, nullptr, 0, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+// ... and, with wg_ws, the four small weight gradients dW3 / dW2 of both heads too (written to
+// dw3m / dw3v [F, C], dw2m / dw2v [C, C]; the log_var head's pointers may be null under mse):
+// split form only (train, bias sums, bf16 saved intermediates).  P2 / dOUT / dP2 are then not
+// written (p2m, p2v, dmux, dlvx, dp2m, dp2v may still be passed; nothing reads them)
+extern "C" int mlvae_heads_fused_ex2(int B, int T, int F, int C, int H2, int loss_type, int train,
+                                     const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
+                                     const float* b1, const float* w2m, const float* b2m,
+                                     const float* w3m, const float* b3m, const float* w2v,
+                                     const float* b2v, const float* w3v, const float* b3v,
+                                     const float* x, const float* lens, const int* count,
+                                     float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
+                                     float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
+                                     float* dp1, float* dy, float* partials, float* bias_ws,
+                                     size_t bias_ws_bytes, float* db3m, float* db3v, float* db2m,
+                                     float* db2v, float* db1, int saved_bf16, float* wg_ws,
+                                     size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
+                                     float* dw2v, void* stream) {
+  return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
+                    b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
+                    dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
+                    db1, saved_bf16, wg_ws, wg_ws_bytes, dw3m, dw3v, dw2m, dw2v, stream);
 }
 
 static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int train,
@@ -796,7 +954,8 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                                  float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
                                  float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
                                  float* db3m, float* db3v, float* db2m, float* db2v, float* db1,
-                                 int saved_bf16, void* stream) {
+                                 int saved_bf16, float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v,
+                                 float* dw2m, float* dw2v, void* stream) {
   if (B <= 0 || T <= 0) return 0;
   if (!mlvae_heads_supported(C, F, H2)) {
     mlvae_set_error("heads: unsupported shape C=%d F=%d 2H=%d (C 64, F 64|80, 2H %% 128)", C, F, H2);
@@ -838,6 +997,17 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
   hipStream_t st = (hipStream_t)stream;
   int rc;
   const bool split = train && bias_ws && (saved_bf16 & 1) && !heads_fused_only();
+  a.wg_ws = nullptr;
+  if (wg_ws) {
+    const bool mse = loss_type == 1;
+    if (!split || wg_ws_bytes < mlvae_heads_wgrad_workspace_size(B, T, F, C) || !dw3m || !dw2m ||
+        (!mse && (!dw3v || !dw2v))) {
+      mlvae_set_error("heads: fused weight gradients need the split form, a workspace of %zu B and "
+                      "the weight gradients", mlvae_heads_wgrad_workspace_size(B, T, F, C));
+      return 1;
+    }
+    a.wg_ws = wg_ws;
+  }
   if (dy_bf16 && !split) {
     mlvae_set_error("heads: bf16 dY (saved_bf16 bit 1) needs the split form (train, bias_ws, saved_bf16 bit 0)");
     return 1;
@@ -848,8 +1018,15 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
     rc = mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
                          nullptr, EPI_LRELU_BF16, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
     if (rc) return rc;
-    rc = F == 80 ? launch_mid<64, 80>(a, st) : launch_mid<64, 64>(a, st);
+    if (a.wg_ws) rc = F == 80 ? launch_mid<64, 80, true>(a, st) : launch_mid<64, 64, true>(a, st);
+    else rc = F == 80 ? launch_mid<64, 80, false>(a, st) : launch_mid<64, 64, false>(a, st);
     if (rc) return rc;
+    if (a.wg_ws) {
+      const bool mse = loss_type == 1;
+      rc = F == 80 ? launch_wg_reduce<64, 80>(a, dw3m, mse ? nullptr : dw3v, dw2m, mse ? nullptr : dw2v, st)
+                   : launch_wg_reduce<64, 64>(a, dw3m, mse ? nullptr : dw3v, dw2m, mse ? nullptr : dw2v, st);
+      if (rc) return rc;
+    }
     rc = mlvae_gemm_bf16(0, 1, a.N, H2, 2 * C, 1, dp1, 2 * C, 0, w1t_bf16, 2 * C, 0, dy, H2, 0, 0.f, nullptr,
                          nullptr, dy_bf16 ? 32 : 0 /* EPI_OUT_BF16 */, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f,
                          nullptr, 0, stream);

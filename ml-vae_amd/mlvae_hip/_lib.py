@@ -69,6 +69,10 @@ _SIGS = {
     "mlvae_heads_bias_workspace_size": [I, I, I, I],
     "mlvae_heads_fused_ex": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
                              P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, I, P],
+    "mlvae_heads_fused_ex2": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
+                              P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, I,
+                              P, SZ, P, P, P, P, P],
+    "mlvae_heads_wgrad_workspace_size": [I, I, I, I],
     "mlvae_skinny_proj": [I, I, I, P, I, P, I, P, P, P, I, P],
     "mlvae_skinny_proj_ex": [I, I, I, P, I, P, I, P, P, P, I, I, P],
     "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],
@@ -133,6 +137,8 @@ _RESTYPE = {
     "mlvae_skinny_tn_workspace_size": SZ,
     "mlvae_encoder_workspace_size": SZ,
     "mlvae_viterbi_workspace_size": SZ,
+    "mlvae_heads_bias_workspace_size": SZ,
+    "mlvae_heads_wgrad_workspace_size": SZ,
 }
 
 _lib = None

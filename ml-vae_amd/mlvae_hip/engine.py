@@ -262,6 +262,9 @@ class _Work:
         # fused heads: per-workgroup bias-gradient column sums (the five head biases)
         self.heads_bws = empty(lib().mlvae_heads_bias_workspace_size(B, T, F, C) // 4 + 1, **f) \
             if self.bf else None
+        # ... and the heads' four small weight gradients accumulated inside the heads kernel
+        nwg = lib().mlvae_heads_wgrad_workspace_size(B, T, F, C) if self.bf else 0
+        self.heads_wgws = empty(nwg // 4 + 1, **f) if nwg else None
         self.dY = [empty(N, 2 * H, **f) for _ in range(L)]
         self.dZs = empty(N, Z, **f)
         self.dML = empty(N, 2 * Z, **f)
@@ -419,6 +422,7 @@ class VAEEngine:
         self.main_stream = torch.cuda.Stream(self.device, priority=-1)
         self._on_side = False
         self.side_prep = True      # weight prep beside the layer-0 recurrence (when it leaves CUs free)
+        self.heads_wgrad = True    # the heads' dW3 / dW2 inside the heads kernel (mlvae_heads_fused_ex2)
         self.kernel_timers = None   # {name: [(start_event, end_event), ...]} when profiling
         self.process_group = None   # set by mlvae_hip.dist for data parallel
         self.world = 1
@@ -839,8 +843,16 @@ class VAEEngine:
                          hg("log_var_fc.blocks.4.bias"), hg("mean_fc.blocks.2.bias"),
                          hg("log_var_fc.blocks.2.bias"), hg("mean_fc.blocks.0.bias")) \
                 if w.heads_bias else (None, 0, None, None, None, None, None)
+            # the heads' dW3 / dW2 (both heads) inside the heads kernel: the backward skips their
+            # four split-K GEMMs (and the kernel skips saving P2 / dOUT / dP2, read by nothing else)
+            w.heads_wgrad = bool(w.heads_bias and self.heads_wgrad and w.heads_wgws is not None)
+            mse_h = lt == 1
+            wg_args = (_p(w.heads_wgws), w.heads_wgws.numel() * 4, hg("mean_fc.blocks.4.weight"),
+                       None if mse_h else hg("log_var_fc.blocks.4.weight"), hg("mean_fc.blocks.2.weight"),
+                       None if mse_h else hg("log_var_fc.blocks.2.weight")) \
+                if w.heads_wgrad else (None, 0, None, None, None, None)
             with self._timed("heads"):
-                check(l.mlvae_heads_fused_ex(
+                check(l.mlvae_heads_fused_ex2(
                   B, T, Fd, C, 2 * H, lt, tr, _pb(w.rnn_out_bf), wb("decoder.mean_fc.blocks.0.weight"),
                   _pb(self.w1_t) if train else None, hp("mean_fc.blocks.0.bias"),
                   hp("mean_fc.blocks.2.weight"), hp("mean_fc.blocks.2.bias"),
@@ -851,8 +863,8 @@ class VAEEngine:
                   _p(w.dMUX) if train else None, _p(w.dLVX) if (train and lt == 0) else None,
                   _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
                   _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
-                  _p(w.ph), *bias_args, (3 if w.dy_bf16[cfg.L - 1] else 1) if w.heads_bias else 0, s),
-                  "heads_fused")
+                  _p(w.ph), *bias_args, (3 if w.dy_bf16[cfg.L - 1] else 1) if w.heads_bias else 0,
+                  *wg_args, s), "heads_fused")
             check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w
@@ -984,7 +996,8 @@ class VAEEngine:
                     self._mm(w, 1, 0, Fd, C, N, _p(dOut), Fd, _p(P2), C, gp(f"decoder.{hd}.blocks.4.weight"), C)
                 if not hb:
                     self._colsum(w, N, Fd, _p(dOut), Fd, gp(f"decoder.{hd}.blocks.4.bias"))
-            side(wg3)
+            if not getattr(w, "heads_wgrad", False):
+                side(wg3)
             if not fused:
                 self._mm(w, 0, 0, N, C, Fd, _p(dOut), Fd, W3, C, _p(dP2), C,
                          B_bf=wb(f"decoder.{hd}.blocks.4.weight"), epi=EPI_DLRELU, aux=_p(P2), ldaux=C)
@@ -998,7 +1011,8 @@ class VAEEngine:
                              gp(f"decoder.{hd}.blocks.2.weight"), C)
                 if not hb:
                     self._colsum(w, N, C, _p(dP2), C, gp(f"decoder.{hd}.blocks.2.bias"))
-            side(wg2)
+            if not getattr(w, "heads_wgrad", False):
+                side(wg2)
             if not fused:
                 self._mm(w, 0, 0, N, C, C, _p(dP2), C, W2, C, _p(w.dP1, off), 2 * C,
                          B_bf=wb(f"decoder.{hd}.blocks.2.weight"), epi=EPI_DLRELU,

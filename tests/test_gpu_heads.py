@@ -173,3 +173,73 @@ def test_heads_fused_bias_sums(loss_type, B, T, F, H2):
     # output above is bit-identical; its bias sums agree to fp32 rounding (1 ulp seen in tiles
     # with masked frames)
     assert rel_err(b1b[:C], first[:C]) < 1e-6
+
+
+@pytest.mark.parametrize("loss_type", [0, 1])
+@pytest.mark.parametrize("B,T,F,H2", [(3, 50, 80, 256), (5, 77, 64, 128), (40, 500, 80, 1024)])
+def test_heads_fused_weight_gradients(loss_type, B, T, F, H2):
+    """mlvae_heads_fused_ex2: dW3 = dOUT_h^T P2_h and dW2 = dP2_h^T P1_h of both heads, accumulated
+    inside the heads' middle kernel, against the fp64 products of the bf16 intermediates the split
+    form saves (the kernel's LDS images hold exactly those values) -- ragged tiles, masked frames,
+    N = 20,000 frames on the full persistent grid; mse writes nothing for the log_var head; the
+    other outputs are bit-identical to mlvae_heads_fused_ex's and two launches are bit-identical."""
+    need_gpu()
+    torch.manual_seed(B + T + F + loss_type + 7)
+    C, N = 64, B * T
+    l = lib()
+    f = dict(device="cuda", dtype=torch.float32)
+    Y = torch.randn(N, H2).to(torch.bfloat16).cuda()
+    W1 = (torch.randn(2 * C, H2) / math.sqrt(H2)).to(torch.bfloat16)
+    dW1, dW1t = W1.cuda(), W1.t().contiguous().cuda()
+    b1 = (torch.randn(2 * C) * 0.1).cuda()
+    W2 = [(torch.randn(C, C) / 8).cuda() for _ in range(2)]
+    b2 = [(torch.randn(C) * 0.1).cuda() for _ in range(2)]
+    W3 = [(torch.randn(F, C) / 8).cuda() for _ in range(2)]
+    b3 = [(torch.randn(F) * 0.1).cuda() for _ in range(2)]
+    x = torch.randn(N, F).cuda()
+    lens = torch.linspace(0.3, 1.0, B).cuda()
+    lik = loss_type == 0
+    ws = torch.zeros(l.mlvae_heads_bias_workspace_size(B, T, F, C) // 4 + 1, **f)
+    wgs = torch.zeros(l.mlvae_heads_wgrad_workspace_size(B, T, F, C) // 4 + 1, **f)
+    nan = lambda *s: torch.full(s, float("nan"), **f)
+
+    def run(wg):
+        o = {k: torch.zeros(N, n, device="cuda", dtype=torch.bfloat16)
+             for k, n in (("p1", 2 * C), ("p2m", C), ("p2v", C), ("dmux", F), ("dlvx", F),
+                          ("dp2m", C), ("dp2v", C), ("dp1", 2 * C))}
+        o.update(mux=torch.zeros(N, F, **f), lvx=torch.zeros(N, F, **f), dy=torch.zeros(N, H2, **f),
+                 parts=torch.zeros(l.mlvae_heads_partials_count(B, T), **f))
+        db = [nan(F), nan(F), nan(C), nan(C), nan(2 * C)]
+        dw = [nan(F, C), nan(F, C), nan(C, C), nan(C, C)]
+        wg_args = (P(wgs), wgs.numel() * 4, P(dw[0]), P(dw[1]) if lik else None, P(dw[2]),
+                   P(dw[3]) if lik else None) if wg else (None, 0, None, None, None, None)
+        check(l.mlvae_heads_fused_ex2(B, T, F, C, H2, loss_type, 1, Y.data_ptr(), dW1.data_ptr(),
+                                      dW1t.data_ptr(), P(b1), P(W2[0]), P(b2[0]), P(W3[0]), P(b3[0]),
+                                      P(W2[1]), P(b2[1]), P(W3[1]), P(b3[1]), P(x), P(lens), None, 0.7,
+                                      P(o["p1"]), P(o["p2m"]), P(o["p2v"]), P(o["mux"]), P(o["lvx"]),
+                                      P(o["dmux"]), P(o["dlvx"]) if lik else None, P(o["dp2m"]),
+                                      P(o["dp2v"]), P(o["dp1"]), P(o["dy"]), P(o["parts"]), P(ws),
+                                      ws.numel() * 4, *[P(t) for t in db], 1, *wg_args, stream()))
+        torch.cuda.synchronize()
+        return o, db, dw
+
+    ref, dbr, _ = run(False)
+    o, db, dw = run(True)
+    # outputs the fused form still writes: bit-identical
+    for k in ("p1", "mux", "lvx", "dy", "dp1", "parts"):
+        assert torch.equal(o[k], ref[k]), k
+    for a_, b_ in zip(db, dbr):
+        assert torch.equal(torch.nan_to_num(a_, 7.0), torch.nan_to_num(b_, 7.0))
+    d = lambda t: t.double()
+    heads = [(0, "p2m", "dmux", "dp2m")] + ([(1, "p2v", "dlvx", "dp2v")] if lik else [])
+    for h, p2, dout, dp2 in heads:
+        want3 = d(ref[dout]).t() @ d(ref[p2])
+        want2 = d(ref[dp2]).t() @ d(ref["p1"][:, h * C:(h + 1) * C])
+        assert rel_err(dw[h], want3) < 1e-5, (h, rel_err(dw[h], want3))
+        assert rel_err(dw[2 + h], want2) < 1e-5, (h, rel_err(dw[2 + h], want2))
+    if not lik:
+        assert torch.isnan(dw[1]).all() and torch.isnan(dw[3]).all()
+    first = [t.clone() for t in dw]
+    _, _, dw2 = run(True)
+    for a_, b_ in zip(first, dw2):
+        assert torch.equal(torch.nan_to_num(a_, 7.0), torch.nan_to_num(b_, 7.0))
