@@ -392,9 +392,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             }
             // a longer back-off thins the L2 poll traffic (3.27 -> 3.20 us/step at B = 256);
             // bit 18: the previous s_sleep(2)
-            if (a.dbg_mode & 262144) { /* bit 18 (A/B): no back-off */ }
-            else if (partial && (a.dbg_mode & (1 << 30))) __builtin_amdgcn_s_sleep(1);
-            else if (partial) __builtin_amdgcn_s_sleep(2);
+            if (partial && (a.dbg_mode & (1 << 30))) __builtin_amdgcn_s_sleep(1);
+            else if (partial || (a.dbg_mode & 262144)) __builtin_amdgcn_s_sleep(2);
             else __builtin_amdgcn_s_sleep(6);
           }
           LSTAMP(1);
@@ -798,7 +797,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
           break;
         }
         // BPTT: a shorter back-off (3.03 -> 2.97 us/step at B = 256); bit 18: s_sleep(2)
-        if (a.dbg_mode & 262144) { /* bit 18 (A/B): no back-off */ }
+        if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
         else __builtin_amdgcn_s_sleep(1);
       }
     }
