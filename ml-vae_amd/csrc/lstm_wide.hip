@@ -497,12 +497,22 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
           gr[t] = pack_bf16(hvals[t], h1, h2, h3, tag);
         }
-        if (AS && q == 0) {  // one 8-byte granule per tile
+        if (AS && q == 0) {
+          if constexpr (MT == 2) {
+            // the poller's two tiles are units 8 w .. 8 w + 7: adjacent granules, one 16-byte store
+            // (consecutive publish stores reach the consumers ~120 ns apart: see the BPTT's publish)
+            const int u0 = j0 + 4 * m0;
+            const u32x4 v = {(unsigned)gr[0], (unsigned)(gr[0] >> 32), (unsigned)gr[1], (unsigned)(gr[1] >> 32)};
+            const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7);
+            if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, cell * sizeof(short), 0, 0);
+            else st_sc1_b128(xr, cell * sizeof(short), v);
+          } else {  // one 8-byte granule per tile
 #pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            const int u0 = j0 + 4 * (m0 + t);
-            publish(xr, ((unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7)) * sizeof(short),
-                    gr[t], same_xcd);
+            for (int t = 0; t < MT; ++t) {
+              const int u0 = j0 + 4 * (m0 + t);
+              publish(xr, ((unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7)) * sizeof(short),
+                      gr[t], same_xcd);
+            }
           }
         } else if (q == 0) {
           const int u0 = j0 + 4 * TPW * wave;  // the wave's first unit
@@ -588,6 +598,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   static_assert(NPL >= 1 && CPG >= 1 && NPL * CPG == 2, "two 16-byte partial loads per lane");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LSTAMP_DECL;
+  RTS_DECL;
   char* aimg = smem;  // [2][16][4HJ] bf16 own dG, gate-major k = g*HJ + u, swizzled slots
   bf16x8* wlds = reinterpret_cast<bf16x8*>(smem + 2 * AIMG);  // [wave][NTW][KLB][lane]
   // cell inputs of a step, staged: [2][16 utt][ gates fp16 4*HJ (+16 B) | c_{t-1} HJ | dy HJ (fp32, +32 B) ]
@@ -641,6 +652,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * NJ, NJ, js, &placement) &&
                         !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) abort_flag = 0;
+  if (DBG && a.dbg && (a.dbg_mode & 8) && tid == 0) a.dbg[blockIdx.x] = same_xcd ? 1 : 2;  // (placement)
   __syncthreads();
 
   // exchange: [slot][consumer][producer][HJ units][16 utterances] bf16
@@ -803,6 +815,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     }
     LSTAMP(1);
     LWSTAMP();
+    RTS(8 + wave);
     // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
     // s+2's loads issued right behind this step's hand-off -- one program point per step, so
     // the loaded registers need no merge (and no wait for the loads)
@@ -908,17 +921,46 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
       const unsigned tag = step_tag_lg(s, nlg);
       const size_t sb = (size_t)(s & nmask) * xslot;
+      // TPW 1: two tiles per 16-byte store.  Consecutive publish stores of a wave reach the
+      // consumers ~120 ns apart (realtime stamps, tools/lstm_handoff.py --bwd: the consumer waves
+      // reading tile k saw their data ~120 k ns later, and reversing the store order reversed
+      // that), and the step's barrier waits for the last.  acc[nt] gives lane (bi, q) utterances
+      // 4q .. 4q+3 of unit nt*16 + bi; a row swap (v_permlane16_swap, q <-> q^1) of tiles A, B
+      // leaves lanes of even q with A's utterances 8(q>>1) .. +7 and odd q with B's -- the
+      // consumer's 16-byte chunk of one unit, so the exchange layout and the polls are unchanged.
+      // Same box, alternating (profiles/ab/r05_bwd_pair_publish.txt): c2 BPTT 0.968 -> 0.940 ms
+      // per launch, step 4.30 -> 4.22 ms; at TPW 2 (c3) 1.312 -> 1.33 (the first store then
+      // waits for the second tile, and the pair still lands 160 ns apart): one store per tile.
+      static_assert(NTW % 2 == 0, "tile pairs");
+      if constexpr (TPW != 1) {
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        // acc[nt][r]: partial dh of utterance 4q + r, unit n
-        const int n = (wave * NTW + nt) * 16 + bi;
+        for (int nt = 0; nt < NTW; ++nt) {
+          // acc[nt][r]: partial dh of utterance 4q + r, unit n
+          const int n = (wave * NTW + nt) * 16 + bi;
+          const int cons = n / HJ, un = n % HJ;
+          const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 4 * q;
+          publish(xr, (unsigned)(off * sizeof(short)),
+                  pack_bf16(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], tag), same_xcd);
+        }
+      } else {
+#pragma unroll
+      for (int pr = 0; pr < NTW / 2; ++pr) {
+        const int ta = 2 * pr, tb = 2 * pr + 1;
+        const unsigned long long ga = pack_bf16(acc[ta][0], acc[ta][1], acc[ta][2], acc[ta][3], tag);
+        const unsigned long long gb = pack_bf16(acc[tb][0], acc[tb][1], acc[tb][2], acc[tb][3], tag);
+        const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ga, (unsigned)gb, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ga >> 32), (unsigned)(gb >> 32), false, false);
+        const u32x4 v = {lo[0], hi[0], lo[1], hi[1]};
+        const int n = (wave * NTW + ((q & 1) ? tb : ta)) * 16 + bi;
         const int cons = n / HJ, un = n % HJ;
-        const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 4 * q;
-        publish(xr, (unsigned)(off * sizeof(short)),
-                pack_bf16(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], tag), same_xcd);
+        const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 8 * (q >> 1);
+        if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, (unsigned)(off * sizeof(short)), 0, 0);
+        else st_sc1_b128(xr, (unsigned)(off * sizeof(short)), v);
+      }
       }
     }
     LSTAMP(4);
+    RTS(wave);
     // dG of this step for the weight-gradient GEMMs: 16-byte rows out of the A-image
     // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|)
     if (!(a.dbg_mode & 1)) {
@@ -954,6 +996,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   for (int s = 0; s < T; ++s)
     if (!step(s)) break;
   LSTAMP_FLUSH();
+  RTS_FLUSH();
   if constexpr (F8) {  // this launch's max |dG| (the next step's fp8 scale): one atomic per wave
     float m = g8max;
 #pragma unroll
