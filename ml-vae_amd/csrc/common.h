@@ -46,6 +46,8 @@ __device__ __forceinline__ float tanh_fast(float x) {
 // The fp32 parity mode's cell math: libm-accurate.  tanh_fast loses relative accuracy near 0
 // (1 - 2/(2 + 2x) cancels: |err| ~ 1e-7 absolute, not relative), which made the fp32 mode's
 // rnn_out 6x further from fp64 than the fp32 oracle's (round 5, tools/parity_heads_dw1.py).
+// (With sigmoid_fast, a few ulp, and libm tanh only, one heads LeakyReLU-derivative flip came
+// back at the c3 test seed: both stay libm; the recurrence's time does not change measurably.)
 template <int PREC> __device__ __forceinline__ float sigmoid_p(float x) {
   if constexpr (PREC == PREC_F32) return 1.f / (1.f + expf(-x)); else return sigmoid_fast(x);
 }

@@ -89,8 +89,11 @@ __device__ __forceinline__ void store1(typename Lds<PREC>::T* dst, float v) {
   if constexpr (PREC == PREC_F32) *dst = v; else *dst = f2bf(v);
 }
 
+// TWO: the fp32 weight gradients' two-level accumulation (below); the extra accumulator set
+// would take the kernel past 256 VGPRs (one wave per SIMD: the fp32 mode's step 112 -> 141 ms),
+// so those instances are bounded to two workgroups per CU
 template <int BM, int BN, int PREC, bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, (PREC == PREC_F32 && TA) ? 2 : 1) void gemm_kernel(GemmArgs g) {
   typedef typename Lds<PREC>::T LT;
   constexpr int LDK = BK + Lds<PREC>::PAD;
   constexpr int WM = BM / 2, WN = BN / 2, MB = WM / 32, NB = WN / 32;
@@ -126,9 +129,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   // chain of kc / 2 accumulations (kc = 10,667 at B = 256) rounds ~sqrt(kc / 256) times worse
   // than the fp32 oracle's blocked sums (round 5, fp64-anchored whole-step test: dW_ih_l1 3.5x
   // the oracle's error at B = 32 before, tests/test_gpu_trajectory.py)
+  // Only the TA instances (the weight gradients: K = frames) run it -- the projections' and
+  // dgrads' K is the feature width (<= 4H)
   constexpr int KBLK = 256;
-  f32x16 tot[PREC == PREC_F32 ? MB : 1][PREC == PREC_F32 ? NB : 1];
-  if constexpr (PREC == PREC_F32) {
+  constexpr bool TWO = PREC == PREC_F32 && TA;
+  f32x16 tot[TWO ? MB : 1][TWO ? NB : 1];
+  if constexpr (TWO) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
             for (int j = 0; j < NB; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][e], b4[j][e], acc[i][j], 0, 0, 0);
       }
-      if ((k0 - kbeg + BK) % KBLK == 0 || k0 + BK >= kend) {  // fold the block (uniform)
+      if (TWO && ((k0 - kbeg + BK) % KBLK == 0 || k0 + BK >= kend)) {  // fold the block (uniform)
 #pragma unroll
         for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -244,7 +250,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  if constexpr (PREC == PREC_F32) {
+  if constexpr (TWO) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll

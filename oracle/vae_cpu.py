@@ -209,9 +209,32 @@ def bilstm(p, x, L, dropout_masks=None, impl="loop"):
     return h
 
 
-def fc_head(p, prefix, r):
-    """FCBlock([2H, fc, fc, F]) (ref:src/modules/fc_block.py:9-16): no end activation."""
-    h = lrelu(Fn.linear(r, p[prefix + ".blocks.0.weight"], p[prefix + ".blocks.0.bias"]))
+class _LReLUKink(torch.autograd.Function):
+    """LeakyReLU whose derivative takes the other branch where `flip` is set (test infrastructure
+    for the fp64-anchored parity tests: at a pre-activation within rounding of 0 either slope is
+    a valid derivative of the computed value, so an fp32 implementation that lands on the other
+    side of the kink is compared with the fp64 step that takes the same branch there)."""
+
+    @staticmethod
+    def forward(ctx, x, flip):
+        ctx.save_for_backward(x, flip)
+        return Fn.leaky_relu(x, NEG_SLOPE)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, flip = ctx.saved_tensors
+        pos = (x > 0) ^ flip
+        return g * torch.where(pos, torch.ones_like(g), torch.full_like(g, NEG_SLOPE)), None
+
+
+def fc_head(p, prefix, r, kink=None, pre_out=None):
+    """FCBlock([2H, fc, fc, F]) (ref:src/modules/fc_block.py:9-16): no end activation.
+    kink (tests): bool [.., fc] -- the first layer's LeakyReLU derivative branch flipped there;
+    pre_out (tests): dict receiving the first layer's pre-activation under `prefix`."""
+    pre = Fn.linear(r, p[prefix + ".blocks.0.weight"], p[prefix + ".blocks.0.bias"])
+    if pre_out is not None:
+        pre_out[prefix] = pre.detach()
+    h = lrelu(pre) if kink is None else _LReLUKink.apply(pre, kink)
     h = lrelu(Fn.linear(h, p[prefix + ".blocks.2.weight"], p[prefix + ".blocks.2.bias"]))
     return Fn.linear(h, p[prefix + ".blocks.4.weight"], p[prefix + ".blocks.4.bias"])
 
@@ -225,11 +248,13 @@ def recon_loss(mean, log_var, target, loss_type):
     raise ValueError(f"Invalid loss type: {loss_type}")
 
 
-def decoder_forward(p, z, x, L, loss_type, dropout_masks=None, impl="loop"):
+def decoder_forward(p, z, x, L, loss_type, dropout_masks=None, impl="loop", head_kink=None):
     r = bilstm(p, z, L, dropout_masks, impl)
-    mean = fc_head(p, "decoder.mean_fc", r)
-    log_var = fc_head(p, "decoder.log_var_fc", r)
-    return {"rnn_out": r, "mean": mean, "log_var": log_var,
+    kink = head_kink or {}
+    pre = {}
+    mean = fc_head(p, "decoder.mean_fc", r, kink.get("decoder.mean_fc"), pre)
+    log_var = fc_head(p, "decoder.log_var_fc", r, kink.get("decoder.log_var_fc"), pre)
+    return {"rnn_out": r, "mean": mean, "log_var": log_var, "p1_pre": pre,
             "losses": {"recon_loss": recon_loss(mean, log_var, x, loss_type)}}
 
 
@@ -251,7 +276,8 @@ def forward_loss(p, x, lens, eps, cfg, dropout_masks=None, impl="loop"):
     """compute_forward + compute_objectives (ref:src/models/test_vanilla_vae/model.py:19-55),
     normaliser omitted (identity)."""
     enc = encoder_forward(p, x, eps)
-    dec = decoder_forward(p, enc["sampled_h"], x, cfg["L"], cfg["loss_type"], dropout_masks, impl)
+    dec = decoder_forward(p, enc["sampled_h"], x, cfg["L"], cfg["loss_type"], dropout_masks, impl,
+                          cfg.get("head_kink"))
     kld = apply_lens_to_loss(enc["loss"], lens)
     rec = apply_lens_to_loss(dec["losses"]["recon_loss"], lens)
     w_kld, w_rec = loss_weights(["kld_loss", "recon_loss"],

@@ -53,15 +53,34 @@ def run_step(cfg, B, T, seed, lens, x=None):
     return eng, w, rec, new_ref, params
 
 
-def oracle_fp64(cfg, params, inputs):
+def oracle_fp64(cfg, params, inputs, head_kink=None):
     """The oracle's step in fp64 on the SAME fp32-representable parameters, inputs and randomness
     (promoted exactly): the truth both the engine and the fp32 oracle are measured against.  lens
-    stays fp32 -- length_to_mask's fp32 rel*T quirk is the reference's semantics, not rounding."""
+    stays fp32 -- length_to_mask's fp32 rel*T quirk is the reference's semantics, not rounding.
+    head_kink: {head prefix: bool [B, T, C]} -- the heads' first-layer LeakyReLU derivative
+    branch flipped there (kink_flips)."""
     x, lens, eps, masks = inputs
     p64 = OrderedDict((k, v.double()) for k, v in params.items())
     return O.train_step(p64, {}, x.double(), lens, eps.double(),
-                        dict(L=cfg.L, loss_type=cfg.loss_type, kld_weight=cfg.kld_weight),
+                        dict(L=cfg.L, loss_type=cfg.loss_type, kld_weight=cfg.kld_weight,
+                             head_kink=head_kink),
                         None if masks is None else masks.double(), impl="aten")
+
+
+HEADS = (("decoder.mean_fc", 0), ("decoder.log_var_fc", 1))
+
+
+def kink_flips(pre64, p1_signs, C):
+    """Where an fp32 computation of the heads' first layer landed on the other side of the
+    LeakyReLU kink than fp64: {prefix: bool [B, T, C]} (None: no flip).  pre64: the fp64
+    oracle's pre-activations (rec["out"]["dec"]["p1_pre"]); p1_signs: bool [B, T, 2C], the fp32
+    side's pre-activation > 0 (the engine's saved post-activation P1 has the same sign)."""
+    out = {}
+    for name, h in HEADS:
+        f = p1_signs[..., h * C:(h + 1) * C] != (pre64[name] > 0)
+        if f.any():
+            out[name] = f
+    return out or None
 
 
 def run_second_step(cfg, B, T, seed, lens):

@@ -13,14 +13,13 @@ randomness is the engine's own (in-kernel eps read back, dropout masks replayed 
   model that has learned, so the decoder's outputs decide it -- and the Adam update are compared:
   fp32 mode (the north-star "ELBO within 1e-4 relative" mode) <= 1e-4 at every step; bf16 mode
   <= BF16_ELBO (measured).
-* Free-running: the oracle trains its OWN copy from the same init for 100 steps, threading its own
-  Adam state.  Two fp32 implementations that round differently drift apart through the chaotic
-  training dynamics (Adam moves weights with tiny gradients by ~lr whichever way their sign falls),
-  so the oracle is run a second time on the batch in reverse utterance order (the same
-  mathematics, rounded differently at every step): the engine-vs-oracle ELBO gap must stay within
-  1e-4 while the dynamics are still smooth (the first 20 steps) and, later, within a small factor
-  of the gap between the oracle and itself -- a kernel error would show up as a gap far above
-  that intrinsic sensitivity.
+* Free-running, fp64-anchored (round 5): the engine and the fp32 oracle each train their OWN copy
+  from the same init for 100 steps, and the fp64 oracle a third on the same (exactly promoted)
+  inputs and randomness.  Two fp32 implementations that round differently drift apart through the
+  chaotic training dynamics, so each is measured against the fp64 truth, with a pre-registered
+  bound on the engine's drift relative to the fp32 oracle's (the test's docstring).
+* fp32 mode at the bench sizes, three-way: engine and fp32 oracle against fp64, every output and
+  gradient tensor (test_fp32_mode_whole_step_at_bench_sizes).
 
 The per-step curves are printed (DESIGN.md section 2 records them)."""
 from collections import OrderedDict
@@ -196,11 +195,16 @@ def test_fp32_mode_whole_step_at_bench_sizes(B_, seed):
     every gradient behind it.  The oracle has one such flip (log_var head) at this seed; the engine
     had one in the mean head while its fp32 recurrence used the hardware tanh (1 - 2/(1+e^2x),
     relatively inaccurate near 0: rnn_out 1.2e-6 from fp64).  With libm cell math in the fp32 mode
-    the engine has none (tools/parity_heads_dw1.py counts them) and every row is within 4e-7 of
-    fp64: asserted as an absolute 1e-6 bound too."""
+    the engine had none (tools/parity_heads_dw1.py counts them) and every row was within 4e-7
+    of fp64.  A flip is a branch decision at a non-differentiable point, not an accumulated
+    rounding error, and whether one occurs at a given seed changes with any rounding change
+    upstream (a GEMM's summation order brought one back): so each side's gradients are now
+    compared with the fp64 step that takes the same branches at its own flipped entries
+    (oracle.vae_cpu._LReLUKink; the flip counts are printed), and the bounds stand as
+    registered -- engine <= 3x oracle and <= 1e-6 absolute on every row."""
     need_gpu()
     from mlvae_hip.engine import VAEConfig
-    from step_parity import oracle_fp64
+    from step_parity import kink_flips, oracle_fp64
     cfg = VAEConfig(F=F, E=E, Z=Z, H=H, L=L, C=C, dropout=0.15, prec="fp32")
     Tn = 500
     lens = torch.linspace(0.6, 1.0, B_)
@@ -211,6 +215,18 @@ def test_fp32_mode_whole_step_at_bench_sizes(B_, seed):
     report(f"fp32 mode B={B_} T=500 vs fp32 oracle", e, grads)
     _, r64 = oracle_fp64(cfg, params, rec["inputs"])
     o64 = r64["out"]
+    # LeakyReLU kinks: where the engine's / the fp32 oracle's heads first-layer pre-activation
+    # fell on the other side of 0 than fp64's, their gradients are compared with the fp64 step
+    # taking the same branch there (kink_flips; each side against its own branch choices)
+    pre64 = o64["dec"]["p1_pre"]
+    sg_e = (w.P1.detach().cpu() > 0).view(B_, Tn, 2 * C)
+    pre32 = rec["out"]["dec"]["p1_pre"]
+    sg_o = torch.cat([pre32["decoder.mean_fc"] > 0, pre32["decoder.log_var_fc"] > 0], dim=-1)
+    fl_e, fl_o = kink_flips(pre64, sg_e, C), kink_flips(pre64, sg_o, C)
+    cnt = lambda f: {k.split(".")[1]: int(v.sum()) for k, v in (f or {}).items()}
+    print(f"[fp32 mode B={B_}] LeakyReLU-kink flips vs fp64: engine {cnt(fl_e)} fp32 oracle {cnt(fl_o)}")
+    g_e = r64["grads"] if fl_e is None else oracle_fp64(cfg, params, rec["inputs"], fl_e)[1]["grads"]
+    g_o = r64["grads"] if fl_o is None else oracle_fp64(cfg, params, rec["inputs"], fl_o)[1]["grads"]
     rel = lambda a, b: abs(float(a) - float(b)) / abs(float(b))
     outs = {"loss": (w.loss[2].item(), rec["out"]["loss"].item(), o64["loss"].item()),
             "kld_loss": (w.loss[0].item(), rec["out"]["kld_loss"].item(), o64["kld_loss"].item()),
@@ -221,7 +237,7 @@ def test_fp32_mode_whole_step_at_bench_sizes(B_, seed):
             "mu_x": (w.MUX.reshape(B_, Tn, -1), rec["out"]["dec"]["mean"], o64["dec"]["mean"]),
             "log_var_x": (w.LVX.reshape(B_, Tn, -1), rec["out"]["dec"]["log_var"], o64["dec"]["log_var"])}
     rows += [(k, norm_rel(a, t), norm_rel(b, t)) for k, (a, b, t) in tens.items()]
-    rows += [(k, norm_rel(g, r64["grads"][k]), norm_rel(rec["grads"][k], r64["grads"][k]))
+    rows += [(k, norm_rel(g, g_e[k]), norm_rel(rec["grads"][k], g_o[k]))
              for k, g in eng.named_grads().items()]
     print(f"[fp32 mode B={B_} T=500, error vs fp64] name: engine / fp32 oracle (ratio)")
     for k, a, b in rows:
