@@ -109,6 +109,23 @@ __device__ __forceinline__ int valid_frames(float rel_len, int T) {
   return c >= (float)T ? T : (int)c;
 }
 
+// Total valid frames for a workgroup: *count when given (data parallel: the all-reduced global
+// count), else summed by the whole workgroup -- integers, so exact in any order.  Every thread
+// must call it (two barriers); all get the result.  (A single thread walking B lengths serially
+// held every workgroup of the heads / encoder-backward kernels for ~128 dependent scalar loads.)
+__device__ __forceinline__ int block_frames(const float* lens, int B, int T, const int* count, int* sh) {
+  if (count) return *count;
+  if (threadIdx.x == 0) *sh = 0;
+  __syncthreads();
+  int c = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) c += valid_frames(lens[b], T);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(sh, c);
+  __syncthreads();
+  return *sh;
+}
+
 // DPP lane move of a float (row_mask = bank_mask = 0xf, bound_ctrl: out-of-row lanes read 0)
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {

@@ -284,11 +284,10 @@ __global__ __launch_bounds__(256) void encoder_bwd_kernel(EncBwdArgs a) {
       wmT[j][kk] = wfrag_t<false>(a.wml, EW, 16 * j + l15, kk, q);
       w1T[j][kk] = wfrag_t<true>(a.w1, EW, 16 * j + l15, kk, q);
     }
-  if (tid == 0) {
-    int c = 0;
-    if (a.count) c = *a.count;
-    else for (int b = 0; b < a.B; ++b) c += valid_frames(a.lens[b], a.T);
-    inv_count = c > 0 ? 1.f / ((float)c * (float)ZW) : 0.f;
+  {
+    __shared__ int cnt_sh;
+    const int c = block_frames(a.lens, a.B, a.T, a.count, &cnt_sh);
+    if (tid == 0) inv_count = c > 0 ? 1.f / ((float)c * (float)ZW) : 0.f;
   }
   __syncthreads();
   const float s_kl = a.kl_scale * inv_count;

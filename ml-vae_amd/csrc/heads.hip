@@ -245,11 +245,10 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
 
   // ---- stage 4: reconstruction loss, masked partial sum, gradient wrt (mu, log_var)
   __shared__ float inv_cnt;
-  if (tid == 0) {
-    int c = 0;
-    if (a.count) c = *a.count;
-    else for (int b = 0; b < a.B; ++b) c += valid_frames(a.lens[b], a.T);
-    inv_cnt = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
+  __shared__ int cnt_sh;
+  {
+    const int c = block_frames(a.lens, a.B, a.T, a.count, &cnt_sh);
+    if (tid == 0) inv_cnt = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
   }
   __syncthreads();  // also: all waves are past stage 1 (the staging aliases P2 / dOUT images)
   const bool lik = a.loss_type == 0;
@@ -451,11 +450,10 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
       sm[O_DO + h * RT * LF + (rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
     }
   }
-  if (tid == 0) {
-    int c = 0;
-    if (a.count) c = *a.count;
-    else for (int b = 0; b < a.B; ++b) c += valid_frames(a.lens[b], a.T);
-    inv_cnt = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
+  {
+    __shared__ int cnt_sh;
+    const int c = block_frames(a.lens, a.B, a.T, a.count, &cnt_sh);
+    if (tid == 0) inv_cnt = c > 0 ? 1.f / ((float)c * (float)F) : 0.f;
   }
 
   // a lane's share of its wave's 16 P1 rows (row l15 + 16 wave... as 4 x 16-byte chunks: chunk
