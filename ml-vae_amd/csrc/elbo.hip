@@ -317,13 +317,8 @@ __global__ __launch_bounds__(256) void masked_mean_bwd_kernel(int B, int T, int 
                                                               int reduction,
                                                               const float* __restrict__ g,
                                                               float* __restrict__ dloss) {
-  __shared__ int cnt;
-  if (threadIdx.x == 0) {
-    int c = 0;
-    for (int b = 0; b < B; ++b) c += valid_frames(lens[b], T);
-    cnt = c;
-  }
-  __syncthreads();
+  __shared__ int cnt_sh;
+  const int cnt = block_frames(lens, B, T, nullptr, &cnt_sh);
   const size_t total = (size_t)B * T * C;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     const int b = (int)(i / ((size_t)T * C)), t = (int)((i / C) % T);
