@@ -37,6 +37,8 @@ constexpr int WW = 8;  // waves per workgroup
 // consume them (the 2-chunk build read one fragment, waited for it and issued its two MFMAs, so
 // every k-chunk exposed an LDS round trip)
 constexpr int FWD_KLF = 4;
+// BPTT: the wave's tiles are multiplied and published in this many halves (below)
+constexpr int BPTT_HALVES = 2;
 #ifndef NT_AUX
 #define NT_AUX 2  // cache policy of the read-once activation streams (2 = nt)
 #endif
@@ -894,69 +896,75 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     LSTAMP(3);
     if (abort_flag) return false;
     if (s + 1 < T) {
-      f32x4 acc[NTW];
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // The A-fragments of a batch of BKB k-chunks are read before its MFMAs: left to itself the
-      // compiler issued each read one k-chunk ahead and waited for it (5 exposed LDS round trips
-      // per step at TPW 1).  (Round 5, measured and dropped: per-wave LDS flags instead of this
-      // barrier, each wave multiplying the k-chunks whose cell outputs were ready -- BPTT 1.36 ->
-      // 1.72 ms per launch at c3, 0.97 -> 1.19 at c2; profiles/r05_bptt_flags_stamps.txt)
-#pragma unroll
-      for (int k0 = 0; k0 < KC; k0 += BKB) {
-        bf16x8 afr[BKB];
-#pragma unroll
-        for (int i = 0; i < BKB; ++i)
-          afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
-        __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
-#pragma unroll
-        for (int i = 0; i < BKB; ++i) {
-          const int kc = k0 + i;
-#pragma unroll
-          for (int nt = 0; nt < NTW; ++nt) {
-            const bf16x8 wf = kc < KR ? wreg[nt][kc < KR ? kc : 0] : wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wf, acc[nt], 0, 0, 0);
-          }
-        }
-      }
       const unsigned tag = step_tag_lg(s, nlg);
       const size_t sb = (size_t)(s & nmask) * xslot;
-      // TPW 1: two tiles per 16-byte store.  Consecutive publish stores of a wave reach the
-      // consumers ~120 ns apart (realtime stamps, tools/lstm_handoff.py --bwd: the consumer waves
-      // reading tile k saw their data ~120 k ns later, and reversing the store order reversed
-      // that), and the step's barrier waits for the last.  acc[nt] gives lane (bi, q) utterances
-      // 4q .. 4q+3 of unit nt*16 + bi; a row swap (v_permlane16_swap, q <-> q^1) of tiles A, B
-      // leaves lanes of even q with A's utterances 8(q>>1) .. +7 and odd q with B's -- the
-      // consumer's 16-byte chunk of one unit, so the exchange layout and the polls are unchanged.
-      // Same box, alternating (profiles/ab/r05_bwd_pair_publish.txt): c2 BPTT 0.968 -> 0.940 ms
-      // per launch, step 4.30 -> 4.22 ms; at TPW 2 (c3) 1.312 -> 1.33 (the first store then
-      // waits for the second tile, and the pair still lands 160 ns apart): one store per tile.
-      static_assert(NTW % 2 == 0, "tile pairs");
-      if constexpr (TPW != 1) {
+      // The wave's NTW tiles in halves, each half's products then its publish: the first half's
+      // stores go out while the second half's MFMAs run, so the last tile's store no longer
+      // queues behind all the others (consecutive publish stores of a wave become visible ~120 ns
+      // apart: realtime stamps, tools/lstm_handoff.py --bwd; the step barrier waits for the
+      // consumer wave whose tile landed last).  The A-fragments are read once per half.
+      static_assert(NTW % (2 * BPTT_HALVES) == 0, "tile pairs per half");
+      constexpr int TPH = NTW / BPTT_HALVES;
 #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-          // acc[nt][r]: partial dh of utterance 4q + r, unit n
-          const int n = (wave * NTW + nt) * 16 + bi;
-          const int cons = n / HJ, un = n % HJ;
-          const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 4 * q;
-          publish(xr, (unsigned)(off * sizeof(short)),
-                  pack_bf16(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3], tag), same_xcd);
+      for (int hf = 0; hf < BPTT_HALVES; ++hf) {
+        f32x4 acc[TPH];
+#pragma unroll
+        for (int t = 0; t < TPH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // The A-fragments of a batch of BKB k-chunks are read before its MFMAs: left to itself the
+        // compiler issued each read one k-chunk ahead and waited for it (5 exposed LDS round trips
+        // per step at TPW 1).  (Round 5, measured and dropped: per-wave LDS flags instead of this
+        // barrier, each wave multiplying the k-chunks whose cell outputs were ready -- BPTT 1.36 ->
+        // 1.72 ms per launch at c3, 0.97 -> 1.19 at c2; profiles/r05_bptt_flags_stamps.txt)
+#pragma unroll
+        for (int k0 = 0; k0 < KC; k0 += BKB) {
+          bf16x8 afr[BKB];
+#pragma unroll
+          for (int i = 0; i < BKB; ++i)
+            afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
+          __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
+#pragma unroll
+          for (int i = 0; i < BKB; ++i) {
+            const int kc = k0 + i;
+#pragma unroll
+            for (int t = 0; t < TPH; ++t) {
+              const int nt = hf * TPH + t;
+              const bf16x8 wf = kc < KR ? wreg[nt][kc < KR ? kc : 0] : wlds[((wave * NTW + nt) * KLB + (kc - KR)) * 64 + lane];
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i], wf, acc[t], 0, 0, 0);
+            }
+          }
         }
-      } else {
+        // TPW 1: two tiles per 16-byte store.  acc[t] gives lane (bi, q) utterances 4q .. 4q+3 of
+        // unit nt*16 + bi; a row swap (v_permlane16_swap, q <-> q^1) of tiles A, B leaves lanes of
+        // even q with A's utterances 8(q>>1) .. +7 and odd q with B's -- the consumer's 16-byte
+        // chunk of one unit, so the exchange layout and the polls are unchanged.  Same box,
+        // alternating (profiles/ab/r05_bwd_pair_publish.txt): c2 BPTT 0.968 -> 0.940 ms per
+        // launch; at TPW 2 (c3) 1.312 -> 1.33 (the pair still lands 160 ns apart): one store per tile.
+        if constexpr (TPW != 1) {
 #pragma unroll
-      for (int pr = 0; pr < NTW / 2; ++pr) {
-        const int ta = 2 * pr, tb = 2 * pr + 1;
-        const unsigned long long ga = pack_bf16(acc[ta][0], acc[ta][1], acc[ta][2], acc[ta][3], tag);
-        const unsigned long long gb = pack_bf16(acc[tb][0], acc[tb][1], acc[tb][2], acc[tb][3], tag);
-        const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ga, (unsigned)gb, false, false);
-        const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ga >> 32), (unsigned)(gb >> 32), false, false);
-        const u32x4 v = {lo[0], hi[0], lo[1], hi[1]};
-        const int n = (wave * NTW + ((q & 1) ? tb : ta)) * 16 + bi;
-        const int cons = n / HJ, un = n % HJ;
-        const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 8 * (q >> 1);
-        if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, (unsigned)(off * sizeof(short)), 0, 0);
-        else st_sc1_b128(xr, (unsigned)(off * sizeof(short)), v);
-      }
+          for (int t = 0; t < TPH; ++t) {
+            // acc[t][r]: partial dh of utterance 4q + r, unit n
+            const int n = (wave * NTW + hf * TPH + t) * 16 + bi;
+            const int cons = n / HJ, un = n % HJ;
+            const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 4 * q;
+            publish(xr, (unsigned)(off * sizeof(short)),
+                    pack_bf16(acc[t][0], acc[t][1], acc[t][2], acc[t][3], tag), same_xcd);
+          }
+        } else {
+#pragma unroll
+          for (int pr = 0; pr < TPH / 2; ++pr) {
+            const int ta = 2 * pr, tb = 2 * pr + 1;
+            const unsigned long long ga = pack_bf16(acc[ta][0], acc[ta][1], acc[ta][2], acc[ta][3], tag);
+            const unsigned long long gb = pack_bf16(acc[tb][0], acc[tb][1], acc[tb][2], acc[tb][3], tag);
+            const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ga, (unsigned)gb, false, false);
+            const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ga >> 32), (unsigned)(gb >> 32), false, false);
+            const u32x4 v = {lo[0], hi[0], lo[1], hi[1]};
+            const int n = (wave * NTW + hf * TPH + ((q & 1) ? tb : ta)) * 16 + bi;
+            const int cons = n / HJ, un = n % HJ;
+            const size_t off = sb + (((size_t)cons * NJ + js) * HJ + un) * 16 + 8 * (q >> 1);
+            if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, (unsigned)(off * sizeof(short)), 0, 0);
+            else st_sc1_b128(xr, (unsigned)(off * sizeof(short)), v);
+          }
+        }
       }
     }
     LSTAMP(4);

@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 shift 3
 VARS=("$@")
-REPS=2
+REPS=${REPS:-2}
 [ ${#VARS[@]} -eq 0 ] && { VARS=("MLVAE_NONE=0"); REPS=1; }
 if [ "$PYT" != "-" ]; then
   timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $PYT \
