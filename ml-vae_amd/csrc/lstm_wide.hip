@@ -37,8 +37,9 @@ constexpr int WW = 8;  // waves per workgroup
 // consume them (the 2-chunk build read one fragment, waited for it and issued its two MFMAs, so
 // every k-chunk exposed an LDS round trip)
 constexpr int FWD_KLF = 4;
-// BPTT: the wave's tiles are multiplied and published in this many halves (below)
-constexpr int BPTT_HALVES = 2;
+// BPTT: the wave's tiles are multiplied and published in this many groups (below): halves
+// (single tiles at TPW 2, the A-fragments then read 4 times: c3 BPTT 1.27 -> 1.35 ms per launch)
+template <int TPW> constexpr int bptt_groups() { return 2; }
 #ifndef NT_AUX
 #define NT_AUX 2  // cache policy of the read-once activation streams (2 = nt)
 #endif
@@ -903,10 +904,11 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       // queues behind all the others (consecutive publish stores of a wave become visible ~120 ns
       // apart: realtime stamps, tools/lstm_handoff.py --bwd; the step barrier waits for the
       // consumer wave whose tile landed last).  The A-fragments are read once per half.
-      static_assert(NTW % (2 * BPTT_HALVES) == 0, "tile pairs per half");
-      constexpr int TPH = NTW / BPTT_HALVES;
+      constexpr int NGRP = bptt_groups<TPW>();
+      static_assert(NTW % NGRP == 0 && (TPW != 1 || (NTW / NGRP) % 2 == 0), "tile groups");
+      constexpr int TPH = NTW / NGRP;
 #pragma unroll
-      for (int hf = 0; hf < BPTT_HALVES; ++hf) {
+      for (int hf = 0; hf < NGRP; ++hf) {
         f32x4 acc[TPH];
 #pragma unroll
         for (int t = 0; t < TPH; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
