@@ -287,16 +287,19 @@ __global__ __launch_bounds__(512) void skinny_dzw_kernel(int M, int K8, const un
     if (f < M) v = *reinterpret_cast<const u32x4*>(Zb + (size_t)f * ldz + 8 * c8);
     *reinterpret_cast<u32x4*>(sz + r * DZW_LZ + 8 * c8) = v;
   }
-  // dG tile loads: 128 rows x 32 16-byte pieces = 4096 pieces, 8 per thread
-  u32x4 va[8];
-  auto aload = [&](int c, int rb) {
+  // dG tile loads: 128 rows x 32 16-byte pieces = 4096 pieces, 8 per thread.  Tiles in the order
+  // (chunk c, row block rb), two register buffers: tile i+2's loads are issued while tile i is
+  // multiplied (one tile ahead left each tile waiting ~one HBM latency: 3.9 TB/s at c3)
+  const int ntl = nch * nrb;
+  auto aload = [&](u32x4 (&va)[8], int ti) {
+    const int c = ti / nrb, rb = ti - c * nrb;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int idx = tid + 512 * i, r = idx >> 5, c8 = idx & 31, f = (rb0 + rb) * 128 + r;
       va[i] = f < M ? *reinterpret_cast<const u32x4*>(A + (size_t)f * lda + c * DZW_KC + 8 * c8) : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  auto astore = [&]() {
+  auto astore = [&](const u32x4 (&va)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int idx = tid + 512 * i, r = idx >> 5, c8 = idx & 31;
@@ -307,68 +310,74 @@ __global__ __launch_bounds__(512) void skinny_dzw_kernel(int M, int K8, const un
 #pragma unroll
   for (int b = 0; b < DZW_NRB; ++b) adz[b][0] = adz[b][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, i4 = lane & 15, qq = i4 >> 2, pp = i4 & 3;
-  aload(0, 0);
-  for (int c = 0; c < nch; ++c) {
-    f32x4 aw[2][3];  // dW^T tiles: m-tiles wave, wave + 8 of the chunk's 16; n-tiles 0..2
+  f32x4 aw[2][3];  // dW^T tiles of the current chunk: m-tiles wave, wave + 8 of its 16; n-tiles 0..2
+  auto tile = [&](int ti, u32x4 (&va)[8]) {
+    const int c = ti / nrb, rb = ti - c * nrb;
+    if (rb == 0) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) aw[t][0] = aw[t][1] = aw[t][2] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int rb = 0; rb < nrb; ++rb) {
-      __syncthreads();  // the previous tile's (and chunk's) LDS reads are done
-      astore();
-      if (rb == 0) {  // this chunk's W_ih^T rows: 32 x 256
-        for (int i = tid; i < DZW_Z * (DZW_KC / 8); i += 512) {
-          const int r = i / (DZW_KC / 8), c8 = i % (DZW_KC / 8);
-          *reinterpret_cast<u32x4*>(sw + r * DZW_LA + 8 * c8) =
-              *reinterpret_cast<const u32x4*>(Wt + (size_t)r * ldw + c * DZW_KC + 8 * c8);
-        }
-      }
-      __syncthreads();
-      // next tile in flight under this one's MFMAs
-      if (rb + 1 < nrb) aload(c, rb + 1);
-      else if (c + 1 < nch) aload(c + 1, 0);
-      // dZ[rows 16 wave .. +15 of block rb][32] += tile . W_ih  (swapped: lane holds z 16 j + 4 q + r)
-#pragma unroll
-      for (int u = 0; u < DZW_KC / 32; ++u) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(sa + (16 * wave + l15) * DZW_LA + 32 * u + 8 * q);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(sw + (16 * j + l15) * DZW_LA + 32 * u + 8 * q);
-#pragma unroll
-          for (int b = 0; b < DZW_NRB; ++b)
-            if (b == rb) adz[b][j] = mfma16(bw, af, adz[b][j]);
-        }
-      }
-      // dW^T[chunk cols][NB] += tile^T . [z | 1]  (transposed reads over the 128 frames)
-      const short* zb = sz + rb * 128 * DZW_LZ;
-#pragma unroll
-      for (int kk = 0; kk < 128; kk += 32) {
-        const int r1 = kk + 8 * g + qq, r2 = r1 + 4;
-        bf16x8 bz[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(zb + r1 * DZW_LZ + 16 * j + 4 * pp));
-          const bf16x4 b2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(zb + r2 * DZW_LZ + 16 * j + 4 * pp));
-          bz[j] = bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int m0 = 16 * (wave + 8 * t);
-          const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r1 * DZW_LA + m0 + 4 * pp));
-          const bf16x4 a2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r2 * DZW_LA + m0 + 4 * pp));
-          const bf16x8 af = {a1[0], a1[1], a1[2], a1[3], a2[0], a2[1], a2[2], a2[3]};
-#pragma unroll
-          for (int j = 0; j < 3; ++j) aw[t][j] = mfma16(bz[j], af, aw[t][j]);  // lane: P[m][16 j + 4 q + r]
-        }
+      for (int t = 0; t < 2; ++t) aw[t][0] = aw[t][1] = aw[t][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();  // the previous tile's (and chunk's) LDS reads are done
+    astore(va);
+    if (rb == 0) {  // this chunk's W_ih^T rows: 32 x 256
+      for (int i = tid; i < DZW_Z * (DZW_KC / 8); i += 512) {
+        const int r = i / (DZW_KC / 8), c8 = i % (DZW_KC / 8);
+        *reinterpret_cast<u32x4*>(sw + r * DZW_LA + 8 * c8) =
+            *reinterpret_cast<const u32x4*>(Wt + (size_t)r * ldw + c * DZW_KC + 8 * c8);
       }
     }
-    // this chunk's slab rows: slab[blockIdx.x][c * 256 + m][NB]
+    __syncthreads();
+    if (ti + 2 < ntl) aload(va, ti + 2);  // two tiles ahead, into the buffer just staged
+    // dZ[rows 16 wave .. +15 of block rb][32] += tile . W_ih  (swapped: lane holds z 16 j + 4 q + r)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int m = c * DZW_KC + 16 * (wave + 8 * t) + l15;
-      float* out = slabs + ((size_t)blockIdx.x * K8 + m) * DZW_NB;
+    for (int u = 0; u < DZW_KC / 32; ++u) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(sa + (16 * wave + l15) * DZW_LA + 32 * u + 8 * q);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) *reinterpret_cast<f32x4*>(out + 16 * j + 4 * q) = aw[t][j];
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 bw = *reinterpret_cast<const bf16x8*>(sw + (16 * j + l15) * DZW_LA + 32 * u + 8 * q);
+#pragma unroll
+        for (int b = 0; b < DZW_NRB; ++b)
+          if (b == rb) adz[b][j] = mfma16(bw, af, adz[b][j]);
+      }
     }
+    // dW^T[chunk cols][NB] += tile^T . [z | 1]  (transposed reads over the 128 frames)
+    const short* zb = sz + rb * 128 * DZW_LZ;
+#pragma unroll
+    for (int kk = 0; kk < 128; kk += 32) {
+      const int r1 = kk + 8 * g + qq, r2 = r1 + 4;
+      bf16x8 bz[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const bf16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(zb + r1 * DZW_LZ + 16 * j + 4 * pp));
+        const bf16x4 b2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(zb + r2 * DZW_LZ + 16 * j + 4 * pp));
+        bz[j] = bf16x8{b1[0], b1[1], b1[2], b1[3], b2[0], b2[1], b2[2], b2[3]};
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int m0 = 16 * (wave + 8 * t);
+        const bf16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r1 * DZW_LA + m0 + 4 * pp));
+        const bf16x4 a2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_b4_p)(sa + r2 * DZW_LA + m0 + 4 * pp));
+        const bf16x8 af = {a1[0], a1[1], a1[2], a1[3], a2[0], a2[1], a2[2], a2[3]};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) aw[t][j] = mfma16(bz[j], af, aw[t][j]);  // lane: P[m][16 j + 4 q + r]
+      }
+    }
+    if (rb == nrb - 1) {  // this chunk's slab rows: slab[blockIdx.x][c * 256 + m][NB]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int m = c * DZW_KC + 16 * (wave + 8 * t) + l15;
+        float* out = slabs + ((size_t)blockIdx.x * K8 + m) * DZW_NB;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<f32x4*>(out + 16 * j + 4 * q) = aw[t][j];
+      }
+    }
+  };
+  u32x4 v0[8], v1[8];
+  aload(v0, 0);
+  if (ntl > 1) aload(v1, 1);
+  for (int ti = 0; ti < ntl; ti += 2) {
+    tile(ti, v0);
+    if (ti + 1 < ntl) tile(ti + 1, v1);
   }
 #pragma unroll
   for (int b = 0; b < DZW_NRB; ++b) {
