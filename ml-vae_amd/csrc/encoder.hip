@@ -251,14 +251,16 @@ int bwd_grid(int N) {
   // cap on workgroups (each folds its tiles into one weight-gradient slab); MLVAE_ENC_BWD_GRID
   // overrides it for A/B timing
   // default: 128 workgroups, which leave CUs to the weight-gradient GEMM beside it when the
-  // recurrence does not fill the chip (c2: 128 -> 256 costs 0.03 ms/step); 512 at B*T >= 64K
-  // frames, where the tail runs serialised on the whole chip (c3: 12.2 -> 12.0 ms/step)
+  // recurrence does not fill the chip (c2: 128 -> 256 costs 0.03 ms/step); 256 at B*T >= 64K
+  // frames, where the tail runs serialised on the whole chip (round 5, c3 same box: 512 / 256 /
+  // 1024 workgroups 75 / 65 / 97 us -- per-workgroup fixed costs (resident weight fragments,
+  // the slab) against the tiles each folds in; round 3 had measured 512 over 128)
   static const int env = [] {
     const char* e = getenv("MLVAE_ENC_BWD_GRID");
     return e ? atoi(e) : 0;
   }();
   const int tiles = (N + 63) / 64;
-  const int cap = env >= 1 ? env : (tiles >= 1024 ? 512 : 128);
+  const int cap = env >= 1 ? env : (tiles >= 1024 ? 256 : 128);
   return tiles > cap ? cap : (tiles < 1 ? 1 : tiles);
 }
 
