@@ -665,6 +665,14 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 
   // reduce-scatter / cell role: 8-lane group gq, lane pg; combo cb -> (unit uc, half);
   // after the reduce lane pg holds utterance half*8 + pg
+  // The reduce-scatter needs no selects: every lane keeps its low register slots and adds the
+  // partner's high ones (half-row mirror, then xor 2, xor 1), so lane pg of a group must hold the
+  // partial of utterance e in slot e ^ rs_perm(pg).  The producer arranges that for free: its
+  // A-image row of utterance u is row u ^ rs_perm(js / NPL), so the MFMA writes the partials of the
+  // consumer lane that loads them in that lane's order.  After the reduce lane pg holds utterance
+  // half * 8 + rs_perm(pg).
+  auto rs_perm = [](int g) { return g ^ ((g & 4) ? 3 : 0); };
+  const int arow = rs_perm(js / NPL);  // A-image row of utterance u: u ^ arow
   const int gq = tid >> 3, pg = lane & 7;
   int uc[CPG], cu[CPG];
   bool bv[CPG];
@@ -672,7 +680,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   for (int ci = 0; ci < CPG; ++ci) {
     const int cb = gq * CPG + ci;
     uc[ci] = cb >> 1;
-    cu[ci] = (cb & 1) * 8 + pg;
+    cu[ci] = (cb & 1) * 8 + rs_perm(pg);
     bv[ci] = grp * BG + cu[ci] < a.B;
   }
   // Cell inputs (gates, c_{t-1}, dy) of step s_ in 16-byte row chunks -- whole 128-byte lines
@@ -817,7 +825,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
     }
     LSTAMP(1);
-    LWSTAMP();
+    // per-wave stamps (slots 8 + wave): poll done, or (debug bit 21) reduce done, (bit 22) the
+    // cell's A-image writes issued, just before the step barrier
+    if (!(a.dbg_mode & (3 << 21))) LWSTAMP();
     RTS(8 + wave);
     // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
     // s+2's loads issued right behind this step's hand-off -- one program point per step, so
@@ -833,38 +843,32 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     if (!late_pf) load_cell(s + 2);
     LSTAMP(6);
     if (s > 0) {
-      const bool b2 = pg & 4, b1 = pg & 2, b0 = pg & 1;
 #pragma unroll
       for (int ci = 0; ci < CPG; ++ci) {
         float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        for (int d = 0; d < 4; ++d) {
+          v[2 * d] = __uint_as_float(pv[ci][0][d] << 16);
+          v[2 * d + 1] = __uint_as_float(pv[ci][0][d] & 0xffff0000u);
+        }
 #pragma unroll
-        for (int i = 0; i < NPL; ++i)
+        for (int i = 1; i < NPL; ++i)
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
             v[2 * d] += __uint_as_float(pv[ci][i][d] << 16);
             v[2 * d + 1] += __uint_as_float(pv[ci][i][d] & 0xffff0000u);
           }
-        // reduce-scatter over the 8 lanes (DPP row_shr/shl:4, quad_perm xor 2 / xor 1)
+        // reduce-scatter over the 8 lanes: DPP row_half_mirror, quad_perm xor 2, quad_perm xor 1
         float w4[4], w2[2];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float send = b2 ? v[k] : v[k + 4], keep = b2 ? v[k + 4] : v[k];
-          const float from_lo = dpp_f<0x114>(send);
-          const float from_hi = dpp_f<0x104>(send);
-          w4[k] = keep + (b2 ? from_lo : from_hi);
-        }
+        for (int k = 0; k < 4; ++k) w4[k] = v[k] + dpp_f<0x141>(v[k + 4]);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const float send = b1 ? w4[k] : w4[k + 2], keep = b1 ? w4[k + 2] : w4[k];
-          w2[k] = keep + dpp_f<0x4E>(send);
-        }
-        const float send = b0 ? w2[0] : w2[1], keep = b0 ? w2[1] : w2[0];
-        dh[ci] = keep + dpp_f<0xB1>(send);
+        for (int k = 0; k < 2; ++k) w2[k] = w4[k] + dpp_f<0x4E>(w4[k + 2]);
+        dh[ci] = w2[0] + dpp_f<0xB1>(w2[1]);
       }
     }
     LSTAMP(2);
+    if (a.dbg_mode & (1 << 21)) LWSTAMP();
     // cell BPTT -> dG of (utterance cu, unit uc), into the A-image of this step
     char* ab = aimg + (s & 1) * AIMG;
 #pragma unroll
@@ -884,7 +888,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
       cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
       bsum[ci][0] += d0; bsum[ci][1] += d1; bsum[ci][2] += d2; bsum[ci][3] += d3;
-      const int u = uc[ci], r = cu[ci];
+      const int u = uc[ci], r = cu[ci] ^ arow;
       const float dg[4] = {d0, d1, d2, d3};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -892,7 +896,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         *reinterpret_cast<short*>(ab + r * ROWB + swz(r, k >> 3) * 16 + (k & 7) * 2) = f2bf(dg[g]);
       }
     }
+    if (a.dbg_mode & (1 << 22)) LWSTAMP();
     __syncthreads();  // double-buffered A-image: one barrier per step
+    LSTAMP(7);
     if (late_pf) load_cell(s + 2);
     LSTAMP(3);
     if (abort_flag) return false;
@@ -978,7 +984,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       const int t = dir ? s : T - 1 - s;
       for (int sl = tid; sl < NSL; sl += 512) {
         const int r = sl / (4 * HJ / 8), kslot = sl % (4 * HJ / 8);
-        const int b = grp * BG + r;
+        const int b = grp * BG + (r ^ arow);
         if (b >= a.B) continue;
         const int k = kslot * 8, g = k / HJ, u = k % HJ;
         const u32x4 v = *reinterpret_cast<const u32x4*>(ab + r * ROWB + swz(r, kslot) * 16);

@@ -7,7 +7,7 @@ Phases (wide kernels; stamps of steps 64..95 buffered in LDS, lstm_common.h LSTA
   fwd: 0 step start | 1 poll done | 2 barrier | 3 MFMA issued | 4 cell + publish | 6 out ring |
        7 drop bits (5: publish ack, debug bit 23)
   bwd: 0 step start | 1 poll done | 5 cell inputs staged | 6 prefetch issued | 2 reduce done |
-       3 barrier | 4 MFMA + publish
+       7 barrier | 3 prefetch issued (late, full-chip grids) | 4 MFMA + publish
 """
 import argparse
 import ctypes
@@ -76,7 +76,7 @@ def main():
     w0, wn = 64, 32
     w = d[w0:w0 + wn]
     names = ({1: "poll done", 5: "cell inputs staged", 6: "prefetch issued", 2: "reduce done",
-              3: "barrier", 4: "MFMA + publish"} if a.bwd else
+              7: "barrier", 3: "prefetch issued (late)", 4: "MFMA + publish"} if a.bwd else
              {1: "poll done", 2: "barrier", 3: "MFMA issued", 4: "cell + publish", 5: "publish ack",
               6: "out ring", 7: "drop bits"})
     order = sorted((b for b in names if (w[:, b] != 0).all()),
@@ -96,7 +96,11 @@ def main():
     else:
         wv = [(w[:, 8 + k] - w[:, 0]).median().item() for k in range(8) if (w[:, 8 + k] != 0).all()]
     if wv:
-        print("per-wave poll done   " + " ".join(f"w{k}:{v:.0f}" for k, v in enumerate(wv)))
+        what = ("reduce done" if a.mode & (1 << 21) else "pre-barrier" if a.mode & (1 << 22) else "poll done")
+        print(f"per-wave {what:11s} " + " ".join(f"w{k}:{v:.0f}" for k, v in enumerate(wv)))
+        if len(wv) == 8:
+            mx = (w[:, 8:16].max(dim=1).values - w[:, 0]).median().item()
+            print(f"{'':20s} slowest wave per step: median {mx:.0f}")
     per = w[1:, 0] - w[:-1, 0]
     print(f"{'step period':20s} median {per.median().item():7.0f} ticks  mean {per.mean().item():7.0f}")
     last = order[-1] if order else 0
