@@ -787,6 +787,26 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     float dh[CPG];
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) dh[ci] = 0.f;
+    // The cell's factors that do not depend on the incoming dh (everything but three FMAs and
+    // four products per cell) are formed while the first poll's loads are in flight, off the
+    // hand-off's critical path:  dcs = dc + dht * fA,  dG = dcs * (f0, f1, f2) and dht * f3,
+    // dc' = dcs * fF  (padded utterances: all zero, so their dG and dc stay 0)
+    float fA[CPG], fF[CPG], f0[CPG], f1[CPG], f2[CPG], f3[CPG];
+    auto factors = [&]() {
+#pragma unroll
+      for (int ci = 0; ci < CPG; ++ci) {
+        const float cpv = s + 1 < T ? xcp[ci] : 0.f;  // c_{t-1}; none at the sequence start
+        const float tc = tanh_fast(cc[ci]);
+        const bool v = bv[ci];
+        fA[ci] = v ? xo[ci] * (1.f - tc * tc) : 0.f;
+        fF[ci] = v ? xf[ci] : 0.f;
+        f0[ci] = v ? xgg[ci] * xi[ci] * (1.f - xi[ci]) : 0.f;
+        f1[ci] = v ? cpv * xf[ci] * (1.f - xf[ci]) : 0.f;
+        f2[ci] = v ? xi[ci] * (1.f - xgg[ci] * xgg[ci]) : 0.f;
+        f3[ci] = v ? tc * xo[ci] * (1.f - xo[ci]) : 0.f;
+        cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
+      }
+    };
     u32x4 pv[CPG][NPL];
     // Step s+1's cell inputs are staged to LDS while the first poll's loads are in flight
     // instead of after the poll (same box, c3: BPTT 1.292 / 1.283 -> 1.269 / 1.260 ms per
@@ -798,8 +818,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       const unsigned tag = step_tag_lg(s - 1, nlg);
       const size_t sb = (size_t)((s - 1) & nmask) * xslot + (size_t)js * NJ * HJ * 16;
       unsigned spins = 0;
-      // (re-loading only the stale partial tiles measured no faster here: full sweeps)
-      while (true) {
+      auto sweep = [&]() {
 #pragma unroll
         for (int ci = 0; ci < CPG; ++ci)
 #pragma unroll
@@ -808,7 +827,12 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
             const size_t off = sb + ((size_t)p * HJ + uc[ci]) * 16 + (cu[ci] >> 3) * 8;
             pv[ci][i] = ld_sc1_b128(xr, (unsigned)(off * sizeof(short)));
           }
-        if (early_stage && spins == 0) stage_cell(s + 1);
+      };
+      // (re-loading only the stale partial tiles measured no faster here: full sweeps)
+      sweep();
+      factors();
+      if (early_stage) stage_cell(s + 1);
+      while (true) {
         bool ok = true;
 #pragma unroll
         for (int ci = 0; ci < CPG; ++ci)
@@ -822,7 +846,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         // BPTT: a shorter back-off (3.03 -> 2.97 us/step at B = 256); bit 18: s_sleep(2)
         if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
         else __builtin_amdgcn_s_sleep(1);
+        sweep();
       }
+    } else {
+      factors();
     }
     LSTAMP(1);
     // per-wave stamps (slots 8 + wave): poll done, or (debug bit 21) reduce done, (bit 22) the
@@ -873,33 +900,25 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     char* ab = aimg + (s & 1) * AIMG;
 #pragma unroll
     for (int ci = 0; ci < CPG; ++ci) {
-      float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
-      const float cpv = s + 1 < T ? xcp[ci] : 0.f;  // c_{t-1}; none at the sequence start
-      if (bv[ci]) {
-        const float dht = xdy[ci] + dh[ci];
-        const float tc = tanh_fast(cc[ci]);
-        const float d_o = dht * tc;
-        const float dcs = dc[ci] + dht * xo[ci] * (1.f - tc * tc);
-        dc[ci] = dcs * xf[ci];
-        d0 = dcs * xgg[ci] * xi[ci] * (1.f - xi[ci]);
-        d1 = dcs * cpv * xf[ci] * (1.f - xf[ci]);
-        d2 = dcs * xi[ci] * (1.f - xgg[ci] * xgg[ci]);
-        d3 = d_o * xo[ci] * (1.f - xo[ci]);
-      }
-      cc[ci] = xcp[ci];  // c_{t-1} is the next step's c_t
-      bsum[ci][0] += d0; bsum[ci][1] += d1; bsum[ci][2] += d2; bsum[ci][3] += d3;
+      const float dht = xdy[ci] + dh[ci];
+      const float dcs = __builtin_fmaf(dht, fA[ci], dc[ci]);
+      dc[ci] = dcs * fF[ci];
+      const float dg[4] = {dcs * f0[ci], dcs * f1[ci], dcs * f2[ci], dht * f3[ci]};
       const int u = uc[ci], r = cu[ci] ^ arow;
-      const float dg[4] = {d0, d1, d2, d3};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int k = g * HJ + u;
         *reinterpret_cast<short*>(ab + r * ROWB + swz(r, k >> 3) * 16 + (k & 7) * 2) = f2bf(dg[g]);
       }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bsum[ci][g] += dg[g];
     }
     if (a.dbg_mode & (1 << 22)) LWSTAMP();
+    const bool pre_pf = late_pf && (a.dbg_mode & (1 << 9));  // A/B: before the barrier
+    if (pre_pf) load_cell(s + 2);
     __syncthreads();  // double-buffered A-image: one barrier per step
     LSTAMP(7);
-    if (late_pf) load_cell(s + 2);
+    if (late_pf && !pre_pf) load_cell(s + 2);
     LSTAMP(3);
     if (abort_flag) return false;
     if (s + 1 < T) {
