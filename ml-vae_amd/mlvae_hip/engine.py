@@ -1081,17 +1081,6 @@ class VAEEngine:
             pgb = lambda t, off=0: None if t is None else _pb(t, off)
             Ybl = w.Yb[li] if w.bf else None
 
-            def wgl(li=li, **kw):
-                # split-K target: the upper layers' weight gradients overlap the next BPTT, so
-                # they take half the CUs; the bottom layer's run in the step's tail, on 160 of
-                # the 256 CUs so the encoder backward beside them is not held off the chip
-                # (alone 26 us, behind a whole-chip GEMM 112 us; c2 5.85 -> 5.80 ms/step)
-                prev = l.mlvae_gemm_bf16_set_split_target(split_tail if li == 0 else split_overlap)
-                try:
-                    wgl_body(li=li, **kw)
-                finally:
-                    l.mlvae_gemm_bf16_set_split_target(prev)
-
             # configs[4]: dW_ih of an fp8 layer on the e4m3 dG (this step's BPTT) and e4m3 input
             f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and li in w.X8 and ldx == din and din % 16 == 0
                        and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, din, N) <= w.gws_bytes)
@@ -1143,6 +1132,19 @@ class VAEEngine:
                 else:
                     self._colsum(w, N, 8 * H, _p(dG), 8 * H, gp(f"decoder.rnn.bias_ih_l{li}"),
                                  gp(f"decoder.rnn.bias_hh_l{li}"))
+            def wgl(li=li, body=wgl_body):
+                # split-K target: the upper layers' weight gradients overlap the next BPTT, so
+                # they take half the CUs; the bottom layer's run in the step's tail, on 160 of
+                # the 256 CUs so the encoder backward beside them is not held off the chip
+                # (alone 26 us, behind a whole-chip GEMM 112 us; c2 5.85 -> 5.80 ms/step).
+                # (body bound here: a call issued after a later layer's loop iteration must
+                # not pick up that iteration's wgl_body)
+                prev = l.mlvae_gemm_bf16_set_split_target(split_tail if li == 0 else split_overlap)
+                try:
+                    body(li=li)
+                finally:
+                    l.mlvae_gemm_bf16_set_split_target(prev)
+
             # The dgrad (+ dropout backward) is the critical path into the next BPTT; the
             # weight gradients go to the side stream after it (so they overlap that BPTT, not
             # this GEMM).  Below the bottom layer nothing waits on the dgrad: its weight
