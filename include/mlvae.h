@@ -165,7 +165,9 @@ int mlvae_lstm_bwd_ex3(int prec, int B, int T, int H, const float* w_hh_fwd, con
 /* fp8 mode (BASELINE.json configs[4]) of the wide-batch recurrences (gates_fp16 shapes, bf16):
  *   fwd: as mlvae_lstm_fwd_ex2 without the fp32 h, plus y_drop_fp8 = e4m3(dropout(h) * x8_scale):
  *        the next layer's fp8 input-projection operand, written by the recurrence itself
- *        (replaces a cast pass over the bf16 copy; ref:src/modules/decoder.py:14-15,22)
+ *        (replaces a cast pass over the bf16 copy; ref:src/modules/decoder.py:14-15,22);
+ *        y_drop_bf16 may be NULL (the e4m3 copy alone: a step whose weight gradient of the next
+ *        layer runs on e4m3 too reads no bf16 dropout(h))
  *   bwd: as mlvae_lstm_bwd_ex2, plus dg_fp8 = e4m3(dG * *dg8_scale) (NULL: none) -- the fp8
  *        dgrad's operand under delayed scaling -- and max |dG| max-ed into *dg_amax (float bits) */
 int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
@@ -177,7 +179,7 @@ int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* 
  * input is the 32-wide latent z): each step's gate inputs z_t W_ih^T + b_ih + b_hh are computed
  * inside the recurrence from z (bf16 [B*T rows, ldz], Z = 32), so the 8H-wide projection is
  * never written or read; gates receives the activated gates (fp16) as from mlvae_lstm_fwd_ex2.
- * y (fp32 h), y_drop_bf16 and y_drop_fp8 (with x8_scale > 0) are optional. */
+ * y (fp32 h), y_drop_bf16 and y_drop_fp8 (with x8_scale > 0) are optional, each on its own. */
 int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, const void* z_bf16,
                      int ldz, int Z, const float* w_ih_fwd, const float* w_ih_rev, const float* b_ih_fwd,
                      const float* b_hh_fwd, const float* b_ih_rev, const float* b_hh_rev, void* gates,

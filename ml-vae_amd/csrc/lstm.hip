@@ -1189,15 +1189,16 @@ extern "C" int mlvae_lstm_fwd_ex2(int prec, int B, int T, int H, const float* w_
 }
 
 // fp8 mode (configs[4]) of the wide kernels: the forward also writes dropout(h) * x8_scale as
-// e4m3 (the next layer's fp8 projection operand); the backward also writes dG * (*dg8_scale) as
+// e4m3 (the next layer's fp8 projection operand; y_drop_bf16 NULL: the e4m3 copy alone, when no
+// bf16 GEMM reads dropout(h) this step); the backward also writes dG * (*dg8_scale) as
 // e4m3 (the fp8 dgrad's operand; NULL: amax only) and max-es max |dG| into *dg_amax (float bits)
 extern "C" int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                                   void* gates, float* cells, void* y_bf16, void* y_drop_bf16,
                                   void* y_drop_fp8, float x8_scale, unsigned long long drop_seed,
                                   unsigned long long drop_offset, float drop_p, void* xbuf,
                                   size_t xbytes, int* err, void* stream) {
-  if (!use_wide(B, H, PREC_BF16) || !y_drop_fp8 || !y_drop_bf16 || !(x8_scale > 0.f)) {
-    mlvae_set_error("lstm_fwd_fp8: wide-batch shapes with a dropout output and a positive scale only");
+  if (!use_wide(B, H, PREC_BF16) || !y_drop_fp8 || !(x8_scale > 0.f)) {
+    mlvae_set_error("lstm_fwd_fp8: wide-batch shapes with an e4m3 dropout output and a positive scale only");
     return 1;
   }
   WideExtra ex;
@@ -1219,8 +1220,8 @@ extern "C" int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, cons
                                 float* y, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
                                 unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
                                 void* xbuf, size_t xbytes, int* err, void* stream) {
-  if (Z != 32 || !z_bf16 || !use_wide(B, H, PREC_BF16) || (y_drop_fp8 && (!y_drop_bf16 || !(x8_scale > 0.f)))) {
-    mlvae_set_error("lstm_fwd_z: Z = 32 on wide-batch shapes; an e4m3 dropout output needs the bf16 one and a scale");
+  if (Z != 32 || !z_bf16 || !use_wide(B, H, PREC_BF16) || (y_drop_fp8 && !(x8_scale > 0.f))) {
+    mlvae_set_error("lstm_fwd_z: Z = 32 on wide-batch shapes; an e4m3 dropout output needs a scale");
     return 1;
   }
   WideExtra ex;

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     static_assert(2 * NC8 <= 256, "one h chunk per io thread");
     const bool drop8 = iot >= NC8;
     const int ci8 = drop8 ? iot - NC8 : iot;
-    if (ci8 < NC8 && (drop8 ? a.Ydb != nullptr : a.Yb != nullptr)) {
+    if (ci8 < NC8 && (drop8 ? (a.Ydb != nullptr || a.Y8 != nullptr) : a.Yb != nullptr)) {
       const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8, b = grp * BG + u;
       if (b < a.B) {
         const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
@@ -267,9 +267,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             v1[e] = (bits >> (4 + e)) & 1 ? v1[e] * a.dscale : 0.f;
           }
         }
-        *reinterpret_cast<bf16x8*>((drop8 ? a.Ydb : a.Yb) + o) =
-            bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
-                   f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+        if (!drop8 || a.Ydb)  // (fp8 mode may ask for the e4m3 dropout(h) alone)
+          *reinterpret_cast<bf16x8*>((drop8 ? a.Ydb : a.Yb) + o) =
+              bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]),
+                     f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
         if (drop8 && a.Y8) {  // fp8 mode: the next layer's e4m3 projection operand, fixed scale
           const float xs = a.x8scale;
           *reinterpret_cast<u32x2*>(a.Y8 + o) =
@@ -282,7 +283,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // The step loop, instantiated once per role (IO: waves 4-7 move the step's HBM traffic;
   // else waves 0-3 poll the hand-off): each instance keeps only its own role's state live,
   // and both pass the same barriers.
-  const bool late_bits = a.Ydb && !(a.dbg_mode & (1 << 27));
+  const bool want_drop = a.Ydb || a.Y8;  // a dropout(h) output (bf16 and / or e4m3)
+  const bool late_bits = want_drop && !(a.dbg_mode & (1 << 27));
   const bool late_dma_s = (2 * a.NB * a.NJ <= 64) != ((a.dbg_mode & (1 << 17)) != 0);
   auto run = [&](auto io_tag) {
     constexpr bool IO = decltype(io_tag)::value;
@@ -560,7 +562,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       // per step).  Tried and reverted as well (same box, c3 12.60-12.73 -> 12.78-12.92 ms):
       // io waves waiting for their gx LDS-DMA alone by a counted vmcnt (their stores left in
       // flight across the barrier), and the BPTT's dG stores moved behind the next poll.
-      if (!IO && a.Ydb && tid < NC8 && (!late_bits || s + 1 == T)) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
+      if (!IO && want_drop && tid < NC8 && (!late_bits || s + 1 == T)) dbl[(s & 1) * NC8 + tid] = drop_bits(s, tid);
       LSTAMP(7);
     }
     __syncthreads();
@@ -1200,8 +1202,8 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
     a.Zb = wz.zb; a.ldz = wz.ldz; a.Wz0 = wz.w0; a.Wz1 = wz.w1;
     for (int i = 0; i < 4; ++i) a.bz[i] = wz.b[i];
   }
-  if (a.Y8 && !ydb) {
-    mlvae_set_error("lstm_wide: the fp8 dropout(h) copy comes with the bf16 one");
+  if (a.Y8 && (!fwd || !(a.x8scale > 0.f) || !(dp >= 0.f && dp < 1.f))) {
+    mlvae_set_error("lstm_wide: the e4m3 dropout(h) output needs the forward, a positive scale and 0 <= p < 1");
     return 1;
   }
   if (a.dG8 && (!a.g8scale || !a.g8amax)) {

@@ -384,6 +384,9 @@ class VAEEngine:
                 # the fp8 weight gradient dW_ih = dG^T X (e4m3 dG and layer input): alpha =
                 # 1 / (q_dG * x-scale) (False: bf16)
                 self.fp8_wgrad = True
+                # ... and then (from the second step) the recurrence below writes the e4m3 layer
+                # input alone: no bf16 GEMM reads dropout(h) (False: both copies every step)
+                self.fp8_skip_ydb = True
                 self.x8s = torch.tensor([x8_scale(cfg.dropout)], device=self.device)
                 self.g8w = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
                 self.g8_ready = False  # a previous step's amax exists (the first step's dgrad is bf16)
@@ -784,6 +787,13 @@ class VAEEngine:
                         and 2 * H % 16 == 0)
             x8_ptr = w.X8[li + 1].data_ptr() if x8_fused else None
             w.__dict__.setdefault("x8_fused", {})[li + 1] = x8_fused
+            # fp8 steady state: layer li+1's dgrad and weight gradient both run on e4m3 (the
+            # backward's f8w), so the bf16 dropout(h) has no reader and is not written
+            skip_ydb = bool(x8_fused and self.g8_ready and self.fp8_wgrad and getattr(self, "fp8_skip_ydb", False)
+                            and (li + 1) in self.g8
+                            and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, 2 * H, N) <= w.gws_bytes)
+            w.__dict__.setdefault("ydb_skipped", {})[li + 1] = skip_ydb
+            ydb_arg = None if skip_ydb else (_pb(w.Ydb[li]) if fuse_drop else None)
             with self._timed("lstm_fwd"):
                 if zproj:
                     rp = lambda n: self._ptr(f"decoder.rnn.{n}")
@@ -792,7 +802,7 @@ class VAEEngine:
                                              rp("bias_ih_l0"), rp("bias_hh_l0"), rp("bias_ih_l0_reverse"),
                                              rp("bias_hh_l0_reverse"), _p(w.G[li]), _p(w.Cs[li]),
                                              _p(w.Y[li]) if need_y else None, _pb(w.Yb[li]),
-                                             _pb(w.Ydb[li]) if fuse_drop else None,
+                                             ydb_arg,
                                              x8_ptr,
                                              x8_scale(cfg.dropout) if x8_fused else 0.0, seed, self._drop_off,
                                              cfg.dropout if fuse_drop else 0.0, _p(w.xbuf), w.xbuf.numel(),
@@ -800,7 +810,7 @@ class VAEEngine:
                 elif x8_fused:
                     check(l.mlvae_lstm_fwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
-                                               _p(w.Cs[li]), _pb(w.Yb[li]), _pb(w.Ydb[li]), x8_ptr,
+                                               _p(w.Cs[li]), _pb(w.Yb[li]), ydb_arg, x8_ptr,
                                                x8_scale(cfg.dropout), seed, self._drop_off, cfg.dropout,
                                                _p(w.xbuf), w.xbuf.numel(), _p(self.err), s), "lstm_fwd_fp8")
                 else:
@@ -1084,6 +1094,8 @@ class VAEEngine:
             # configs[4]: dW_ih of an fp8 layer on the e4m3 dG (this step's BPTT) and e4m3 input
             f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and li in w.X8 and ldx == din and din % 16 == 0
                        and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, din, N) <= w.gws_bytes)
+            if w.__dict__.get("ydb_skipped", {}).get(li) and not f8w:
+                raise RuntimeError(f"layer {li}: the forward skipped the bf16 dropout(h) the bf16 weight gradient reads")
 
             def wgl_body(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx,
                          Ybl=Ybl, f8w=f8w):

@@ -81,7 +81,8 @@ def test_c5_fp8_second_step_fp8_dgrad_matches_oracle():
     """configs[4] in its steady state: from the second step on the fp8 mode also runs the layer-1
     dgrad on e4m3 operands (dG written by the BPTT under delayed scaling from the first step's
     amax, W_ih^T with the forward's scale, the dropout backward in the epilogue) and the layer
-    input arrives as e4m3 from the recurrence itself.  The oracle replays step 2 from the engine's
+    input arrives as e4m3 from the recurrence itself -- alone, without the bf16 copy no GEMM
+    reads any more.  The oracle replays step 2 from the engine's
     state after step 1 (parameters, Adam moments)."""
     need_gpu()
     from mlvae_hip.engine import VAEConfig
@@ -90,6 +91,7 @@ def test_c5_fp8_second_step_fp8_dgrad_matches_oracle():
     lens = torch.linspace(0.6, 1.0, B)
     eng, w, rec, new_ref, params = run_second_step(cfg, B, T, 810, lens)
     assert eng.g8_ready and float(eng.g8[1][0].item()) != 1.0   # a real delayed scale was used
+    assert w.ydb_skipped.get(1)   # layer 0 wrote the e4m3 dropout(h) alone (no bf16 reader)
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report("c5 fp8 step 2 (fp8 dgrad) B=64 T=500", e, grads)
     _check(e, grads, 0.12, 3e-2)
@@ -108,6 +110,7 @@ def test_fp8_three_layers_second_step_matches_oracle():
     lens = torch.linspace(0.6, 1.0, B)
     eng, w, rec, new_ref, params = run_second_step(cfg, B, T, 811, lens)
     assert eng.g8_ready and all(float(eng.g8[li][0].item()) != 1.0 for li in (1, 2))
+    assert w.ydb_skipped.get(1) and w.ydb_skipped.get(2)
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report("fp8 L=3 step 2 B=48 T=120", e, grads)
     _check(e, grads, 0.12, 3e-2)
