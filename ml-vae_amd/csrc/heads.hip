@@ -418,6 +418,9 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
   constexpr int NBS = nbs<C, F>();
   __shared__ __attribute__((aligned(16))) float bred[4][NBS];
   __shared__ float inv_cnt;
+  // b2 | b3 of both heads, staged once: read from global memory inside the tile loop, every bias
+  // quad's vmcnt wait also waited for the next tile's prefetch and this tile's stores
+  __shared__ __attribute__((aligned(16))) float sbias[2 * C + 2 * F];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, q = lane >> 4;
@@ -461,9 +464,12 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
   const unsigned short* P1b = reinterpret_cast<const unsigned short*>(a.P1);
   u32x4 pn[4];
   f32x4 xn[NF];
+  float lnn;  // ... and the row's utterance length (read in stage 4: with the tile's own loads its
+              // wait would include the next tile's prefetch)
   auto prefetch = [&](int tile) {
     const int grow = tile * RT + 16 * wave + l15;
     const bool rv = tile < ntiles && grow < a.N;
+    lnn = rv ? a.lens[grow / a.T] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       pn[i] = rv ? *reinterpret_cast<const u32x4*>(P1b + (size_t)grow * C2 + 8 * (q + 4 * i)) : u32x4{0u, 0u, 0u, 0u};
@@ -472,6 +478,8 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
       xn[j] = rv ? *reinterpret_cast<const f32x4*>(a.x + (size_t)grow * F + 16 * j + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   prefetch(blockIdx.x);
+  for (int i = tid; i < 2 * C; i += 256) sbias[i] = a.b2[i / C] ? a.b2[i / C][i % C] : 0.f;
+  for (int i = tid; i < 2 * F; i += 256) sbias[2 * C + i] = a.b3[i / F] ? a.b3[i / F][i % F] : 0.f;
   __syncthreads();
 
   const int lrow = 16 * wave + l15;
@@ -488,6 +496,7 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int grow = tile * RT + lrow;
     const bool rv = grow < a.N;
+    const float lenb = lnn;
     // this tile's P1 rows into the wave's P1 image; the next tile's loads go out behind them
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(sm + O_P1 + lrow * L2C + 8 * (q + 4 * i)) = pn[i];
@@ -520,8 +529,9 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
 #pragma unroll
       for (int j = 0; j < NC; ++j) {
         const int col = 16 * j + 4 * q;
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(sbias + h * C + col);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc2[h][j][r] = lrelu(acc2[h][j][r] + a.b2[h][col + r]);
+        for (int r = 0; r < 4; ++r) acc2[h][j][r] = lrelu(acc2[h][j][r] + bb[r]);
         st4bf(sm + O_P2 + h * RT * LC + lrow * LC + col, acc2[h][j]);
         if (SAVE && rv) st_saved(a.P2[h], (size_t)grow * C + col, acc2[h][j], 1);
       }
@@ -537,18 +547,16 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         const int col = 16 * j + 4 * q;
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(sbias + 2 * C + h * F + col);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc3[h][j][r] += a.b3[h][col + r];
+        for (int r = 0; r < 4; ++r) acc3[h][j][r] += bb[r];
         if (rv) *reinterpret_cast<f32x4*>(a.OUT[h] + (size_t)grow * F + col) = acc3[h][j];
       }
     }
 
     // ---- stage 4: reconstruction loss, masked partial sum, gradient wrt (mu, log_var)
     bool m = false;
-    if (rv) {
-      const int b = grow / a.T, t = grow % a.T;
-      m = t < valid_frames(a.lens[b], a.T);
-    }
+    if (rv) m = grow % a.T < valid_frames(lenb, a.T);
     const float sc = m ? a.rec_scale * inv_cnt : 0.f;
     float lsum = 0.f;
 #pragma unroll
