@@ -933,6 +933,16 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       constexpr int NGRP = bptt_groups<TPW>();
       static_assert(NTW % NGRP == 0 && (TPW != 1 || (NTW / NGRP) % 2 == 0), "tile groups");
       constexpr int TPH = NTW / NGRP;
+      // TPW 1 (one batch of BKB = KC k-chunks): the step's A-fragments are read once, for both
+      // tile groups (the VGPRs are there at TPW 1), instead of once per group
+      constexpr bool AONCE = BKB == KC && NGRP > 1;
+      bf16x8 afr_all[AONCE ? KC : 1];
+      if constexpr (AONCE) {
+#pragma unroll
+        for (int i = 0; i < KC; ++i)
+          afr_all[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, i * 4 + q) * 16);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int hf = 0; hf < NGRP; ++hf) {
         f32x4 acc[TPH];
@@ -946,10 +956,15 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 #pragma unroll
         for (int k0 = 0; k0 < KC; k0 += BKB) {
           bf16x8 afr[BKB];
+          if constexpr (AONCE) {
 #pragma unroll
-          for (int i = 0; i < BKB; ++i)
-            afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
-          __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
+            for (int i = 0; i < BKB; ++i) afr[i] = afr_all[k0 + i];
+          } else {
+#pragma unroll
+            for (int i = 0; i < BKB; ++i)
+              afr[i] = *reinterpret_cast<const bf16x8*>(ab + bi * ROWB + swz(bi, (k0 + i) * 4 + q) * 16);
+            __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
+          }
 #pragma unroll
           for (int i = 0; i < BKB; ++i) {
             const int kc = k0 + i;
