@@ -325,6 +325,10 @@ def timed_run(eng, x, lens, steps, warmup, world, timers=None, norm=None):
     dt = time.perf_counter() - t0
     eng.kernel_timers = None
     eng.check_errors()
+    # a step whose numbers went non-finite is not a measurement (NaN data also draws less power,
+    # so such a run can even look faster): refuse to report it
+    if loss is not None and not bool(torch.isfinite(loss).all()):
+        raise SystemExit(f"bench: non-finite ELBO {loss.tolist()} -- invalid run, not reported")
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], device=x.device)
