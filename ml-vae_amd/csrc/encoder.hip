@@ -312,10 +312,12 @@ __global__ __launch_bounds__(256) void encoder_bwd_kernel(EncBwdArgs a) {
   const int lrow = 16 * wave + l15;
   f32x4 pg[2], pmu[2], plv[2], pep[2], px[XP][2];
   unsigned long long pe2[4], pe1[4];   // bf16x4 bit patterns (scalar words: no stack copy)
+  float plen;   // the row's utterance length (read in the loop, its wait included the prefetch)
   auto prefetch = [&](int tile_) __attribute__((always_inline)) {
     const int row_ = tile_ * 64 + lrow;
     const bool rv_ = tile_ < ntiles && row_ < a.N;
     const size_t rr_ = rv_ ? row_ : 0;
+    plen = rv_ ? a.lens[row_ / a.T] : 0.f;
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       const int z0 = 8 * q + 4 * h2;
@@ -349,6 +351,7 @@ __global__ __launch_bounds__(256) void encoder_bwd_kernel(EncBwdArgs a) {
     // this tile's inputs out of the prefetch registers, the next tile's loads issued behind them
     f32x4 cg[2], cmu[2], clv[2], cep[2], cx[XP][2];
     unsigned long long ce2[4], ce1[4];
+    const float clen = plen;
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) { cg[h2] = pg[h2]; cmu[h2] = pmu[h2]; clv[h2] = plv[h2]; cep[h2] = pep[h2]; }
 #pragma unroll
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(256) void encoder_bwd_kernel(EncBwdArgs a) {
     // reparameterisation + KL gradient (as reparam_kl_bwd in elbo.hip), z index 8 q + e
     float dmu[8], dlv[8];
     if (rv) {
-      const float s = frame_valid(a.lens, row, a.T) ? s_kl : 0.f;
+      const float s = row % a.T < valid_frames(clen, a.T) ? s_kl : 0.f;
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
 #pragma unroll
