@@ -364,6 +364,10 @@ int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int 
  * mlvae_heads_wgrad_workspace_size(B, T, F, C); under mse (loss_type 1) dw3v / dw2v may be NULL
  * and are not written.  P2 / dOUT / dP2 (p2m, p2v, dmux, dlvx, dp2m, dp2v) are then not written. */
 size_t mlvae_heads_wgrad_workspace_size(int B, int T, int F, int C);
+/* The split form's two first-layer products (P1 = LReLU(Y W1^T + b1), dY = dP1 W1) run on a
+ * 128-row kernel (mode 1, the default: from 64K frames; 2: at every size; 0: on the 256² GEMM).
+ * Both compute each output with the same k-order, so the modes agree bit for bit. */
+int mlvae_heads_set_nt_mode(int mode);
 int mlvae_heads_fused_ex2(int B, int T, int F, int C, int H2, int loss_type, int train,
                           const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
                           const float* w2m, const float* b2m, const float* w3m, const float* b3m,

@@ -743,6 +743,142 @@ int launch_heads(const HeadArgs& a, hipStream_t st) {
   return 0;
 }
 
+// ---- the split form's two first-layer products on a 128-row kernel (instead of 256² tiles
+// with a 128-wide N or K: 500 tiles in two rounds at c3).  C[M x Nn] = A[M x K] . B[Nn x K]^T,
+// bf16 operands (both k-contiguous), fp32 accumulation:
+//   P1 = lrelu(rnn_out W1^T + b1) -> bf16   (Nn = 2C = 128, K = 2H)
+//   dY = dP1 W1                  -> bf16 / fp32 (Nn = 2H, K = 2C = 128; B = W1^T)
+// A workgroup (8 waves, one 16-row slice each) walks 128-row blocks; per block the (n-chunk,
+// k-chunk) pieces of B [128 x 128] pass through LDS (register double buffer, loaded one piece
+// ahead), A fragments come straight from global memory into registers (each used by all 8
+// n-tiles) and are kept across the n-chunks when K is one chunk.  Swapped MFMA operands: lane
+// (l15, q) holds C[row 16 w + l15][16 nt + 4 q + r] -- 8- / 16-byte row stores.
+constexpr int HNT_BN = 128;
+template <bool LRELU, int HNT_BK>
+__global__ __launch_bounds__(512) void heads_nt_kernel(int M, int Nn, int K, const unsigned short* __restrict__ A,
+                                                       int lda, const unsigned short* __restrict__ B, int ldb,
+                                                       void* __restrict__ Cv, int ldc, const float* __restrict__ bias,
+                                                       int out_bf16) {
+  constexpr int HNT_LB = HNT_BK + 8;  // LDS row stride (bf16)
+  constexpr int BPT = HNT_BN * HNT_BK / 8 / 512;  // 16-byte B pieces per thread
+  extern __shared__ __attribute__((aligned(16))) short hsm[];  // [2][HNT_BN][HNT_LB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l15 = lane & 15, q = lane >> 4;
+  const int nch = Nn / HNT_BN, kch = K / HNT_BK, npc = nch * kch;  // pieces per block
+  const int nblk = (M + 127) / 128;
+  // B piece p = (n-chunk p / kch, k-chunk p % kch): 128 x HNT_BK bf16 in 16-byte pieces
+  u32x4 bq[BPT];
+  auto bload = [&](int p) {
+    const int nc = p / kch, kc = p - nc * kch;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int idx = tid + 512 * i, n = idx / (HNT_BK / 8), k16 = idx % (HNT_BK / 8);
+      bq[i] = *reinterpret_cast<const u32x4*>(B + (size_t)(nc * HNT_BN + n) * ldb + kc * HNT_BK + 8 * k16);
+    }
+  };
+  auto bstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int idx = tid + 512 * i, n = idx / (HNT_BK / 8), k16 = idx % (HNT_BK / 8);
+      *reinterpret_cast<u32x4*>(hsm + buf * HNT_BN * HNT_LB + n * HNT_LB + 8 * k16) = bq[i];
+    }
+  };
+  // A fragments of piece p of block b: rows 16 w + l15 of the block, k-chunk p % kch (a new chunk
+  // per piece when K has several chunks; once per block when it has one)
+  auto aload = [&](bf16x8 (&af)[HNT_BK / 32], int b, int p) {
+    const int row = b * 128 + 16 * wave + l15;
+    const unsigned short* arow = A + (size_t)(row < M ? row : M - 1) * lda + (p % kch) * HNT_BK;
+#pragma unroll
+    for (int ks = 0; ks < HNT_BK / 32; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(arow + 32 * ks + 8 * q);
+  };
+  int blk = blockIdx.x;
+  if (blk >= nblk) return;
+  bf16x8 afr[HNT_BK / 32], anx[HNT_BK / 32];
+  bload(0);
+  aload(afr, blk, 0);
+  int buf = 0;
+  f32x4 acc[HNT_BN / 16];
+  for (; blk < nblk; blk += gridDim.x) {
+    const int row = blk * 128 + 16 * wave + l15;
+    const bool rv = row < M;
+    for (int p = 0; p < npc; ++p) {
+      const int nc = p / kch, kc = p - nc * kch;
+      // piece p: registers -> LDS buffer (its previous piece, p - 2, was read before every wave
+      // passed the barrier of p - 1); the next piece's B and, when it needs new ones, A fragments
+      // are loaded behind it and land under this piece's MFMAs
+      bstore(buf);
+      __syncthreads();
+      const int nb = p + 1 < npc ? blk : blk + (int)gridDim.x, np = p + 1 < npc ? p + 1 : 0;
+      const bool more = nb < nblk, new_a = more && (kch > 1 || np == 0);
+      if (more) bload(np);
+      if (new_a) aload(anx, nb, np);
+      if (kc == 0) {
+#pragma unroll
+        for (int nt = 0; nt < HNT_BN / 16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      const short* bb = hsm + buf * HNT_BN * HNT_LB;
+#pragma unroll
+      for (int ks = 0; ks < HNT_BK / 32; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < HNT_BN / 16; ++nt)
+          acc[nt] = mfma(*reinterpret_cast<const bf16x8*>(bb + (16 * nt + l15) * HNT_LB + 32 * ks + 8 * q), afr[ks],
+                         acc[nt]);
+      buf ^= 1;
+      if (kc == kch - 1 && rv) {
+#pragma unroll
+        for (int nt = 0; nt < HNT_BN / 16; ++nt) {
+          const int col = nc * HNT_BN + 16 * nt + 4 * q;
+          f32x4 v = acc[nt];
+          if (LRELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r] + bias[col + r]);
+          }
+          if (out_bf16)
+            *reinterpret_cast<bf16x4*>(static_cast<unsigned short*>(Cv) + (size_t)row * ldc + col) =
+                bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          else
+            *reinterpret_cast<f32x4*>(static_cast<float*>(Cv) + (size_t)row * ldc + col) = v;
+        }
+      }
+      if (new_a) {
+#pragma unroll
+        for (int ks = 0; ks < HNT_BK / 32; ++ks) afr[ks] = anx[ks];
+      }
+    }
+  }
+}
+
+int heads_cus();
+int heads_nt(bool lrelu_bias, int M, int Nn, int K, const void* A, int lda, const void* B, int ldb, void* C,
+             int ldc, const float* bias, bool out_bf16, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (Nn % HNT_BN || K % 128 || lda % 8 || ldb % 8 || ldc % 4 || (lrelu_bias && !bias)) {
+    mlvae_set_error("heads_nt: Nn %% 128, K %% 128, 16-byte rows and a bias with the LReLU epilogue");
+    return 1;
+  }
+  // k-chunks of 128, two workgroups per CU (k-chunks of 256 at one per CU: c3 heads 0.367 -> 0.375 ms)
+  constexpr size_t lds = (size_t)2 * HNT_BN * (128 + 8) * sizeof(short);
+  const int nblk = (M + 127) / 128, grid = nblk < 2 * heads_cus() ? nblk : 2 * heads_cus();
+  auto k = lrelu_bias ? heads_nt_kernel<true, 128> : heads_nt_kernel<false, 128>;
+  static bool attr[2] = {false, false};
+  if (!attr[lrelu_bias]) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+      mlvae_set_error("heads_nt: cannot reserve %zu B LDS", lds);
+      return 2;
+    }
+    attr[lrelu_bias] = true;
+  }
+  k<<<grid, 512, lds, st>>>(M, Nn, K, static_cast<const unsigned short*>(A), lda,
+                            static_cast<const unsigned short*>(B), ldb, C, ldc, bias, out_bf16 ? 1 : 0);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+// 0: the 256² GEMM for the two products; 1 (default): the 128-row kernel from 64K frames; 2: the
+// 128-row kernel at every size (tests).  MLVAE_HEADS_NT sets the initial mode (A/B timing).
+int g_heads_nt = [] {
+  const char* e = getenv("MLVAE_HEADS_NT");
+  return e ? atoi(e) : 1;
+}();
+
 int heads_cus() {
   static int n = 0;
   if (!n) {
@@ -876,6 +1012,14 @@ extern "C" size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C) {
 }
 
 // the fused small weight gradients (mlvae_heads_fused_ex2): per-workgroup slabs + WG_NZ partials
+extern "C" int mlvae_heads_set_nt_mode(int mode) {
+  if (mode < 0 || mode > 2) {
+    mlvae_set_error("heads: nt mode %d (0 off, 1 auto, 2 always)", mode);
+    return 1;
+  }
+  g_heads_nt = mode;
+  return 0;
+}
 extern "C" size_t mlvae_heads_wgrad_workspace_size(int B, int T, int F, int C) {
   if (C != 64 || (F != 64 && F != 80) || B <= 0 || T <= 0) return 0;
   const size_t S = F == 80 ? wg_slab<64, 80>() : wg_slab<64, 64>();
@@ -1021,8 +1165,12 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
   if (split) {
     // split form: P1 GEMM, the persistent middle stages, dY GEMM (heads_mid_kernel comment)
     constexpr int EPI_LRELU_BF16 = 1 | 32;  // gemm_fast.hip: EPI_LRELU | EPI_OUT_BF16
-    rc = mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
-                         nullptr, EPI_LRELU_BF16, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
+    // (the 256² GEMM below 64K frames: the 128-row kernel's blocks then leave CUs idle, c2 +6 us)
+    const bool nt = g_heads_nt != 0 && (2 * C) % HNT_BN == 0 && H2 % 128 == 0 &&
+                    (a.N >= 65536 || g_heads_nt == 2);
+    rc = nt ? heads_nt(true, a.N, 2 * C, H2, y_bf16, H2, w1_bf16, H2, p1, 2 * C, b1, true, st)
+            : mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
+                              nullptr, EPI_LRELU_BF16, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
     if (rc) return rc;
     if (a.wg_ws) rc = F == 80 ? launch_mid<64, 80, true>(a, st) : launch_mid<64, 64, true>(a, st);
     else rc = F == 80 ? launch_mid<64, 80, false>(a, st) : launch_mid<64, 64, false>(a, st);
@@ -1033,9 +1181,10 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                    : launch_wg_reduce<64, 64>(a, dw3m, mse ? nullptr : dw3v, dw2m, mse ? nullptr : dw2v, st);
       if (rc) return rc;
     }
-    rc = mlvae_gemm_bf16(0, 1, a.N, H2, 2 * C, 1, dp1, 2 * C, 0, w1t_bf16, 2 * C, 0, dy, H2, 0, 0.f, nullptr,
-                         nullptr, dy_bf16 ? 32 : 0 /* EPI_OUT_BF16 */, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f,
-                         nullptr, 0, stream);
+    rc = nt ? heads_nt(false, a.N, H2, 2 * C, dp1, 2 * C, w1t_bf16, 2 * C, dy, H2, nullptr, dy_bf16, st)
+            : mlvae_gemm_bf16(0, 1, a.N, H2, 2 * C, 1, dp1, 2 * C, 0, w1t_bf16, 2 * C, 0, dy, H2, 0, 0.f, nullptr,
+                              nullptr, dy_bf16 ? 32 : 0 /* EPI_OUT_BF16 */, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f,
+                              nullptr, 0, stream);
   } else {
     rc = F == 80 ? launch_heads<64, 80>(a, st) : launch_heads<64, 64>(a, st);
   }

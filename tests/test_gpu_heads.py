@@ -243,3 +243,61 @@ def test_heads_fused_weight_gradients(loss_type, B, T, F, H2):
     _, _, dw2 = run(True)
     for a_, b_ in zip(first, dw2):
         assert torch.equal(torch.nan_to_num(a_, 7.0), torch.nan_to_num(b_, 7.0))
+
+
+@pytest.mark.parametrize("loss_type", [0, 1])
+@pytest.mark.parametrize("B,T,F,H2", [(3, 50, 80, 256), (5, 77, 64, 128), (40, 500, 80, 1024), (140, 500, 80, 1024)])
+def test_heads_nt_products_match_the_gemm_bit_for_bit(loss_type, B, T, F, H2):
+    """The split form's P1 = LReLU(Y W1^T + b1) and dY = dP1 W1 on the 128-row kernel
+    (mlvae_heads_set_nt_mode 2; the default from 64K frames -- the last shape) against the 256²
+    GEMM (mode 0): every output of the heads launch bit-identical (the same k-order per output),
+    ragged 128-row blocks included."""
+    need_gpu()
+    torch.manual_seed(B + T + F + H2 + loss_type)
+    C, N = 64, B * T
+    l = lib()
+    f = dict(device="cuda", dtype=torch.float32)
+    Y = torch.randn(N, H2).to(torch.bfloat16).cuda()
+    W1 = (torch.randn(2 * C, H2) / math.sqrt(H2)).to(torch.bfloat16)
+    dW1, dW1t = W1.cuda(), W1.t().contiguous().cuda()
+    b1 = (torch.randn(2 * C) * 0.1).cuda()
+    W2 = [(torch.randn(C, C) / 8).cuda() for _ in range(2)]
+    b2 = [(torch.randn(C) * 0.1).cuda() for _ in range(2)]
+    W3 = [(torch.randn(F, C) / 8).cuda() for _ in range(2)]
+    b3 = [(torch.randn(F) * 0.1).cuda() for _ in range(2)]
+    x = torch.randn(N, F).cuda()
+    lens = (torch.rand(B) * 0.7 + 0.3).cuda()
+    lik = loss_type == 0
+
+    def run(mode):
+        check(l.mlvae_heads_set_nt_mode(mode))
+        o = {k: torch.zeros(N, n, device="cuda", dtype=torch.bfloat16)
+             for k, n in (("p1", 2 * C), ("p2m", C), ("p2v", C), ("dmux", F), ("dlvx", F), ("dp2m", C),
+                          ("dp2v", C), ("dp1", 2 * C))}
+        o.update({k: torch.zeros(N, n, **f) for k, n in (("mux", F), ("lvx", F), ("dy", H2))})
+        parts = torch.zeros(l.mlvae_heads_partials_count(B, T), **f)
+        ws = torch.zeros(l.mlvae_heads_bias_workspace_size(B, T, F, C) // 4 + 1, **f)
+        db = [torch.zeros(n, **f) for n in (F, F, C, C, 2 * C)]
+        check(l.mlvae_heads_fused_ex(B, T, F, C, H2, loss_type, 1, Y.data_ptr(), dW1.data_ptr(), dW1t.data_ptr(),
+                                     P(b1), P(W2[0]), P(b2[0]), P(W3[0]), P(b3[0]), P(W2[1]), P(b2[1]),
+                                     P(W3[1]), P(b3[1]), P(x), P(lens), None, 0.7, P(o["p1"]), P(o["p2m"]),
+                                     P(o["p2v"]), P(o["mux"]), P(o["lvx"]), P(o["dmux"]),
+                                     P(o["dlvx"]) if lik else None, P(o["dp2m"]), P(o["dp2v"]), P(o["dp1"]),
+                                     P(o["dy"]), P(parts), P(ws), ws.numel() * 4, P(db[0]), P(db[1]), P(db[2]),
+                                     P(db[3]), P(db[4]), 1, stream()))
+        torch.cuda.synchronize()
+        return o, parts, db
+
+    try:
+        ref, ref_parts, ref_db = run(0)
+        new, new_parts, new_db = run(2)
+    finally:
+        check(l.mlvae_heads_set_nt_mode(1))
+    assert new["p1"].float().abs().sum() > 0 and new["dy"].abs().sum() > 0
+    for k in ref:
+        assert torch.equal(ref[k], new[k]), k
+    assert torch.equal(ref_parts, new_parts)
+    for a, b in zip(ref_db, new_db):
+        assert torch.equal(a, b)
+    with pytest.raises(Exception):
+        check(l.mlvae_heads_set_nt_mode(3))
