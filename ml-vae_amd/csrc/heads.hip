@@ -816,27 +816,38 @@ __global__ __launch_bounds__(512) void heads_nt_kernel(int M, int Nn, int K, con
         for (int nt = 0; nt < HNT_BN / 16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
       const short* bb = hsm + buf * HNT_BN * HNT_LB;
+      // n-tile pair (2 t, 2 t + 1) covers columns 32 t .. 32 t + 31 with MFMA row i of tile 2 t + h
+      // on column 32 t + 8 (i >> 2) + 4 h + (i & 3): lane (l15, q) then holds 8 consecutive
+      // columns 32 t + 8 q .. + 7 of its row -- one 16-byte bf16 store per pair
 #pragma unroll
       for (int ks = 0; ks < HNT_BK / 32; ++ks)
 #pragma unroll
-        for (int nt = 0; nt < HNT_BN / 16; ++nt)
-          acc[nt] = mfma(*reinterpret_cast<const bf16x8*>(bb + (16 * nt + l15) * HNT_LB + 32 * ks + 8 * q), afr[ks],
-                         acc[nt]);
+        for (int nt = 0; nt < HNT_BN / 16; ++nt) {
+          const int brow = 32 * (nt >> 1) + 8 * (l15 >> 2) + 4 * (nt & 1) + (l15 & 3);
+          acc[nt] = mfma(*reinterpret_cast<const bf16x8*>(bb + brow * HNT_LB + 32 * ks + 8 * q), afr[ks], acc[nt]);
+        }
       buf ^= 1;
       if (kc == kch - 1 && rv) {
 #pragma unroll
-        for (int nt = 0; nt < HNT_BN / 16; ++nt) {
-          const int col = nc * HNT_BN + 16 * nt + 4 * q;
-          f32x4 v = acc[nt];
+        for (int t = 0; t < HNT_BN / 32; ++t) {
+          const int col = nc * HNT_BN + 32 * t + 8 * q;
+          f32x4 v0 = acc[2 * t], v1 = acc[2 * t + 1];
           if (LRELU) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = lrelu(v[r] + bias[col + r]);
+            for (int r = 0; r < 4; ++r) {
+              v0[r] = lrelu(v0[r] + bias[col + r]);
+              v1[r] = lrelu(v1[r] + bias[col + 4 + r]);
+            }
           }
-          if (out_bf16)
-            *reinterpret_cast<bf16x4*>(static_cast<unsigned short*>(Cv) + (size_t)row * ldc + col) =
-                bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-          else
-            *reinterpret_cast<f32x4*>(static_cast<float*>(Cv) + (size_t)row * ldc + col) = v;
+          if (out_bf16) {
+            *reinterpret_cast<bf16x8*>(static_cast<unsigned short*>(Cv) + (size_t)row * ldc + col) =
+                bf16x8{f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3]), f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]),
+                       f2bf(v1[3])};
+          } else {
+            float* cr = static_cast<float*>(Cv) + (size_t)row * ldc + col;
+            *reinterpret_cast<f32x4*>(cr) = v0;
+            *reinterpret_cast<f32x4*>(cr + 4) = v1;
+          }
         }
       }
       if (new_a) {
@@ -851,7 +862,7 @@ int heads_cus();
 int heads_nt(bool lrelu_bias, int M, int Nn, int K, const void* A, int lda, const void* B, int ldb, void* C,
              int ldc, const float* bias, bool out_bf16, hipStream_t st) {
   if (M <= 0) return 0;
-  if (Nn % HNT_BN || K % 128 || lda % 8 || ldb % 8 || ldc % 4 || (lrelu_bias && !bias)) {
+  if (Nn % HNT_BN || K % 128 || lda % 8 || ldb % 8 || ldc % 8 || (lrelu_bias && !bias)) {
     mlvae_set_error("heads_nt: Nn %% 128, K %% 128, 16-byte rows and a bias with the LReLU epilogue");
     return 1;
   }
