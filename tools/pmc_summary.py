@@ -27,7 +27,9 @@ import sys
 ROLES_BF16 = [
     ("lstm_fwd_wide_kernel", ["lstm_fwd_l0", "lstm_fwd_l1"]),
     ("lstm_bwd_wide_kernel", ["lstm_bwd_l1", "lstm_bwd_l0"]),
-    ("gemm256_kernel<true, true, 12>", ["proj_l1", "heads_p1", "heads_dy", "dgrad_l1"]),
+    ("gemm256_kernel<true, true, 12>", ["proj_l1", "dgrad_l1"]),
+    ("heads_nt_kernel<true", ["heads_p1"]),    # from 64K frames the heads' products run on the
+    ("heads_nt_kernel<false", ["heads_dy"]),   # 128-row kernel (heads.hip heads_nt)
     ("gemm256_kernel<false, false, 0>", ["heads_dw1", "wgrad_ih_l1", "wgrad_hh_l1", "wgrad_hh_l0"]),
     ("heads_mid_kernel", ["heads_mid"]),
     ("encoder_fwd_kernel", ["encoder_fwd"]),
@@ -37,13 +39,16 @@ ROLES_BF16 = [
     ("conv_kernel<4, true>", ["conv_dgrad"]),
     ("conv_wgrad_kernel", ["conv_wgrad_l2", "conv_wgrad_l1"]),
 ]
-ROLES_FP8 = [r for r in ROLES_BF16 if not r[0].startswith("gemm256")] + [
+ROLES_FP8 = [r for r in ROLES_BF16 if not r[0].startswith(("gemm256", "heads_nt"))] + [
     ("gemm256_kernel<true, true, 12>", ["heads_p1", "heads_dy"]),
     ("gemm256_kernel<true, true, 8>", ["proj_l1", "dgrad_l1"]),       # e4m3 operands
     ("gemm256_kernel<false, false, 9>", ["wgrad_ih_l1"]),               # e4m3 operands
     ("gemm256_kernel<false, false, 0>", ["heads_dw1", "wgrad_hh_l1", "wgrad_hh_l0"]),
 ]
-ROLES = {"c5": ROLES_FP8}
+# below 64K frames (c2, the c5 shard, c3h) the heads' products stay on the 256² GEMM
+ROLES_SMALL = [r for r in ROLES_BF16 if not r[0].startswith(("gemm256_kernel<true", "heads_nt"))] + [
+    ("gemm256_kernel<true, true, 12>", ["proj_l1", "heads_p1", "heads_dy", "dgrad_l1"])]
+ROLES = {"c5": ROLES_FP8, "c2": ROLES_SMALL, "c3h": ROLES_SMALL}
 
 
 def dispatches(path):
