@@ -139,6 +139,24 @@ __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
   }
   float kl_acc = 0.f;
   const int ntiles = (a.N + 15) / 16;
+  // the wave's next tile's x row pieces and utterance length are loaded one tile ahead
+  // (unconditional loads from clamped addresses: rows past N, columns past F read valid data that
+  // is zeroed / unused), so they are in flight while this tile's MFMAs and stores run
+  f32x4 px[KS0][2];
+  float plen;
+  auto prefetch = [&](int tile_) {
+    const int row_ = tile_ * 16 + l15;
+    const bool rv_ = tile_ < ntiles && row_ < a.N;
+    const size_t rr_ = rv_ ? row_ : 0;
+#pragma unroll
+    for (int kk = 0; kk < KS0; ++kk) {
+      const int k0 = 32 * kk + 8 * q, kc = k0 < F ? k0 : F - 8;
+      px[kk][0] = *reinterpret_cast<const f32x4*>(a.x + rr_ * F + kc);
+      px[kk][1] = *reinterpret_cast<const f32x4*>(a.x + rr_ * F + kc + 4);
+    }
+    plen = a.lens[rr_ / a.T];
+  };
+  prefetch(blockIdx.x * 4 + wave);
   for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += gridDim.x * 4) {
     const int row = tile * 16 + l15;
     const bool rv = row < a.N;
@@ -147,15 +165,12 @@ __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
 #pragma unroll
     for (int kk = 0; kk < KS0; ++kk) {
       const int k0 = 32 * kk + 8 * q;
-      if (k0 < F) {
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(a.x + rr * F + k0);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(a.x + rr * F + k0 + 4);
-        const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        xa[kk] = pack8(v);
-      } else {
-        xa[kk] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
+      const float v[8] = {px[kk][0][0], px[kk][0][1], px[kk][0][2], px[kk][0][3],
+                          px[kk][1][0], px[kk][1][1], px[kk][1][2], px[kk][1][3]};
+      xa[kk] = k0 < F ? pack8(v) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
+    const float clen = plen;
+    prefetch(tile + gridDim.x * 4);
     // E1 = lrelu(x W0^T + b0)
     float h[4][4];
 #pragma unroll
@@ -193,7 +208,7 @@ __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
                   f32x4{ml[j][0], ml[j][1], ml[j][2], ml[j][3]};
     }
     if (rv) {
-      const bool fv = frame_valid(a.lens, row, a.T);
+      const bool fv = row % a.T < valid_frames(clen, a.T);
 #pragma unroll
       for (int jz = 0; jz < 2; ++jz) {
         const int z0 = 16 * jz + 4 * q;
