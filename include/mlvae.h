@@ -339,11 +339,9 @@ int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int tra
  * weight-gradient GEMMs' operand precision) instead of fp32; mux / lvx / dy stay fp32.
  * With bias_ws and saved_bf16 in train mode the work runs in split form: P1 and dY as 256^2
  * GEMMs (bias + LReLU + bf16 epilogue; fp32 dY) around a persistent kernel for the middle stages
- * (same outputs; mlvae_heads_set_mode(1) or MLVAE_HEADS_FUSED=1 keeps the single fused kernel,
- * for A/B timing; returns the previous mode).  saved_bf16 bit 1 (value 3): the split form writes
+ * (same outputs).  saved_bf16 bit 1 (value 3): the split form writes
  * dY as bf16 [N, 2H] (mlvae_lstm_bwd_ex3's dy_bf16 input); an error without the split form. */
 size_t mlvae_heads_bias_workspace_size(int B, int T, int F, int C);
-int mlvae_heads_set_mode(int mode);
 int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
                          const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
                          const float* w2m, const float* b2m, const float* w3m, const float* b3m,

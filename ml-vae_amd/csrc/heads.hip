@@ -996,22 +996,6 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
                                unsigned long long drop_offset, float drop_p,
                                float* ws, size_t ws_bytes, void* stream);
 
-// heads path (diagnostics / A/B): 1 = the single fused kernel in train mode too (default: the
-// split form whenever the saved intermediates are bf16 and the bias sums are in-kernel)
-static int g_heads_fused_only = -1;
-extern "C" int mlvae_heads_set_mode(int mode) {
-  const int prev = g_heads_fused_only;
-  g_heads_fused_only = mode;
-  return prev;
-}
-static bool heads_fused_only() {
-  if (g_heads_fused_only < 0) {
-    const char* e = getenv("MLVAE_HEADS_FUSED");
-    g_heads_fused_only = e && atoi(e) != 0 ? 1 : 0;
-  }
-  return g_heads_fused_only == 1;
-}
-
 extern "C" int mlvae_heads_partials_count(int B, int T) { return (B * T + RT - 1) / RT; }
 
 extern "C" int mlvae_heads_supported(int C, int F, int H2) {
@@ -1157,7 +1141,7 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
   }
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  const bool split = train && bias_ws && (saved_bf16 & 1) && !heads_fused_only();
+  const bool split = train && bias_ws && (saved_bf16 & 1);
   a.wg_ws = nullptr;
   if (wg_ws) {
     const bool mse = loss_type == 1;

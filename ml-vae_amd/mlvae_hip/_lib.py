@@ -63,7 +63,6 @@ _SIGS = {
     "mlvae_elbo_partials_count": [I, I, I],
     "mlvae_heads_partials_count": [I, I],
     "mlvae_heads_supported": [I, I, I],
-    "mlvae_heads_set_mode": [I],
     "mlvae_heads_fused": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
                           P, P, P, P, P, P, P, P, P, P, P, P, P],
     "mlvae_heads_bias_workspace_size": [I, I, I, I],

@@ -41,7 +41,10 @@ def _worker(rank, world, port, q):
     # together) -- the MAX all-reduce the engine runs before the fused Adam
     err = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)
     mdist.allreduce_err(err)
-    q.put((rank, loss3[2].item(), flat.reshape(B, T, C), params, int(err.item())))
+    # numpy copies pickle by value (a CPU tensor is shared by fd via this process's resource
+    # sharer, which may be gone before the parent unpickles it)
+    q.put((rank, loss3[2].item(), flat.reshape(B, T, C).numpy().copy(), params.numpy().copy(),
+           int(err.item())))
     dist.destroy_process_group()
 
 
@@ -72,6 +75,7 @@ def test_two_rank_allreduce_matches_global_masked_mean():
     lr = loss.clone().requires_grad_(True)
     O.apply_lens_to_loss(lr, lens).backward()
     for rank, l, g, params, err in res:
+        g, params = torch.from_numpy(g), torch.from_numpy(params)
         assert abs(l - ref.item()) < 1e-6
         assert torch.allclose(g, lr.grad, atol=1e-7)
         assert torch.equal(params, torch.zeros(5))

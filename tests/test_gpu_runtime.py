@@ -167,7 +167,9 @@ def _dp_worker(rank, world, port, q):
         losses.append(eng.train_step(xg[sl].cuda(), lg[sl].cuda()).clone())
     torch.cuda.synchronize()
     eng.check_errors()
-    q.put((rank, eng.flat.cpu(), torch.stack(losses).cpu()))
+    # numpy copies pickle by value: a CPU tensor in a spawn queue is shared by file descriptor
+    # through this process's resource sharer, which is gone once it exits (GPUTEST r05)
+    q.put((rank, eng.flat.cpu().numpy().copy(), torch.stack(losses).cpu().numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -195,7 +197,8 @@ def _err_worker(rank, world, port, q):
     for _ in range(2):
         eng.train_step(xg[sl].cuda(), torch.ones(B).cuda())
     torch.cuda.synchronize()
-    q.put((rank, before, eng.flat.cpu(), int(eng.err.item()), int(eng.err_skips.item())))
+    q.put((rank, before.numpy().copy(), eng.flat.cpu().numpy().copy(), int(eng.err.item()),
+           int(eng.err_skips.item())))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -217,6 +220,7 @@ def test_a_timeout_on_one_rank_skips_the_update_on_every_rank():
     for p in procs:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
+    res = [(r[0], torch.from_numpy(r[1]), torch.from_numpy(r[2])) + tuple(r[3:]) for r in res]
     for rank, before, after, err, skips in res:
         assert err == 1 and skips == 2, (rank, err, skips)
         assert torch.equal(before, after), rank
@@ -250,5 +254,6 @@ def test_two_gloo_ranks_through_the_engine_equal_one_engine_on_the_global_batch(
     torch.cuda.synchronize()
     full = eng.flat.cpu()
     for rank, flat, ls in res:
+        flat, ls = torch.from_numpy(flat), torch.from_numpy(ls)
         assert torch.allclose(ls, torch.stack(losses).cpu(), rtol=2e-5, atol=1e-7), (rank, ls, losses)
         assert (flat - full).abs().max().item() < 2e-6, (rank, (flat - full).abs().max().item())

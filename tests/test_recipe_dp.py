@@ -50,7 +50,7 @@ def _norm_worker(rank, world, port, q):
     n.train()
     for _ in range(2):
         n(x[2 * rank:2 * rank + 2], lens[2 * rank:2 * rank + 2])
-    q.put((rank, n.glob_mean.clone(), n.glob_std.clone()))
+    q.put((rank, n.glob_mean.numpy().copy(), n.glob_std.numpy().copy()))   # by value, not by fd
     dist.destroy_process_group()
 
 
@@ -74,4 +74,5 @@ def test_normaliser_statistics_are_global_under_data_parallel():
     for _ in range(2):
         ref(x, lens)
     for _, m, s in res:
+        m, s = torch.from_numpy(m), torch.from_numpy(s)
         assert torch.allclose(m, ref.glob_mean, atol=1e-6) and torch.allclose(s, ref.glob_std, atol=1e-6)
