@@ -377,6 +377,27 @@ int mlvae_heads_fused_ex2(int B, int T, int F, int C, int H2, int loss_type, int
                           float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
                           float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
                           float* dw2v, void* stream);
+/* mlvae_heads_fused_ex2 with the split-bf16 forward when w1_split is given (split form only): the
+ * forward products of ref:src/modules/fc_block.py:9-16 as bf16 hi + lo operand pairs -- P1 = LReLU(Y
+ * (W1_hi + W1_lo)^T + b1) on the 128-row kernel, P2 = LReLU(P1 (W2_hi + W2_lo)^T + b2) and OUT =
+ * P2_hi (W3_hi + W3_lo)^T + P2_lo W3_hi^T + b3 -- so mu_x / log_var_x (and the ELBO) carry no bf16
+ * rounding of the heads' weights.  w1_split = mlvae_bf16_split_rows(W1 [2C, 2H], chunk 64).  The
+ * backward products stay bf16. */
+int mlvae_heads_fused_ex3(int B, int T, int F, int C, int H2, int loss_type, int train,
+                          const void* y_bf16, const void* w1_bf16, const void* w1t_bf16, const float* b1,
+                          const float* w2m, const float* b2m, const float* w3m, const float* b3m,
+                          const float* w2v, const float* b2v, const float* w3v, const float* b3v,
+                          const float* x, const float* lens, const int* count, float rec_scale,
+                          float* p1, float* p2m, float* p2v, float* mux, float* lvx, float* dmux,
+                          float* dlvx, float* dp2m, float* dp2v, float* dp1, float* dy,
+                          float* partials, float* bias_ws, size_t bias_ws_bytes, float* db3m,
+                          float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
+                          float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
+                          float* dw2v, const void* w1_split, void* stream);
+/* dst [rows][2 cols] bf16 = src [rows][cols] fp32 as split-bf16 pairs: each chunk-wide column block
+ * c becomes [hi | lo] at columns 2 c chunk .. 2 (c + 1) chunk - 1 (x = hi + lo to ~2^-17).  cols %
+ * chunk == 0. */
+int mlvae_bf16_split_rows(const float* src, int rows, int cols, int chunk, void* dst, void* stream);
 /* Skinny products of the bottom LSTM layer (bf16; one side is the latent width):
  * mlvae_skinny_nt: C [M, N] (fp32, ldc) = A [M, K] . Bt [N, K]^T, bf16 k-contiguous operands,
  *   N in {16, 32, 48, 64}, K % 32 == 0: dZ = dG W_ih over the k-contiguous W_ih^T copy.
@@ -427,6 +448,15 @@ int mlvae_encoder_fwd(int B, int T, int F, int E, int Z, const float* x, const f
                       unsigned long long offset, const float* lens, void* e1_bf16, void* e2_bf16,
                       float* ml, float* z, void* z_bf16, int z_ld, float* eps_out,
                       float* kl_partials, void* stream);
+/* mlvae_encoder_fwd with split = 1: every forward product as a_hi W_hi + a_hi W_lo + a_lo W_hi
+ * (bf16 hi + lo pairs of the fp32 x, activations and weights: mu / log_var / z / KL to ~1e-5 of
+ * fp32 at the same HBM traffic; e1 / e2 are still saved bf16).  split = 0 is mlvae_encoder_fwd. */
+int mlvae_encoder_fwd_ex(int B, int T, int F, int E, int Z, const float* x, const float* w0,
+                         const float* b0, const float* w1, const float* b1, const float* wml,
+                         const float* bml, const float* eps_in, unsigned long long seed,
+                         unsigned long long offset, const float* lens, void* e1_bf16, void* e2_bf16,
+                         float* ml, float* z, void* z_bf16, int z_ld, float* eps_out,
+                         float* kl_partials, int split, void* stream);
 int mlvae_encoder_bwd(int B, int T, int F, int E, int Z, const float* dz, const float* ml,
                       const float* eps, const void* e1_bf16, const void* e2_bf16, const float* x,
                       const float* wml, const float* w1, const float* lens, const int* count,

@@ -76,6 +76,11 @@ __device__ __forceinline__ float bf2f(short s) {
   unsigned u = ((unsigned)(unsigned short)s) << 16;
   return __uint_as_float(u);
 }
+// the low half of a split-bf16 pair: x ~ bf2f(f2bf(x)) + bf2f(f2bf_lo(x)) to ~2^-17 relative
+// (the split forward's operands: a product a_hi b_hi + a_hi b_lo + a_lo b_hi on the bf16 MFMA)
+__device__ __forceinline__ short f2bf_lo(float x) {
+  return f2bf(x - bf2f(f2bf(x)));
+}
 
 // ---- write-through (sc1) hand-off primitives (MI355X_MICROARCH.md "Valid forms" row 1)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {

@@ -61,6 +61,18 @@ __device__ __forceinline__ bf16x8 wfrag_t(const float* W, int ldn, int n, int kk
   return r;
 }
 
+// the low halves of wfrag's elements (split-bf16 forward)
+template <bool PERM>
+__device__ __forceinline__ bf16x8 wfrag_lo(const float* W, int ld, int kmax, int n, int kk, int q) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = PERM ? perm_k(kk, q, e) : 32 * kk + 8 * q + e;
+    r[e] = k < kmax ? f2bf_lo(W[(size_t)n * ld + k]) : (short)0;
+  }
+  return r;
+}
+
 __device__ __forceinline__ bf16x8 pack8(const float* v) {
   return bf16x8{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]),
                 f2bf(v[4]), f2bf(v[5]), f2bf(v[6]), f2bf(v[7])};
@@ -73,6 +85,11 @@ __device__ __forceinline__ bf16x8 next_frag(float (*h)[4], int kk) {
   return bf16x8{f2bf(h[2 * kk][0]), f2bf(h[2 * kk][1]), f2bf(h[2 * kk][2]), f2bf(h[2 * kk][3]),
                 f2bf(h[2 * kk + 1][0]), f2bf(h[2 * kk + 1][1]), f2bf(h[2 * kk + 1][2]),
                 f2bf(h[2 * kk + 1][3])};
+}
+__device__ __forceinline__ bf16x8 next_frag_lo(float (*h)[4], int kk) {
+  return bf16x8{f2bf_lo(h[2 * kk][0]), f2bf_lo(h[2 * kk][1]), f2bf_lo(h[2 * kk][2]), f2bf_lo(h[2 * kk][3]),
+                f2bf_lo(h[2 * kk + 1][0]), f2bf_lo(h[2 * kk + 1][1]), f2bf_lo(h[2 * kk + 1][2]),
+                f2bf_lo(h[2 * kk + 1][3])};
 }
 
 // operand fragment (m or n = base + (lane & 15), k = kk + 8 (lane >> 4) + e) of an LDS image
@@ -113,12 +130,36 @@ int fwd_grid(int N) {
   return g > 256 ? 256 : (g < 1 ? 1 : g);
 }
 
-template <int F>
+// SPL (split-bf16 forward): every product a W^T runs as a_hi W_hi + a_hi W_lo + a_lo W_hi (three
+// bf16 MFMAs, fp32 accumulation), with the fp32 x / E1 / E2 / weights split into bf16 hi + lo pairs
+// in registers -- fp32-grade mu / log_var (and so z, KL) for the same HBM traffic.  The saved
+// E1 / E2 (the backward's operands) stay bf16.  The bf16 rounding of the encoder's weights is a
+// fixed per-step perturbation, not a per-frame one, so it does not average out over the batch:
+// tools/elbo_budget.py attributes to it (with the heads' weights) most of the bf16 step's ELBO error.
+template <int F, bool SPL>
 __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
   constexpr int KS0 = (F + 31) / 32;
   __shared__ float red[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l15 = lane & 15, q = lane >> 4;
   bf16x8 w0f[4][KS0], w1f[4][2], wmf[4][2];
+  // SPL: the weights' lo fragments live in LDS (every wave holds the same fragments; in registers
+  // beside the hi ones they spilled): [fragment][lane], fragment = w0 (j, kk) | w1 (j, kk) | wml (j, kk)
+  constexpr int NLF = SPL ? 4 * KS0 + 16 : 1;
+  __shared__ bf16x8 wlo[NLF][64];
+  if constexpr (SPL) {
+    for (int idx = threadIdx.x; idx < NLF * 64; idx += 256) {
+      const int f = idx >> 6, ln = idx & 63, n_ = ln & 15, q_ = ln >> 4;
+      bf16x8 v;
+      if (f < 4 * KS0) v = wfrag_lo<false>(a.w0, F, F, 16 * (f / KS0) + n_, f % KS0, q_);
+      else if (f < 4 * KS0 + 8) v = wfrag_lo<true>(a.w1, EW, EW, 16 * ((f - 4 * KS0) / 2) + n_, (f - 4 * KS0) % 2, q_);
+      else v = wfrag_lo<true>(a.wml, EW, EW, 16 * ((f - 4 * KS0 - 8) / 2) + n_, (f - 4 * KS0 - 8) % 2, q_);
+      wlo[f][ln] = v;
+    }
+    __syncthreads();
+  }
+  auto w0l = [&](int j, int kk) { return wlo[j * KS0 + kk][lane]; };
+  auto w1l = [&](int j, int kk) { return wlo[4 * KS0 + 2 * j + kk][lane]; };
+  auto wmlo = [&](int j, int kk) { return wlo[4 * KS0 + 8 + 2 * j + kk][lane]; };
   float b0v[4][4], b1v[4][4], bmv[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -130,6 +171,7 @@ __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
       w1f[j][kk] = wfrag<true>(a.w1, EW, EW, n, kk, q);
       wmf[j][kk] = wfrag<true>(a.wml, EW, EW, n, kk, q);
     }
+
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       b0v[j][r] = a.b0[16 * j + 4 * q + r];
@@ -161,13 +203,19 @@ __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
     const int row = tile * 16 + l15;
     const bool rv = row < a.N;
     const size_t rr = rv ? row : 0;
-    bf16x8 xa[KS0];
+    bf16x8 xa[KS0], xl[SPL ? KS0 : 1];
 #pragma unroll
     for (int kk = 0; kk < KS0; ++kk) {
       const int k0 = 32 * kk + 8 * q;
       const float v[8] = {px[kk][0][0], px[kk][0][1], px[kk][0][2], px[kk][0][3],
                           px[kk][1][0], px[kk][1][1], px[kk][1][2], px[kk][1][3]};
       xa[kk] = k0 < F ? pack8(v) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (SPL) {
+        bf16x8 lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) lo[e] = f2bf_lo(v[e]);
+        xl[kk] = k0 < F ? lo : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
     const float clen = plen;
     prefetch(tile + gridDim.x * 4);
@@ -177,31 +225,52 @@ __global__ __launch_bounds__(256) void encoder_fwd_kernel(EncFwdArgs a) {
     for (int j = 0; j < 4; ++j) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < KS0; ++kk) acc = mfma16(w0f[j][kk], xa[kk], acc);
+      for (int kk = 0; kk < KS0; ++kk) {
+        acc = mfma16(w0f[j][kk], xa[kk], acc);
+        if constexpr (SPL) {
+          acc = mfma16(w0l(j, kk), xa[kk], acc);
+          acc = mfma16(w0f[j][kk], xl[kk], acc);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[j][r] = lrelu(acc[r] + b0v[j][r]);
       if (rv) *reinterpret_cast<bf16x4*>(a.e1 + rr * EW + 16 * j + 4 * q) = pack4(h[j]);
     }
     bf16x8 ha[2] = {next_frag(h, 0), next_frag(h, 1)};
+    bf16x8 hl[2];
+    if constexpr (SPL) { hl[0] = next_frag_lo(h, 0); hl[1] = next_frag_lo(h, 1); }
     // E2 = lrelu(E1 W1^T + b1)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) acc = mfma16(w1f[j][kk], ha[kk], acc);
+      for (int kk = 0; kk < 2; ++kk) {
+        acc = mfma16(w1f[j][kk], ha[kk], acc);
+        if constexpr (SPL) {
+          acc = mfma16(w1l(j, kk), ha[kk], acc);
+          acc = mfma16(w1f[j][kk], hl[kk], acc);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[j][r] = lrelu(acc[r] + b1v[j][r]);
       if (rv) *reinterpret_cast<bf16x4*>(a.e2 + rr * EW + 16 * j + 4 * q) = pack4(h[j]);
     }
     ha[0] = next_frag(h, 0);
     ha[1] = next_frag(h, 1);
+    if constexpr (SPL) { hl[0] = next_frag_lo(h, 0); hl[1] = next_frag_lo(h, 1); }
     // [mu | lv] = E2 [Wm; Wv]^T + [bm; bv]: tiles 0-1 mu, 2-3 lv (column 16 j + 4 q + r of ML)
     float ml[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) acc = mfma16(wmf[j][kk], ha[kk], acc);
+      for (int kk = 0; kk < 2; ++kk) {
+        acc = mfma16(wmf[j][kk], ha[kk], acc);
+        if constexpr (SPL) {
+          acc = mfma16(wmlo(j, kk), ha[kk], acc);
+          acc = mfma16(wmf[j][kk], hl[kk], acc);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) ml[j][r] = acc[r] + bmv[j][r];
       if (rv) *reinterpret_cast<f32x4*>(a.ml + rr * 2 * ZW + 16 * j + 4 * q) =
@@ -546,12 +615,27 @@ extern "C" size_t mlvae_encoder_workspace_size(int B, int T, int F, int E, int Z
 // the mlvae_randn stream, written to eps_out if given).  Outputs: e1/e2 bf16 [B*T, E],
 // ml [B*T, 2Z] = [mu | log_var], z [B*T, Z] fp32, z_bf16 [B*T, z_ld] (z_ld = Z, or >= Z + 16:
 // then columns Z..Z+15 = [1, 0, ...]), kl_partials [mlvae_encoder_partials_count] (masked KL sums).
+extern "C" int mlvae_encoder_fwd_ex(int B, int T, int F, int E, int Z, const float* x, const float* w0,
+                                    const float* b0, const float* w1, const float* b1, const float* wml,
+                                    const float* bml, const float* eps_in, unsigned long long seed,
+                                    unsigned long long offset, const float* lens, void* e1_bf16,
+                                    void* e2_bf16, float* ml, float* z, void* z_bf16, int z_ld,
+                                    float* eps_out, float* kl_partials, int split, void* stream);
 extern "C" int mlvae_encoder_fwd(int B, int T, int F, int E, int Z, const float* x, const float* w0,
                                  const float* b0, const float* w1, const float* b1, const float* wml,
                                  const float* bml, const float* eps_in, unsigned long long seed,
                                  unsigned long long offset, const float* lens, void* e1_bf16,
                                  void* e2_bf16, float* ml, float* z, void* z_bf16, int z_ld,
                                  float* eps_out, float* kl_partials, void* stream) {
+  return mlvae_encoder_fwd_ex(B, T, F, E, Z, x, w0, b0, w1, b1, wml, bml, eps_in, seed, offset, lens, e1_bf16,
+                              e2_bf16, ml, z, z_bf16, z_ld, eps_out, kl_partials, 0, stream);
+}
+extern "C" int mlvae_encoder_fwd_ex(int B, int T, int F, int E, int Z, const float* x, const float* w0,
+                                    const float* b0, const float* w1, const float* b1, const float* wml,
+                                    const float* bml, const float* eps_in, unsigned long long seed,
+                                    unsigned long long offset, const float* lens, void* e1_bf16,
+                                    void* e2_bf16, float* ml, float* z, void* z_bf16, int z_ld,
+                                    float* eps_out, float* kl_partials, int split, void* stream) {
   const int N = B * T;
   if (N <= 0) return 0;
   if (!mlvae_encoder_supported(F, E, Z)) {
@@ -574,8 +658,9 @@ extern "C" int mlvae_encoder_fwd(int B, int T, int F, int E, int Z, const float*
   a.zb = static_cast<unsigned short*>(z_bf16);
   a.ml = ml; a.z = z; a.eps_out = eps_out; a.partials = kl_partials;
   hipStream_t st = (hipStream_t)stream;
-  if (F == 80) encoder_fwd_kernel<80><<<fwd_grid(N), 256, 0, st>>>(a);
-  else encoder_fwd_kernel<64><<<fwd_grid(N), 256, 0, st>>>(a);
+  auto k = F == 80 ? (split ? encoder_fwd_kernel<80, true> : encoder_fwd_kernel<80, false>)
+                   : (split ? encoder_fwd_kernel<64, true> : encoder_fwd_kernel<64, false>);
+  k<<<fwd_grid(N), 256, 0, st>>>(a);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }

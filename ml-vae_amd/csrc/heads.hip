@@ -403,14 +403,24 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
 // the stages already hold -- instead of four split-K GEMM launches (+ their reduces) re-reading
 // the saved P2 / dOUT / dP2 from HBM, which are then not written at all.  Each wave owns a quarter
 // of the 16 x 16 output tiles; per-workgroup slabs, reduced in a fixed order (heads_wg_reduce*).
-template <int C, int F, bool WG>
+// SPL (split-bf16 forward, the accurate-ELBO step): stages 2-3 run as P1 (W2_hi + W2_lo)^T and
+// P2_hi (W3_hi + W3_lo)^T + P2_lo W3_hi^T (P2 split in registers, its lo fragment in the encoder's
+// permuted k order, W3_hi read in that order by two 8-byte LDS reads), so mu_x / log_var_x carry
+// the bf16 rounding of no weight (tools/elbo_budget.py: the heads' W2 / W3 rounding is the largest
+// single term of the bf16 step's ELBO error).  The lo images take the room of the transposed
+// W2^T / W3^T images, whose backward fragments are then read transposed from the row-major ones
+// (ds_read_b64_tr_b16); W3's image then has FK zero-padded rows per head.  The backward stages
+// stay bf16.
+template <int C, int F, bool WG, bool SPL>
 __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
   constexpr int C2 = 2 * C, FK = (F + 31) / 32 * 32;
   constexpr int LC = C + 8, LF = FK + 8, L2C = C2 + 8;
   constexpr int NC = C / 16, NF = F / 16, NC2 = C2 / 16;
+  constexpr int W3R = SPL ? FK : F;  // rows per head of the W3 image
   constexpr int O_W2I = 0, O_W2T = O_W2I + 2 * C * LC, O_W3I = O_W2T + 2 * C * LC;
-  constexpr int O_W3T = O_W3I + 2 * F * LC, O_P1 = O_W3T + 2 * C * LF;
+  constexpr int O_W3T = O_W3I + 2 * W3R * LC, O_P1 = O_W3T + 2 * C * LF;  // SPL: W2T = W2 lo, W3T = W3 lo
   constexpr int O_P2 = O_P1 + RT * L2C, O_DO = O_P2 + 2 * RT * LC, O_END = O_DO + 2 * RT * LF;
+  static_assert(!SPL || 2 * F * LC <= 2 * C * LF, "W3 lo image fits the W3^T room");
   static_assert(O_END * 2 <= 160 * 1024, "LDS budget");
   static_assert(C2 == 128, "P1 row = 16 lanes x 16 bytes");
   extern __shared__ __attribute__((aligned(16))) short sm[];
@@ -433,20 +443,35 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
     const int h = idx / (C * C / 4), rem = idx % (C * C / 4), n = rem / (C / 4), k = (rem % (C / 4)) * 4;
     const f32x4 v = *reinterpret_cast<const f32x4*>(a.W2[h] + n * C + k);
     st4bf(sm + O_W2I + h * C * LC + n * LC + k, v);
+    if constexpr (SPL) {
+      *reinterpret_cast<bf16x4*>(sm + O_W2T + h * C * LC + n * LC + k) =
+          bf16x4{f2bf_lo(v[0]), f2bf_lo(v[1]), f2bf_lo(v[2]), f2bf_lo(v[3])};
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sm[O_W2T + h * C * LC + (k + i) * LC + n] = f2bf(v[i]);
+      for (int i = 0; i < 4; ++i) sm[O_W2T + h * C * LC + (k + i) * LC + n] = f2bf(v[i]);
+    }
   }
   for (int idx = tid; idx < 2 * F * (C / 4); idx += 256) {
     const int h = idx / (F * C / 4), rem = idx % (F * C / 4), f = rem / (C / 4), k = (rem % (C / 4)) * 4;
     const f32x4 v = *reinterpret_cast<const f32x4*>(a.W3[h] + f * C + k);
-    st4bf(sm + O_W3I + h * F * LC + f * LC + k, v);
+    st4bf(sm + O_W3I + h * W3R * LC + f * LC + k, v);
+    if constexpr (SPL) {
+      *reinterpret_cast<bf16x4*>(sm + O_W3T + h * F * LC + f * LC + k) =
+          bf16x4{f2bf_lo(v[0]), f2bf_lo(v[1]), f2bf_lo(v[2]), f2bf_lo(v[3])};
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sm[O_W3T + h * C * LF + (k + i) * LF + f] = f2bf(v[i]);
+      for (int i = 0; i < 4; ++i) sm[O_W3T + h * C * LF + (k + i) * LF + f] = f2bf(v[i]);
+    }
   }
   if constexpr (FK > F) {  // zero K padding of W3^T and of the dOUT images (never rewritten)
-    for (int idx = tid; idx < 2 * C * (FK - F); idx += 256) {
-      const int h = idx / (C * (FK - F)), rem = idx % (C * (FK - F));
-      sm[O_W3T + h * C * LF + (rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
+    if constexpr (SPL) {   // (SPL: the padding rows F..FK-1 of each head's W3 image)
+      for (int idx = tid; idx < 2 * (FK - F) * LC; idx += 256)
+        sm[O_W3I + (idx / ((FK - F) * LC)) * W3R * LC + F * LC + idx % ((FK - F) * LC)] = 0;
+    } else {
+      for (int idx = tid; idx < 2 * C * (FK - F); idx += 256) {
+        const int h = idx / (C * (FK - F)), rem = idx % (C * (FK - F));
+        sm[O_W3T + h * C * LF + (rem / (FK - F)) * LF + F + rem % (FK - F)] = 0;
+      }
     }
     for (int idx = tid; idx < 2 * RT * (FK - F); idx += 256) {
       const int h = idx / (RT * (FK - F)), rem = idx % (RT * (FK - F));
@@ -523,8 +548,11 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
       for (int kk = 0; kk < C; kk += 32) {
         const bf16x8 av = lds8(sm + O_P1 + lrow * L2C + h * C + kk + 8 * q);
 #pragma unroll
-        for (int j = 0; j < NC; ++j)
+        for (int j = 0; j < NC; ++j) {
           acc2[h][j] = mfma(lds8(sm + O_W2I + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc2[h][j]);
+          if constexpr (SPL)
+            acc2[h][j] = mfma(lds8(sm + O_W2T + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc2[h][j]);
+        }
       }
 #pragma unroll
       for (int j = 0; j < NC; ++j) {
@@ -541,8 +569,23 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
       for (int kk = 0; kk < C; kk += 32) {
         const bf16x8 av = lds8(sm + O_P2 + h * RT * LC + lrow * LC + kk + 8 * q);
 #pragma unroll
-        for (int j = 0; j < NF; ++j)
-          acc3[h][j] = mfma(lds8(sm + O_W3I + h * F * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc3[h][j]);
+        for (int j = 0; j < NF; ++j) {
+          const short* wr = sm + O_W3I + h * W3R * LC + (16 * j + l15) * LC;
+          acc3[h][j] = mfma(lds8(wr + kk + 8 * q), av, acc3[h][j]);
+          if constexpr (SPL) {
+            acc3[h][j] = mfma(lds8(sm + O_W3T + h * F * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc3[h][j]);
+            // P2_lo W3_hi^T: the lo fragment of k-step kk / 32 straight from the stage-2 results
+            // (tiles 2s, 2s + 1: k = kk + 4 q + r and kk + 16 + 4 q + r), W3_hi read in that order
+            const int s2 = kk / 32;
+            const bf16x8 pl = {f2bf_lo(acc2[h][2 * s2][0]), f2bf_lo(acc2[h][2 * s2][1]),
+                               f2bf_lo(acc2[h][2 * s2][2]), f2bf_lo(acc2[h][2 * s2][3]),
+                               f2bf_lo(acc2[h][2 * s2 + 1][0]), f2bf_lo(acc2[h][2 * s2 + 1][1]),
+                               f2bf_lo(acc2[h][2 * s2 + 1][2]), f2bf_lo(acc2[h][2 * s2 + 1][3])};
+            const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(wr + kk + 4 * q);
+            const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(wr + kk + 16 + 4 * q);
+            acc3[h][j] = mfma(bf16x8{w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]}, pl, acc3[h][j]);
+          }
+        }
       }
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
@@ -621,7 +664,8 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
           const bf16x8 av = lds8(sm + O_DO + h * RT * LF + lrow * LF + kk + 8 * q);
 #pragma unroll
           for (int j = 0; j < NC; ++j)
-            acc5[j] = mfma(lds8(sm + O_W3T + h * C * LF + (16 * j + l15) * LF + kk + 8 * q), av, acc5[j]);
+            acc5[j] = mfma(SPL ? trk(sm + O_W3I + h * W3R * LC, LC, 16 * j, kk, lane)
+                               : lds8(sm + O_W3T + h * C * LF + (16 * j + l15) * LF + kk + 8 * q), av, acc5[j]);
         }
       }
 #pragma unroll
@@ -642,7 +686,8 @@ __global__ __launch_bounds__(256) void heads_mid_kernel(HeadArgs a) {
           const bf16x8 av = lds8(sm + O_P2 + h * RT * LC + lrow * LC + kk + 8 * q);
 #pragma unroll
           for (int j = 0; j < NC; ++j)
-            acc6[j] = mfma(lds8(sm + O_W2T + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc6[j]);
+            acc6[j] = mfma(SPL ? trk(sm + O_W2I + h * C * LC, LC, 16 * j, kk, lane)
+                               : lds8(sm + O_W2T + h * C * LC + (16 * j + l15) * LC + kk + 8 * q), av, acc6[j]);
         }
       }
 #pragma unroll
@@ -754,7 +799,10 @@ int launch_heads(const HeadArgs& a, hipStream_t st) {
 // n-tiles) and are kept across the n-chunks when K is one chunk.  Swapped MFMA operands: lane
 // (l15, q) holds C[row 16 w + l15][16 nt + 4 q + r] -- 8- / 16-byte row stores.
 constexpr int HNT_BN = 128;
-template <bool LRELU, int HNT_BK>
+// SPB (split-bf16 B, the accurate-ELBO step's P1): B is [Nn][2K'] with each 128-wide k-chunk holding
+// [B_hi k 64c .. 64c+63 | B_lo same k] (mlvae_bf16_split_rows), K = 2K'; a piece's A fragments cover
+// the 64 k of its chunk and are used twice, so P1 = A (W1_hi + W1_lo)^T at one pass over A.
+template <bool LRELU, int HNT_BK, bool SPB = false>
 __global__ __launch_bounds__(512) void heads_nt_kernel(int M, int Nn, int K, const unsigned short* __restrict__ A,
                                                        int lda, const unsigned short* __restrict__ B, int ldb,
                                                        void* __restrict__ Cv, int ldc, const float* __restrict__ bias,
@@ -784,15 +832,16 @@ __global__ __launch_bounds__(512) void heads_nt_kernel(int M, int Nn, int K, con
   };
   // A fragments of piece p of block b: rows 16 w + l15 of the block, k-chunk p % kch (a new chunk
   // per piece when K has several chunks; once per block when it has one)
-  auto aload = [&](bf16x8 (&af)[HNT_BK / 32], int b, int p) {
+  constexpr int AKC = SPB ? HNT_BK / 2 : HNT_BK;  // A's k per piece
+  auto aload = [&](bf16x8 (&af)[AKC / 32], int b, int p) {
     const int row = b * 128 + 16 * wave + l15;
-    const unsigned short* arow = A + (size_t)(row < M ? row : M - 1) * lda + (p % kch) * HNT_BK;
+    const unsigned short* arow = A + (size_t)(row < M ? row : M - 1) * lda + (p % kch) * AKC;
 #pragma unroll
-    for (int ks = 0; ks < HNT_BK / 32; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(arow + 32 * ks + 8 * q);
+    for (int ks = 0; ks < AKC / 32; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(arow + 32 * ks + 8 * q);
   };
   int blk = blockIdx.x;
   if (blk >= nblk) return;
-  bf16x8 afr[HNT_BK / 32], anx[HNT_BK / 32];
+  bf16x8 afr[AKC / 32], anx[AKC / 32];
   bload(0);
   aload(afr, blk, 0);
   int buf = 0;
@@ -824,7 +873,8 @@ __global__ __launch_bounds__(512) void heads_nt_kernel(int M, int Nn, int K, con
 #pragma unroll
         for (int nt = 0; nt < HNT_BN / 16; ++nt) {
           const int brow = 32 * (nt >> 1) + 8 * (l15 >> 2) + 4 * (nt & 1) + (l15 & 3);
-          acc[nt] = mfma(*reinterpret_cast<const bf16x8*>(bb + brow * HNT_LB + 32 * ks + 8 * q), afr[ks], acc[nt]);
+          acc[nt] = mfma(*reinterpret_cast<const bf16x8*>(bb + brow * HNT_LB + 32 * ks + 8 * q),
+                         afr[ks % (AKC / 32)], acc[nt]);
         }
       buf ^= 1;
       if (kc == kch - 1 && rv) {
@@ -852,31 +902,36 @@ __global__ __launch_bounds__(512) void heads_nt_kernel(int M, int Nn, int K, con
       }
       if (new_a) {
 #pragma unroll
-        for (int ks = 0; ks < HNT_BK / 32; ++ks) afr[ks] = anx[ks];
+        for (int ks = 0; ks < AKC / 32; ++ks) afr[ks] = anx[ks];
       }
     }
   }
 }
 
 int heads_cus();
+// split_b: B is the split-bf16 [Nn][2K] image (SPB above; K is A's depth, the kernel runs 2K)
 int heads_nt(bool lrelu_bias, int M, int Nn, int K, const void* A, int lda, const void* B, int ldb, void* C,
-             int ldc, const float* bias, bool out_bf16, hipStream_t st) {
+             int ldc, const float* bias, bool out_bf16, hipStream_t st, bool split_b = false) {
   if (M <= 0) return 0;
-  if (Nn % HNT_BN || K % 128 || lda % 8 || ldb % 8 || ldc % 8 || (lrelu_bias && !bias)) {
+  if (Nn % HNT_BN || K % 128 || lda % 8 || ldb % 8 || ldc % 8 || (lrelu_bias && !bias) ||
+      (split_b && (!lrelu_bias || ldb < 2 * K))) {
     mlvae_set_error("heads_nt: Nn %% 128, K %% 128, 16-byte rows and a bias with the LReLU epilogue");
     return 1;
   }
   // k-chunks of 128, two workgroups per CU (k-chunks of 256 at one per CU: c3 heads 0.367 -> 0.375 ms)
   constexpr size_t lds = (size_t)2 * HNT_BN * (128 + 8) * sizeof(short);
   const int nblk = (M + 127) / 128, grid = nblk < 2 * heads_cus() ? nblk : 2 * heads_cus();
-  auto k = lrelu_bias ? heads_nt_kernel<true, 128> : heads_nt_kernel<false, 128>;
-  static bool attr[2] = {false, false};
-  if (!attr[lrelu_bias]) {
+  const int ki = split_b ? 2 : lrelu_bias ? 1 : 0;
+  auto k = split_b ? heads_nt_kernel<true, 128, true>
+                   : lrelu_bias ? heads_nt_kernel<true, 128> : heads_nt_kernel<false, 128>;
+  if (split_b) K *= 2;
+  static bool attr[3] = {false, false, false};
+  if (!attr[ki]) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
       mlvae_set_error("heads_nt: cannot reserve %zu B LDS", lds);
       return 2;
     }
-    attr[lrelu_bias] = true;
+    attr[ki] = true;
   }
   k<<<grid, 512, lds, st>>>(M, Nn, K, static_cast<const unsigned short*>(A), lda,
                             static_cast<const unsigned short*>(B), ldb, C, ldc, bias, out_bf16 ? 1 : 0);
@@ -906,12 +961,12 @@ int mid_grid(int N) {
   return ntiles < cus ? ntiles : cus;
 }
 
-template <int C, int F, bool WG>
+template <int C, int F, bool WG, bool SPL>
 int launch_mid(const HeadArgs& a, hipStream_t st) {
   constexpr int FK = (F + 31) / 32 * 32, LC = C + 8, LF = FK + 8, L2C = 2 * C + 8;
-  constexpr size_t lds = (size_t)(2 * C * LC * 2 + 2 * F * LC + 2 * C * LF + RT * L2C + 2 * RT * LC +
-                                  2 * RT * LF) * sizeof(short);
-  auto k = heads_mid_kernel<C, F, WG>;
+  constexpr size_t lds = (size_t)(2 * C * LC * 2 + 2 * (SPL ? FK : F) * LC + 2 * C * LF + RT * L2C +
+                                  2 * RT * LC + 2 * RT * LF) * sizeof(short);
+  auto k = heads_mid_kernel<C, F, WG, SPL>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -1032,7 +1087,7 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                       float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
                       float* db3m, float* db3v, float* db2m, float* db2v, float* db1, int saved_bf16,
                       float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
-                      float* dw2v, void* stream);
+                      float* dw2v, const void* w1_split, void* stream);
 
 extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_type, int train,
                                  const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
@@ -1046,7 +1101,7 @@ extern "C" int mlvae_heads_fused(int B, int T, int F, int C, int H2, int loss_ty
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
-                    nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, stream);
+                    nullptr, 0, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss_type, int train,
@@ -1063,7 +1118,7 @@ extern "C" int mlvae_heads_fused_ex(int B, int T, int F, int C, int H2, int loss
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
-                    db1, saved_bf16, nullptr, 0, nullptr, nullptr, nullptr, nullptr, stream);
+                    db1, saved_bf16, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 // ... and, with wg_ws, the four small weight gradients dW3 / dW2 of both heads too (written to
@@ -1086,7 +1141,53 @@ extern "C" int mlvae_heads_fused_ex2(int B, int T, int F, int C, int H2, int los
   return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
                     b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
                     dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
-                    db1, saved_bf16, wg_ws, wg_ws_bytes, dw3m, dw3v, dw2m, dw2v, stream);
+                    db1, saved_bf16, wg_ws, wg_ws_bytes, dw3m, dw3v, dw2m, dw2v, nullptr, stream);
+}
+
+// ... and, with w1_split (mlvae_bf16_split_rows of the stacked W1 [2C, 2H], chunk 64), the split-bf16
+// forward: P1 = Y (W1_hi + W1_lo)^T and stages 2-3 on split W2 / W3 / P2 (heads_mid_kernel SPL)
+extern "C" int mlvae_heads_fused_ex3(int B, int T, int F, int C, int H2, int loss_type, int train,
+                                     const void* y_bf16, const void* w1_bf16, const void* w1t_bf16,
+                                     const float* b1, const float* w2m, const float* b2m,
+                                     const float* w3m, const float* b3m, const float* w2v,
+                                     const float* b2v, const float* w3v, const float* b3v,
+                                     const float* x, const float* lens, const int* count,
+                                     float rec_scale, float* p1, float* p2m, float* p2v, float* mux,
+                                     float* lvx, float* dmux, float* dlvx, float* dp2m, float* dp2v,
+                                     float* dp1, float* dy, float* partials, float* bias_ws,
+                                     size_t bias_ws_bytes, float* db3m, float* db3v, float* db2m,
+                                     float* db2v, float* db1, int saved_bf16, float* wg_ws,
+                                     size_t wg_ws_bytes, float* dw3m, float* dw3v, float* dw2m,
+                                     float* dw2v, const void* w1_split, void* stream) {
+  return heads_impl(B, T, F, C, H2, loss_type, train, y_bf16, w1_bf16, w1t_bf16, b1, w2m, b2m, w3m,
+                    b3m, w2v, b2v, w3v, b3v, x, lens, count, rec_scale, p1, p2m, p2v, mux, lvx, dmux,
+                    dlvx, dp2m, dp2v, dp1, dy, partials, bias_ws, bias_ws_bytes, db3m, db3v, db2m, db2v,
+                    db1, saved_bf16, wg_ws, wg_ws_bytes, dw3m, dw3v, dw2m, dw2v, w1_split, stream);
+}
+
+// dst [rows][2 cols] bf16: each chunk-wide column block c of src [rows][cols] fp32 becomes
+// [hi(src block c) | lo(src block c)] at columns 2 c chunk .. (split-bf16 operand images)
+__global__ void bf16_split_rows_kernel(const float* __restrict__ src, int rows, int cols, int chunk,
+                                       unsigned short* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)rows * cols) return;
+  const int r = (int)(i / cols), c = (int)(i % cols), blk = c / chunk, w = c % chunk;
+  const float v = src[i];
+  unsigned short* d = dst + (size_t)r * 2 * cols + (size_t)blk * 2 * chunk + w;
+  d[0] = (unsigned short)f2bf(v);
+  d[chunk] = (unsigned short)f2bf_lo(v);
+}
+extern "C" int mlvae_bf16_split_rows(const float* src, int rows, int cols, int chunk, void* dst, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (!src || !dst || chunk <= 0 || cols % chunk) {
+    mlvae_set_error("mlvae_bf16_split_rows: null pointer or cols %% chunk");
+    return 1;
+  }
+  const long long n = (long long)rows * cols;
+  bf16_split_rows_kernel<<<(unsigned)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      src, rows, cols, chunk, static_cast<unsigned short*>(dst));
+  MLVAE_CHECK_LAUNCH();
+  return 0;
 }
 
 static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int train,
@@ -1100,7 +1201,7 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
                                  float* dp1, float* dy, float* partials, float* bias_ws, size_t bias_ws_bytes,
                                  float* db3m, float* db3v, float* db2m, float* db2v, float* db1,
                                  int saved_bf16, float* wg_ws, size_t wg_ws_bytes, float* dw3m, float* dw3v,
-                                 float* dw2m, float* dw2v, void* stream) {
+                                 float* dw2m, float* dw2v, const void* w1_split, void* stream) {
   if (B <= 0 || T <= 0) return 0;
   if (!mlvae_heads_supported(C, F, H2)) {
     mlvae_set_error("heads: unsupported shape C=%d F=%d 2H=%d (C 64, F 64|80, 2H %% 128)", C, F, H2);
@@ -1153,6 +1254,10 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
     }
     a.wg_ws = wg_ws;
   }
+  if (w1_split && !split) {
+    mlvae_set_error("heads: the split-bf16 forward (w1_split) needs the split form (train, bias_ws, saved_bf16)");
+    return 1;
+  }
   if (dy_bf16 && !split) {
     mlvae_set_error("heads: bf16 dY (saved_bf16 bit 1) needs the split form (train, bias_ws, saved_bf16 bit 0)");
     return 1;
@@ -1163,12 +1268,17 @@ static int heads_impl(int B, int T, int F, int C, int H2, int loss_type, int tra
     // (the 256² GEMM below 64K frames: the 128-row kernel's blocks then leave CUs idle, c2 +6 us)
     const bool nt = g_heads_nt != 0 && (2 * C) % HNT_BN == 0 && H2 % 128 == 0 &&
                     (a.N >= 65536 || g_heads_nt == 2);
-    rc = nt ? heads_nt(true, a.N, 2 * C, H2, y_bf16, H2, w1_bf16, H2, p1, 2 * C, b1, true, st)
-            : mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
-                              nullptr, EPI_LRELU_BF16, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
+    // the split-bf16 forward runs P1 on the 128-row kernel at every size (its split-B form)
+    rc = w1_split ? heads_nt(true, a.N, 2 * C, H2, y_bf16, H2, w1_split, 2 * H2, p1, 2 * C, b1, true, st, true)
+         : nt ? heads_nt(true, a.N, 2 * C, H2, y_bf16, H2, w1_bf16, H2, p1, 2 * C, b1, true, st)
+              : mlvae_gemm_bf16(0, 1, a.N, 2 * C, H2, 1, y_bf16, H2, 0, w1_bf16, H2, 0, p1, 2 * C, 0, 0.f, b1,
+                                nullptr, EPI_LRELU_BF16, nullptr, 0, 0, 0, 0, 0ull, 0ull, 0.f, nullptr, 0, stream);
     if (rc) return rc;
-    if (a.wg_ws) rc = F == 80 ? launch_mid<64, 80, true>(a, st) : launch_mid<64, 64, true>(a, st);
-    else rc = F == 80 ? launch_mid<64, 80, false>(a, st) : launch_mid<64, 64, false>(a, st);
+    const bool spl = w1_split != nullptr;
+    if (a.wg_ws) rc = F == 80 ? (spl ? launch_mid<64, 80, true, true>(a, st) : launch_mid<64, 80, true, false>(a, st))
+                              : (spl ? launch_mid<64, 64, true, true>(a, st) : launch_mid<64, 64, true, false>(a, st));
+    else rc = F == 80 ? (spl ? launch_mid<64, 80, false, true>(a, st) : launch_mid<64, 80, false, false>(a, st))
+                      : (spl ? launch_mid<64, 64, false, true>(a, st) : launch_mid<64, 64, false, false>(a, st));
     if (rc) return rc;
     if (a.wg_ws) {
       const bool mse = loss_type == 1;

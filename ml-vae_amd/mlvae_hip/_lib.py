@@ -71,6 +71,10 @@ _SIGS = {
     "mlvae_heads_fused_ex2": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
                               P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, I,
                               P, SZ, P, P, P, P, P],
+    "mlvae_heads_fused_ex3": [I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, F,
+                              P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, I,
+                              P, SZ, P, P, P, P, P, P],
+    "mlvae_bf16_split_rows": [P, I, I, I, P, P],
     "mlvae_heads_wgrad_workspace_size": [I, I, I, I],
     "mlvae_heads_set_nt_mode": [I],
     "mlvae_skinny_proj": [I, I, I, P, I, P, I, P, P, P, I, P],
@@ -84,6 +88,7 @@ _SIGS = {
     "mlvae_encoder_partials_count": [I, I],
     "mlvae_encoder_workspace_size": [I, I, I, I, I],
     "mlvae_encoder_fwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, U64, U64, P, P, P, P, P, P, I, P, P, P],
+    "mlvae_encoder_fwd_ex": [I, I, I, I, I, P, P, P, P, P, P, P, P, U64, U64, P, P, P, P, P, P, I, P, P, I, P],
     "mlvae_encoder_bwd": [I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, F, P, P, P, P, P, P, P, SZ, P],
     "mlvae_reparam_kl_fwd": [I, I, I, P, I, P, P, P, P, P, P],
     "mlvae_reparam_kl_bwd": [I, I, I, P, I, P, P, P, P, P, F, P, I, P],

@@ -364,6 +364,12 @@ class VAEEngine:
         self.dy_bf16 = cfg.prec == "bf16"
         self.w1_t = (torch.empty(2 * cfg.C * 2 * cfg.H, device=self.device, dtype=torch.bfloat16)
                      if self.fused_heads else None)
+        # the split-bf16 forward of the encoder and the heads (bf16 hi + lo operand pairs: the ELBO,
+        # mu and log_var without the bf16 rounding of those weights -- the bulk of the bf16 step's
+        # ELBO error, tools/elbo_budget.py); False: plain bf16 operands
+        self.split_fwd = cfg.prec == "bf16"
+        self.w1_split = (torch.empty(2 * cfg.C * 4 * cfg.H, device=self.device, dtype=torch.bfloat16)
+                         if self.fused_heads else None)
         # bf16 mode: the encoder (+ reparameterisation + KL) runs as two fused kernels
         # (encoder.hip) and the bottom layer's products on skinny kernels (skinny.hip)
         self.fused_encoder = (cfg.prec == "bf16" and not cfg.enc_conv and
@@ -693,12 +699,13 @@ class VAEEngine:
             # (encoder.hip; ref:src/modules/vanilla_vae.py:21-45)
             ep = lambda n: self._ptr(f"encoder.{n}")
             with self._timed("encoder_fwd"):
-                check(l.mlvae_encoder_fwd(B, T, Fd, E, Z, X, ep("fc.0.blocks.0.weight"), ep("fc.0.blocks.0.bias"),
-                                        ep("fc.0.blocks.2.weight"), ep("fc.0.blocks.2.bias"),
-                                        ep("mean_fc.weight"), ep("mean_fc.bias"),
-                                        None if eps_t is None else _p(eps_t), self.seed, eps_off, _p(lens),
-                                        _pb(w.E1b), _pb(w.E2b), _p(w.ML), _p(w.Zs), _pb(w.Zb), w.ZA,
-                                        _p(w.eps) if eps_t is None else None, _p(w.pke), s), "encoder_fwd")
+                check(l.mlvae_encoder_fwd_ex(B, T, Fd, E, Z, X, ep("fc.0.blocks.0.weight"), ep("fc.0.blocks.0.bias"),
+                                           ep("fc.0.blocks.2.weight"), ep("fc.0.blocks.2.bias"),
+                                           ep("mean_fc.weight"), ep("mean_fc.bias"),
+                                           None if eps_t is None else _p(eps_t), self.seed, eps_off, _p(lens),
+                                           _pb(w.E1b), _pb(w.E2b), _p(w.ML), _p(w.Zs), _pb(w.Zb), w.ZA,
+                                           _p(w.eps) if eps_t is None else None, _p(w.pke), int(self.split_fwd),
+                                           s), "encoder_fwd")
             w.kl_parts = (w.pke, w.nke)
         else:
             # ---- reparameterisation noise
@@ -861,8 +868,13 @@ class VAEEngine:
                        None if mse_h else hg("log_var_fc.blocks.4.weight"), hg("mean_fc.blocks.2.weight"),
                        None if mse_h else hg("log_var_fc.blocks.2.weight")) \
                 if w.heads_wgrad else (None, 0, None, None, None, None)
+            # split-bf16 forward (split form only): P1 on W1 hi + lo, stages 2-3 on split W2 / W3 / P2
+            w1s = self.split_fwd and w.heads_bias and self.w1_split is not None
+            if w1s:
+                check(l.mlvae_bf16_split_rows(hp("mean_fc.blocks.0.weight"), 2 * C, 2 * H, 64, _pb(self.w1_split), s),
+                      "bf16_split_rows")
             with self._timed("heads"):
-                check(l.mlvae_heads_fused_ex2(
+                check(l.mlvae_heads_fused_ex3(
                   B, T, Fd, C, 2 * H, lt, tr, _pb(w.rnn_out_bf), wb("decoder.mean_fc.blocks.0.weight"),
                   _pb(self.w1_t) if train else None, hp("mean_fc.blocks.0.bias"),
                   hp("mean_fc.blocks.2.weight"), hp("mean_fc.blocks.2.bias"),
@@ -874,7 +886,7 @@ class VAEEngine:
                   _p(w.dP2m) if train else None, _p(w.dP2v) if train else None,
                   _p(w.dP1) if train else None, _p(w.dY[cfg.L - 1]) if train else None,
                   _p(w.ph), *bias_args, (3 if w.dy_bf16[cfg.L - 1] else 1) if w.heads_bias else 0,
-                  *wg_args, s), "heads_fused")
+                  *wg_args, _pb(self.w1_split) if w1s else None, s), "heads_fused")
             check(l.mlvae_elbo_finalize(_p(w.kl_parts[0]), w.kl_parts[1], _p(w.ph), w.nh, _p(lens), count, B, T, Z, Fd,
                                         w_kl, w_rec, _p(w.loss), s), "elbo_finalize")
             return w

@@ -42,7 +42,7 @@ def _reference(x, prm, eps, mask, dz, kl_scale):
                 grads=[W0.grad, b0.grad, W1.grad, b1.grad, Wml.grad, bml.grad])
 
 
-def _forward(B, T, F, x, prm, lens, eps=None, seed=0, offset=0):
+def _forward(B, T, F, x, prm, lens, eps=None, seed=0, offset=0, split=0):
     l = lib()
     N = B * T
     bf = dict(device="cuda", dtype=torch.bfloat16)
@@ -53,11 +53,11 @@ def _forward(B, T, F, x, prm, lens, eps=None, seed=0, offset=0):
     d = [p.cuda() for p in prm]
     dx, dl = x.cuda(), lens.cuda()
     de = eps.cuda() if eps is not None else None
-    check(l.mlvae_encoder_fwd(B, T, F, E, Z, P(dx), *[P(t) for t in d],
-                              P(de) if de is not None else None, seed, offset, P(dl),
-                              o["e1"].data_ptr(), o["e2"].data_ptr(), P(o["ml"]), P(o["z"]),
-                              o["zb"].data_ptr(), ZA, None if de is not None else P(o["eps"]),
-                              P(o["parts"]), stream()))
+    check(l.mlvae_encoder_fwd_ex(B, T, F, E, Z, P(dx), *[P(t) for t in d],
+                                 P(de) if de is not None else None, seed, offset, P(dl),
+                                 o["e1"].data_ptr(), o["e2"].data_ptr(), P(o["ml"]), P(o["z"]),
+                                 o["zb"].data_ptr(), ZA, None if de is not None else P(o["eps"]),
+                                 P(o["parts"]), split, stream()))
     torch.cuda.synchronize()
     o["keep"] = (d, dx, dl, de)
     return o
@@ -88,6 +88,35 @@ def test_encoder_forward(B, T, F):
     zb = o["zb"].cpu()
     assert torch.equal(zb[:, :Z], o["z"].cpu().to(torch.bfloat16))
     assert torch.all(zb[:, Z] == 1.0) and torch.all(zb[:, Z + 1:] == 0.0)
+
+
+@pytest.mark.parametrize("B,T,F", CASES)
+def test_encoder_forward_split_bf16(B, T, F):
+    """The split-bf16 forward (mlvae_encoder_fwd_ex split = 1: every product a_hi W_hi + a_hi W_lo +
+    a_lo W_hi) against the fp64 forward WITHOUT operand rounding: mu / log_var / z and the KL sums
+    to ~1e-5 of fp64 (the plain bf16 forward is ~3e-3 away), e1 / e2 still saved as bf16."""
+    need_gpu()
+    x, prm, lens, eps = _inputs(B, T, F, 3 + B + T + F)
+    mask = _mask(lens, T)
+    lrelu = lambda v: torch.nn.functional.leaky_relu(v, 0.01)
+    W0, b0, W1, b1, Wml, bml = [p.double() for p in prm]
+    e1 = lrelu(x.double() @ W0.t() + b0)
+    e2 = lrelu(e1 @ W1.t() + b1)
+    ml = e2 @ Wml.t() + bml
+    mu, lv = ml[:, :Z], ml[:, Z:]
+    z = eps.double() * torch.exp(0.5 * lv) + mu
+    kl = ((-0.5 * (1 + lv - mu * mu - torch.exp(lv))) * mask.double()[:, None]).sum().item()
+    o = _forward(B, T, F, x, prm, lens, eps=eps, split=1)
+    p = _forward(B, T, F, x, prm, lens, eps=eps, split=0)
+    e_ml, e_plain = rel_err(o["ml"], ml), rel_err(p["ml"], ml)
+    e_kl = abs(o["parts"].double().sum().item() - kl) / abs(kl)
+    print(f"\nsplit encoder B={B} T={T} F={F}: ml {e_ml:.2e} (plain bf16 {e_plain:.2e}) z {rel_err(o['z'], z):.2e} "
+          f"KL {e_kl:.2e}")
+    assert e_ml < 5e-5 and rel_err(o["z"], z) < 5e-5 and e_kl < 2e-5
+    assert e_ml < 0.05 * e_plain
+    assert rel_err(o["e1"].float(), e1) < 1e-2 and rel_err(o["e2"].float(), e2) < 1e-2
+    zb = o["zb"].cpu()
+    assert torch.equal(zb[:, :Z], o["z"].cpu().to(torch.bfloat16))
 
 
 def test_encoder_noise_matches_randn():

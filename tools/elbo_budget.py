@@ -46,9 +46,11 @@ def batches(seed=5):
     return out
 
 
-def emulate(p, x, lens, eps, mask, on, split=()):
+def emulate(p, x, lens, eps, mask, on, split=(), wsplit=()):
     """ELBO of the bf16 forward in fp64 with the rounding points in `on` applied.  `split`: the
-    groups whose bf16 operands are instead hi + lo pairs (three products: hi hi + hi lo + lo hi)."""
+    groups whose bf16 operands are instead hi + lo pairs (three products: hi hi + hi lo + lo hi);
+    `wsplit`: the groups whose WEIGHT operand alone is a hi + lo pair (two products a_bf16 (W_hi +
+    W_lo): the activation stays a bf16 operand)."""
     d = lambda t: t.double()
     bf = lambda t: t.to(torch.bfloat16).double()
     f16 = lambda t: t.to(torch.float16).double()
@@ -62,6 +64,9 @@ def emulate(p, x, lens, eps, mask, on, split=()):
         return bf(t)
 
     def mm(a, w, g):        # a w^T with both operands rounded at g (split: drop lo*lo)
+        if g in on and g in wsplit:
+            wh = bf(w)
+            return bf(a) @ (wh + bf(d(w) - wh)).t()
         if g in on and g in split:
             ah, wh = bf(a), bf(w)
             al, wl = bf(d(a) - ah), bf(d(w) - wh)
@@ -139,7 +144,10 @@ def main():
             row = {grp: abs(emulate(params, x, lens, eps, mask, {grp}) - exact) / abs(exact) for grp in GROUPS}
             allr = abs(emulate(params, x, lens, eps, mask, set(GROUPS)) - exact) / abs(exact)
             spl = abs(emulate(params, x, lens, eps, mask, set(GROUPS), split=set(GROUPS)) - exact) / abs(exact)
-            print(f"step {st:4d} ELBO {exact:.5f} | all bf16 {allr:.2e} | all split {spl:.2e} | " +
+            ws = abs(emulate(params, x, lens, eps, mask, set(GROUPS), wsplit={"enc", "heads1", "heads23"})
+                     - exact) / abs(exact)
+            print(f"step {st:4d} ELBO {exact:.5f} | all bf16 {allr:.2e} | all split {spl:.2e} | "
+                  f"enc/heads weights split {ws:.2e} | " +
                   " ".join(f"{k} {v:.1e}" for k, v in row.items()), flush=True)
         params, _ = O.train_step(params, state, x, lens, eps, cfg, mask.unsqueeze(0), impl="aten")
 
