@@ -462,6 +462,12 @@ int mlvae_encoder_bwd(int B, int T, int F, int E, int Z, const float* dz, const 
                       const float* wml, const float* w1, const float* lens, const int* count,
                       float kl_scale, float* dwml, float* dbml, float* dw1, float* db1, float* dw0,
                       float* db0, float* ws, size_t ws_bytes, void* stream);
+/* Data parallel: the step's scalars in a 4-float header before the flat gradient, summed by the
+ * last gradient bucket's all-reduce (one collective instead of a loss-sum and an err-max).  pack =
+ * 1: hdr = [loss3 | err != 0]; pack = 0 (after the sum): loss3 = hdr[0..2], err = 1 when any rank
+ * set it.  ref:src/prepare_experiment.py:12,55 (SpeechBrain run_opts data parallel), the loss
+ * sync of ref:src/models/md_model.py:77-88 fit_batch. */
+int mlvae_dp_scalars(int pack, float* hdr, float* loss3, int* err, void* stream);
 /* out[3] = {kld_loss, recon_loss, w_kl*kld + w_rec*recon}
  * (ref:src/utils/data_utils.py:67-104, ref:src/models/md_model.py:189-213). */
 int mlvae_elbo_finalize(const float* kl_partials, int nk, const float* rec_partials, int nr,

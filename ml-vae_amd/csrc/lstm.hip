@@ -109,7 +109,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
     }
   }
   const bool plain_st = a.xcd_local && group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement);
-  if (a.dbg && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
+  if (DPTR(a) && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
   if (tid == 0) { abort_flag = 0; poll_seq = 0; }
 
   // ---- io wave (IOW): lane (b = lane >> 2, g = lane & 3) moves the 64-byte row segment of
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
     for (int u = 0; u < 16; ++u) d[u * 4] = v[u >> 2][u & 3];
   };
   auto io_store = [&](int s_) {
-    if (s_ < 0 || s_ >= T || (a.dbg_mode & 1)) return;
+    if (s_ < 0 || s_ >= T || (DMODE(a) & 1)) return;
     const int t_ = dir ? T - 1 - s_ : s_;
     const float* src = outr + (s_ & 1) * 16 * OUS;
     if (iobv) {  // activated gates of (b, g)
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
   // plain stores, so the compiler never has to drain those stores to order an aliasing load)
   float gx[4] = {0.f, 0.f, 0.f, 0.f};
   auto load_gx = [&](int s_) {
-    if (valid && s_ < T && !(s_ > 0 && (a.dbg_mode & 2048))) {  // bit 11: timing without prefetch
+    if (valid && s_ < T && !(s_ > 0 && (DMODE(a) & 2048))) {  // bit 11: timing without prefetch
       const int t_ = dir ? T - 1 - s_ : s_;
       const float* gp = a.G + ((size_t)bglob * T + t_) * GLD + dir * 4 * H + j0 + jj;
 #pragma unroll
@@ -204,10 +204,10 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
         const unsigned ebase = (unsigned)(((s - 1) & (NSLOT - 1)) * xslot) + bi * a.Kp + kb + EPL * q;
         u32x4 hv[NL];
         unsigned spins = 0;
-        for (int d = (a.dbg_mode >> 5) & 63; d > 0; --d) __builtin_amdgcn_s_sleep(1);  // diag: delayed first sweep
+        for (int d = (DMODE(a) >> 5) & 63; d > 0; --d) __builtin_amdgcn_s_sleep(1);  // diag: delayed first sweep
         unsigned long long t_issue = 0;
         while (true) {
-          if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
+          if (DPTR(a)) t_issue = __builtin_amdgcn_s_memtime();
 #pragma unroll
           for (int i = 0; i < NL; ++i) hv[i] = ld_sc1_b128(xr, (ebase + i * KSTEP) * sizeof(ET));
           bool ok = true;
@@ -221,11 +221,11 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
             if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
             break;
           }
-          if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
+          if (DMODE(a) & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
         }
         STAMP(1);
         if (tid == 0) poll_seq = s;  // the io wave issues its HBM traffic behind this poll
-        if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
+        if (DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0) {
           a.dbg[(size_t)s * 16 + 5] = t_issue;
           a.dbg[(size_t)s * 16 + 6] = spins;
         }
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_kernel(LstmArgs a) {
       }
     } else {
       load_gx(s + 1);
-      if (valid && !(a.dbg_mode & 1)) {  // saved activations: plain stores, off the critical path
+      if (valid && !(DMODE(a) & 1)) {  // saved activations: plain stores, off the critical path
         float* gp = a.G + n * GLD + dir * 4 * H + j0 + jj;
         gp[0] = ig; gp[H] = fg; gp[2 * H] = gg; gp[3 * H] = og;
         a.Cs[n * YLD + dir * H + j0 + jj] = c;
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
       unsigned spins = 0;
       unsigned long long t_issue = 0;
       while (true) {
-        if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
+        if (DPTR(a)) t_issue = __builtin_amdgcn_s_memtime();
 #pragma unroll
         for (int i = 0; i < NL; ++i) gv[i] = ld_sc1_b128(xr, (ebase + i * KSTEP) * sizeof(ET));
         bool ok = true;
@@ -472,10 +472,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_kernel(LstmArgs a) {
           if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
           break;
         }
-        if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
+        if (DMODE(a) & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
       }
       STAMP(1);
-      if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
+      if (DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0) {
         a.dbg[(size_t)s * 16 + 5] = t_issue;
         a.dbg[(size_t)s * 16 + 6] = spins;
       }
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
       }
   }
   const bool plain_st = a.xcd_local && group_on_one_xcd(a.xtab + gid * NJ, NJ, js, &placement);
-  if (a.dbg && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
+  if (DPTR(a) && blockIdx.x == 0 && tid == 0) a.dbg[7] = (plain_st ? 1 : 0) | (a.xcd_local ? 2 : 0);
   if (tid == 0) abort_flag = 0;
   __syncthreads();
 
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
   struct CellIn { float gi, gf, gg, go, cc, cp, dy; };
   const int j = j0 + uc;
   auto load_cell = [&](int s_, CellIn& c) {
-    if (bvalid && s_ < T && !(s_ > 0 && (a.dbg_mode & 2048))) {  // bit 11: timing without prefetch
+    if (bvalid && s_ < T && !(s_ > 0 && (DMODE(a) & 2048))) {  // bit 11: timing without prefetch
       const int t_ = dir ? s_ : T - 1 - s_;
       const int tp_ = dir ? t_ + 1 : t_ - 1;
       const size_t n_ = (size_t)bglob * T + t_;
@@ -694,10 +694,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
                                         uc * 16 + half * 8);
       u32x4 pv[NPL];
       unsigned spins = 0;
-      for (int d = (a.dbg_mode >> 5) & 63; d > 0; --d) __builtin_amdgcn_s_sleep(1);  // diag: delayed first sweep
+      for (int d = (DMODE(a) >> 5) & 63; d > 0; --d) __builtin_amdgcn_s_sleep(1);  // diag: delayed first sweep
       unsigned long long t_issue = 0;
       while (true) {
-        if (a.dbg) t_issue = __builtin_amdgcn_s_memtime();
+        if (DPTR(a)) t_issue = __builtin_amdgcn_s_memtime();
 #pragma unroll
         for (int i = 0; i < NPL; ++i)
           pv[i] = ld_sc1_b128(xr, (ebase + (unsigned)(pg * NPL + i) * 256u) * sizeof(short));
@@ -709,12 +709,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
           if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
           break;
         }
-        if (a.dbg_mode & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
+        if (DMODE(a) & 16) __builtin_amdgcn_s_sleep(1); else __builtin_amdgcn_s_sleep(4);
       }
       STAMP(1);
       WSTAMP(8);
       load_cell(s + 2, fill);
-      if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {
+      if (DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0) {
         a.dbg[(size_t)s * 16 + 5] = t_issue;
         a.dbg[(size_t)s * 16 + 6] = spins;
       }
@@ -798,7 +798,7 @@ __global__ __launch_bounds__(256) void lstm_bwd_rs_kernel(LstmArgs a) {
       }
     }
     STAMP(4);
-    if (bvalid && !(a.dbg_mode & 1)) {  // dG for the weight-gradient GEMMs: plain stores
+    if (bvalid && !(DMODE(a) & 1)) {  // dG for the weight-gradient GEMMs: plain stores
       const size_t o = n * GLD + dir * 4 * H + j;
       if (a.dGb) {
         unsigned short* gb = a.dGb + o;
@@ -1343,12 +1343,18 @@ extern "C" int mlvae_lstm_bwd(int prec, int B, int T, int H, const float* w_hh_f
 
 // Diagnostics: when set, the next recurrence launches record per-step phase stamps of
 // workgroup 0 into buf[T*8] (s_memtime ticks).  Pass NULL to disable.
+// Needs the diagnostics build (MLVAE_DIAG, lstm_common.h): the shipped library refuses a buffer.
 extern "C" int mlvae_lstm_set_debug(void* buf) {
+  if (buf && !MLVAE_DIAG) {
+    mlvae_set_error("lstm stamps need the diagnostics build (python -m mlvae_hip.build --diag, MLVAE_LIB_PATH)");
+    return 1;
+  }
   g_dbg = reinterpret_cast<unsigned long long*>(buf);
   return 0;
 }
 
-// Diagnostics only (timing experiments): bit0 skips the forward's saved-activation stores,
+// Diagnostics only (timing experiments; the bits read inside the kernels act in the MLVAE_DIAG
+// build only, the launchers' bits -- 12, and 8 of the wide forward -- in both): bit0 skips the forward's saved-activation stores,
 // bit1 enables XCD-local group placement of the reduce-scatter backward (measured at c2: poll
 // round trip 980 vs 1376 cycles, the same step time, and 3 % slower training steps -- the
 // groups take whole XCDs from the side-stream GEMMs), bit2 disables it for the forward,

@@ -5,6 +5,17 @@
 #include "common.h"
 #include <type_traits>
 
+// Diagnostics -- phase / realtime stamps and the debug-mode timing variants of the recurrences'
+// step loops -- compile in only with -DMLVAE_DIAG=1 (python -m mlvae_hip.build --diag ->
+// libmlvae_diag.so, which tools/lstm_stamps.py and friends load through MLVAE_LIB_PATH): the
+// shipped kernels carry no runtime debug branch.  Host-side launch choices (mlvae_lstm_set_debug_mode
+// bits read by the launchers, e.g. 4096 / 256 in the tests) stay runtime in both builds.
+#ifndef MLVAE_DIAG
+#define MLVAE_DIAG 0
+#endif
+#define DMODE(a) (MLVAE_DIAG ? (a).dbg_mode : 0)
+#define DPTR(a) (MLVAE_DIAG ? (a).dbg : (unsigned long long*)nullptr)
+
 namespace {
 
 constexpr int BG = 16;             // utterances per batch group (= MFMA N/M tile)
@@ -89,13 +100,13 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
 // carry no stamp code (it cost the forward 35 spilled SGPRs).
 #define STAMP(ph)                                                              \
   do {                                                                         \
-    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                          \
+    if (DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0)                          \
       a.dbg[(size_t)s * 16 + (ph)] = __builtin_amdgcn_s_memtime();             \
   } while (0)
 // per-wave stamp (lane 0 of every wave of workgroup 0): dbg[s*16 + slot + wave]
 #define WSTAMP(slot)                                                           \
   do {                                                                         \
-    if (a.dbg && blockIdx.x == 0 && (threadIdx.x & 63) == 0)                   \
+    if (DPTR(a) && blockIdx.x == 0 && (threadIdx.x & 63) == 0)                   \
       a.dbg[(size_t)s * 16 + (slot) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
@@ -103,7 +114,7 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
 // slots 8 + k instead of the per-wave poll-completion stamps
 #define IOSTAMP(k)                                                             \
   do {                                                                         \
-    if (DBG && a.dbg && (a.dbg_mode & 16) && blockIdx.x == 0 && threadIdx.x == 256 && \
+    if (DBG && DPTR(a) && (DMODE(a) & 16) && blockIdx.x == 0 && threadIdx.x == 256 && \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + 8 + (k)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
@@ -113,25 +124,25 @@ __device__ bool group_on_one_xcd(unsigned* tab, int members, int me, int* scratc
 constexpr int STW0 = 64, STWN = 32;
 #define LSTAMP_DECL                                                            \
   __shared__ unsigned long long stamp_lds[DBG ? STWN * 16 : 1];                \
-  if (DBG && a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                     \
+  if (DBG && DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0)                     \
     for (int i_ = 0; i_ < STWN * 16; ++i_) stamp_lds[i_] = 0
 #define LSTAMP(ph)                                                             \
   do {                                                                         \
-    if (DBG && a.dbg && blockIdx.x == 0 && threadIdx.x == 0 &&                        \
+    if (DBG && DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0 &&                        \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + (ph)] = __builtin_amdgcn_s_memtime();        \
   } while (0)
 // per-wave stamp (lane 0 of every wave of workgroup 0) into slot 8 + wave
 #define LWSTAMP()                                                              \
   do {                                                                         \
-    if (DBG && a.dbg && !(a.dbg_mode & 16) && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && \
+    if (DBG && DPTR(a) && !(DMODE(a) & 16) && blockIdx.x == 0 && (threadIdx.x & 63) == 0 && \
         (unsigned)(s - STW0) < (unsigned)STWN)                                 \
       stamp_lds[(s - STW0) * 16 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #define LSTAMP_FLUSH()                                                         \
   do {                                                                         \
     if (DBG) __syncthreads();                                                  \
-    if (DBG && a.dbg && blockIdx.x == 0 && threadIdx.x == 0)                   \
+    if (DBG && DPTR(a) && blockIdx.x == 0 && threadIdx.x == 0)                   \
       for (int i_ = 0; i_ < STWN * 16; ++i_)                                   \
         a.dbg[(size_t)STW0 * 16 + i_] = stamp_lds[i_];                         \
   } while (0)
@@ -143,7 +154,7 @@ constexpr int STW0 = 64, STWN = 32;
 // dbg[T * 16 + blockIdx * STWN * 16 + (s - STW0) * 16 + slot].
 #define RTS_DECL                                                               \
   __shared__ unsigned long long rts_lds[DBG ? STWN * 16 : 1];                  \
-  const bool rts_on = DBG && a.dbg && (a.dbg_mode & 8);                        \
+  const bool rts_on = DBG && DPTR(a) && (DMODE(a) & 8);                        \
   if (rts_on)                                                                  \
     for (int i_ = threadIdx.x; i_ < STWN * 16; i_ += blockDim.x) rts_lds[i_] = 0
 #define RTS(slot)                                                              \

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   // exchange slots in use: 2 (every member of a group is producer and consumer of every other,
   // so a slot is rewritten only after all its readers have loaded it); bit 24: all NSLOT
-  const int nlg = (a.dbg_mode & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
+  const int nlg = (DMODE(a) & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // at run time, never assumed (lstm_common.h group_on_one_xcd)
   __shared__ int placement;
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * a.NJ, a.NJ, js, &placement) &&
-                        !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
+                        !(DMODE(a) & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) abort_flag = 0;
 
   const size_t xslot = (size_t)BG * H;  // elements per exchange slot
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const auto rgx = make_rsrc(G16 + (size_t)grp * BG * T * 8 * H, 0xffffffffu);
   // debug bit 10 (timing probe only, outputs wrong): the saved activations and the gx loads
   // addressed time-major (row t * B + b) -- one step's rows of all utterances contiguous in HBM
-  const bool tmaj = (a.dbg_mode & 1024) != 0;
+  const bool tmaj = (DMODE(a) & 1024) != 0;
   auto rowof = [&](int b_, int t_) -> size_t { return tmaj ? (size_t)t_ * a.B + b_ : (size_t)b_ * T + t_; };
   // (the probe's absolute descriptor: range-checked to the gate buffer, at most 4 GB)
   const auto rgx_abs = make_rsrc(G16, (unsigned)min((size_t)a.B * T * 8 * H * 2, (size_t)0xffffffffu));
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   unsigned short* zr = gxr;
   const auto rz = make_rsrc(a.Zb, (unsigned)min((size_t)a.B * T * a.ldz * 2, (size_t)0x7fffffff));
   auto io_load = [&](int s_) {  // input projection of step s_ into gx ring slot s_ & 1
-    if (s_ >= T || (s_ > 0 && (a.dbg_mode & 8192))) return;  // bit 13: timing without the loads
+    if (s_ >= T || (s_ > 0 && (DMODE(a) & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
     if constexpr (ZP) {
       if (wave == 4) {
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     return bits;
   };
   auto io_store = [&](int s_) {  // saved activations of step s_ from out ring slot s_ & 1
-    if (s_ < 0 || s_ >= T || (a.dbg_mode & 1)) return;
+    if (s_ < 0 || s_ >= T || (DMODE(a) & 1)) return;
     const int t_ = dir ? T - 1 - s_ : s_;
     const char* src = outr + (s_ & 1) * 16 * OUB;
     // activated gates (fp16 in the ring already): 16 utt x 4 gates x HJ/8 chunks, LDS -> HBM
@@ -284,8 +284,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // else waves 0-3 poll the hand-off): each instance keeps only its own role's state live,
   // and both pass the same barriers.
   const bool want_drop = a.Ydb || a.Y8;  // a dropout(h) output (bf16 and / or e4m3)
-  const bool late_bits = want_drop && !(a.dbg_mode & (1 << 27));
-  const bool late_dma_s = (2 * a.NB * a.NJ <= 64) != ((a.dbg_mode & (1 << 17)) != 0);
+  const bool late_bits = want_drop && !(DMODE(a) & (1 << 27));
+  const bool late_dma_s = (2 * a.NB * a.NJ <= 64) != ((DMODE(a) & (1 << 17)) != 0);
   auto run = [&](auto io_tag) {
     constexpr bool IO = decltype(io_tag)::value;
     constexpr int MT = IO ? TPI : TPP;         // this wave's tiles
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     float c[MTA];
 #pragma unroll
     for (int t = 0; t < MTA; ++t) c[t] = 0.f;
-    stagger_start(gid, a.dbg_mode);
+    stagger_start(gid, DMODE(a));
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
       IOSTAMP(0);
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (s == 0) read_gx();
       if (s > 0) {
         if (IO) {
-          if (!(a.dbg_mode & 16384))  // bit 14: timing without the wait
+          if (!(DMODE(a) & 16384))  // bit 14: timing without the wait
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gx(s) LDS-DMA has landed
           IOSTAMP(1);
         } else {
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           // a finer retry period (same box, alternating: c3 12.15 -> 11.77 and 12.19 -> 11.98
           // ms/step; at c2's 128 workgroups full sweeps with s_sleep 6 stay 1 % faster).  A/B
           // bit 28: full re-loads with s_sleep 6 at every size; bit 30: s_sleep 1
-          const bool partial = (int)gridDim.x >= 256 && !(a.dbg_mode & (1 << 28));
+          const bool partial = (int)gridDim.x >= 256 && !(DMODE(a) & (1 << 28));
 #pragma unroll
           for (int i = 0; i < PL; ++i) hv[i] = u32x4{tag ^ 1u, 0u, tag ^ 1u, 0u};  // stale: first sweep loads all
           while (true) {
@@ -397,8 +397,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             }
             // a longer back-off thins the L2 poll traffic (3.27 -> 3.20 us/step at B = 256);
             // bit 18: the previous s_sleep(2)
-            if (partial && (a.dbg_mode & (1 << 30))) __builtin_amdgcn_s_sleep(1);
-            else if (partial || (a.dbg_mode & 262144)) __builtin_amdgcn_s_sleep(2);
+            if (partial && (DMODE(a) & (1 << 30))) __builtin_amdgcn_s_sleep(1);
+            else if (partial || (DMODE(a) & 262144)) __builtin_amdgcn_s_sleep(2);
             else __builtin_amdgcn_s_sleep(6);
           }
           LSTAMP(1);
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // waves' cells following both MFMA streams (same box, alternating: c3 12.06 -> 11.99,
         // c2 4.95 -> 4.79 ms/step).  A/B bits: 25 off; 26 the pollers first instead (no gain)
         // (AS: the pollers, owning most tiles, go first)
-        const bool first = AS ? !IO : IO ? !(a.dbg_mode & (1 << 25)) : (a.dbg_mode & (1 << 26)) != 0;
+        const bool first = AS ? !IO : IO ? !(DMODE(a) & (1 << 25)) : (DMODE(a) & (1 << 26)) != 0;
         if (first) __builtin_amdgcn_s_setprio(1);
         // k-chunks in the order KR .. NKC-1, 0 .. KR-1: the chunks whose A-fragments live in LDS
         // first, their fragment reads (and ZP's z-row read) issued with the first batch's h
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       LSTAMP(4);
       RTS(wave);
       IOSTAMP(5);
-      if (!IO && (a.dbg_mode & (1 << 23))) {  // diagnostics: the publish stores' ack latency
+      if (!IO && (DMODE(a) & (1 << 23))) {  // diagnostics: the publish stores' ack latency
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         LSTAMP(5);
       }
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   // exchange slots in use: 2 (every member of a group is producer and consumer of every other,
   // so a slot is rewritten only after all its readers have loaded it); bit 24: all NSLOT
-  const int nlg = (a.dbg_mode & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
+  const int nlg = (DMODE(a) & (1 << 24)) ? 2 : 1, nmask = (1 << nlg) - 1;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
@@ -655,9 +655,9 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
   }
   __shared__ int placement;
   const bool same_xcd = group_on_one_xcd(a.xtab + gid * NJ, NJ, js, &placement) &&
-                        !(a.dbg_mode & 32768);  // bit 15: force write-through hand-offs
+                        !(DMODE(a) & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) abort_flag = 0;
-  if (DBG && a.dbg && (a.dbg_mode & 8) && tid == 0) a.dbg[blockIdx.x] = same_xcd ? 1 : 2;  // (placement)
+  if (DBG && DPTR(a) && (DMODE(a) & 8) && tid == 0) a.dbg[blockIdx.x] = same_xcd ? 1 : 2;  // (placement)
   __syncthreads();
 
   // exchange: [slot][consumer][producer][HJ units][16 utterances] bf16
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     // launch; bit 19 restores the old place).  (The pollers at priority 2 while they poll, so a
     // wave still polling gets the issue slots before its SIMD partner's post-poll work: 1.337 /
     // 1.304, dropped.)
-    const bool early_stage = !(a.dbg_mode & (1 << 19)) && s > 0;
+    const bool early_stage = !(DMODE(a) & (1 << 19)) && s > 0;
     if (s > 0) {
       const unsigned tag = step_tag_lg(s - 1, nlg);
       const size_t sb = (size_t)((s - 1) & nmask) * xslot + (size_t)js * NJ * HJ * 16;
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
           break;
         }
         // BPTT: a shorter back-off (3.03 -> 2.97 us/step at B = 256); bit 18: s_sleep(2)
-        if (a.dbg_mode & 262144) __builtin_amdgcn_s_sleep(2);
+        if (DMODE(a) & 262144) __builtin_amdgcn_s_sleep(2);
         else __builtin_amdgcn_s_sleep(1);
         sweep();
       }
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     LSTAMP(1);
     // per-wave stamps (slots 8 + wave): poll done, or (debug bit 21) reduce done, (bit 22) the
     // cell's A-image writes issued, just before the step barrier
-    if (!(a.dbg_mode & (3 << 21))) LWSTAMP();
+    if (!(DMODE(a) & (3 << 21))) LWSTAMP();
     RTS(8 + wave);
     // step s+1's inputs (landed: the poll waited for every earlier load) to LDS, and step
     // s+2's loads issued right behind this step's hand-off -- one program point per step, so
@@ -868,7 +868,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     // ms/step; at c2's 128 workgroups right after the poll stays 2 % faster).  A/B bit 16:
     // right after the poll at every size.  (The io waves' stores issued before their MFMAs
     // instead of behind their publish, in the forward: c3 12.11 -> 12.48, c2 4.97 -> 5.62.)
-    const bool late_pf = (int)gridDim.x >= 256 && !(a.dbg_mode & (1 << 16));
+    const bool late_pf = (int)gridDim.x >= 256 && !(DMODE(a) & (1 << 16));
     if (!late_pf) load_cell(s + 2);
     LSTAMP(6);
     if (s > 0) {
@@ -897,7 +897,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
       }
     }
     LSTAMP(2);
-    if (a.dbg_mode & (1 << 21)) LWSTAMP();
+    if (DMODE(a) & (1 << 21)) LWSTAMP();
     // cell BPTT -> dG of (utterance cu, unit uc), into the A-image of this step
     char* ab = aimg + (s & 1) * AIMG;
 #pragma unroll
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) bsum[ci][g] += dg[g];
     }
-    if (a.dbg_mode & (1 << 22)) LWSTAMP();
+    if (DMODE(a) & (1 << 22)) LWSTAMP();
     __syncthreads();  // double-buffered A-image: one barrier per step
     LSTAMP(7);
     // (issued before the barrier instead, by each wave as it arrives: c3 BPTT 1.13 -> 1.23 ms)
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     RTS(wave);
     // dG of this step for the weight-gradient GEMMs: 16-byte rows out of the A-image
     // (fp8 mode: also the e4m3 copy for the fp8 dgrad, and the running max |dG|)
-    if (!(a.dbg_mode & 1)) {
+    if (!(DMODE(a) & 1)) {
       constexpr int NSL = 16 * 4 * HJ / 8;  // 16-byte slots
       const int t = dir ? s : T - 1 - s;
       for (int sl = tid; sl < NSL; sl += 512) {
@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
     }
     return true;
   };
-  stagger_start(gid, a.dbg_mode);
+  stagger_start(gid, DMODE(a));
   for (int s = 0; s < T; ++s)
     if (!step(s)) break;
   LSTAMP_FLUSH();

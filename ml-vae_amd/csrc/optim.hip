@@ -355,3 +355,25 @@ extern "C" int mlvae_dropout(size_t n, const float* x, float* y, const float* ma
                              unsigned long long seed, float p, void* stream) {
   return mlvae_dropout_ex(n, x, y, nullptr, mask, seed, 0ull, p, stream);
 }
+
+// ---- data parallel: the step's scalars ride in the gradient all-reduce.  hdr[4] is a float
+// header placed right before the flat gradient (one contiguous all-reduce with the last bucket):
+// pack writes [loss3 | err != 0], unpack reads the SUMMED header back -- loss3 = the global loss
+// shares, err = set when any rank's recurrence timed out (the fused Adam then skips the update on
+// every rank).  One collective instead of the separate loss-sum and err-max ones.
+__global__ void dp_scalars_kernel(int pack, float* hdr, float* loss3, int* err) {
+  if (threadIdx.x || blockIdx.x) return;
+  if (pack) {
+    hdr[0] = loss3[0]; hdr[1] = loss3[1]; hdr[2] = loss3[2];
+    hdr[3] = *err != 0 ? 1.f : 0.f;
+  } else {
+    loss3[0] = hdr[0]; loss3[1] = hdr[1]; loss3[2] = hdr[2];
+    if (hdr[3] > 0.f && *err == 0) *err = 1;
+  }
+}
+extern "C" int mlvae_dp_scalars(int pack, float* hdr, float* loss3, int* err, void* stream) {
+  if (!hdr || !loss3 || !err) { mlvae_set_error("dp_scalars: null pointer"); return 1; }
+  dp_scalars_kernel<<<1, 64, 0, (hipStream_t)stream>>>(pack, hdr, loss3, err);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}

@@ -75,6 +75,7 @@ _SIGS = {
                               P, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P, P, P, P, I,
                               P, SZ, P, P, P, P, P, P],
     "mlvae_bf16_split_rows": [P, I, I, I, P, P],
+    "mlvae_dp_scalars": [I, P, P, P, P],
     "mlvae_heads_wgrad_workspace_size": [I, I, I, I],
     "mlvae_heads_set_nt_mode": [I],
     "mlvae_skinny_proj": [I, I, I, P, I, P, I, P, P, P, I, P],

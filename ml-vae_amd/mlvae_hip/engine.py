@@ -336,7 +336,10 @@ class VAEEngine:
         n = self.layout.total
         f = dict(device=self.device, dtype=torch.float32)
         self.flat = torch.zeros(n, **f)
-        self.grad = torch.zeros(n, **f)
+        # the flat gradient sits behind a 4-float header: in data parallel the step's loss shares
+        # and err word ride in the last gradient bucket's all-reduce (mlvae_dp_scalars)
+        self._grad_ext = torch.zeros(4 + n, **f)
+        self.grad = self._grad_ext[4:]
         self.exp_avg = torch.zeros(n, **f)
         self.exp_avg_sq = torch.zeros(n, **f)
         self.step_ctr = torch.zeros(1, device=self.device, dtype=torch.int32)
@@ -1330,17 +1333,22 @@ class VAEEngine:
         self._ar_pending = True
 
     def _allreduce_grads(self, w):
+        """The last gradient bucket (the prefix, or the whole buffer) with the step's scalars in
+        its header: loss3 summed, and the skip-on-timeout decision made global -- a rank whose
+        recurrence timed out contributed an undefined share to the summed gradient, so every rank
+        skips that update.  Per step a rank issues three collectives: the frame count (forward),
+        the suffix bucket (during the lower layers' BPTT) and this one."""
         from . import dist as mdist
+        l, s = lib(), self._stream()
+        hdr = self._grad_ext
+        check(l.mlvae_dp_scalars(1, _p(hdr), _p(w.loss), self.err.data_ptr(), s), "dp_scalars")
         if self._ar_pending:
             torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
-            mdist.allreduce_grad_bucket(self.grad[:self.ar_split], self.process_group)
+            mdist.allreduce_grad_bucket(hdr[:4 + self.ar_split], self.process_group)
             self._ar_pending = False
         else:
-            mdist.allreduce_grad_bucket(self.grad, self.process_group)
-        mdist.allreduce_loss(w.loss, self.process_group)
-        # the skip-on-timeout decision is global: a rank whose recurrence timed out contributed
-        # an undefined share to the summed gradient, so every rank skips that update
-        mdist.allreduce_err(self.err, self.process_group)
+            mdist.allreduce_grad_bucket(hdr, self.process_group)
+        check(l.mlvae_dp_scalars(0, _p(hdr), _p(w.loss), self.err.data_ptr(), s), "dp_scalars")
 
     def _main(self):
         """Context: run on the high-priority main stream, ordered after (and before) the

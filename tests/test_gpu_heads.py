@@ -360,9 +360,11 @@ def test_heads_split_bf16_forward(loss_type, B, T, F, H2):
     lr = lambda t: torch.where(t > 0, t, 0.01 * t)
     pre64 = d(Y) @ d(W1).t() + d(b1)
     p1_64 = lr(pre64)
-    big = p1_64.abs() > 1e-3 * p1_64.abs().max()
-    ulp = (d(o["p1"]) - p1_64).abs()[big] / p1_64.abs()[big]
-    ulp_plain = (d(p["p1"]) - p1_64).abs()[big] / p1_64.abs()[big]
+    # relative to |P1| with a floor (an entry near 0 after cancellation carries the fp32 sum's
+    # absolute error): the split P1 is within half a bf16 ulp of fp64, the plain one is not
+    den = p1_64.abs() + 1e-3 * p1_64.abs().max()
+    ulp = (d(o["p1"]) - p1_64).abs() / den
+    ulp_plain = (d(p["p1"]) - p1_64).abs() / den
     # stages 2-3 from the kernel's own bf16 P1 (the mid kernel's input)
     outs, rec_sum = [], 0.0
     for h in range(2):
@@ -382,7 +384,7 @@ def test_heads_split_bf16_forward(loss_type, B, T, F, H2):
     e_rec_plain = abs(p["parts"].double().sum().item() - rec_sum) / abs(rec_sum)
     print(f"\nsplit heads lt={loss_type} B={B} T={T} H2={H2}: P1 max {ulp.max():.2e} (plain {ulp_plain.max():.2e}) "
           f"mu_x {e_mu:.2e} (plain {e_mu_plain:.2e}) log_var_x {e_lv:.2e} rec sum {e_rec:.2e} (plain {e_rec_plain:.2e})")
-    assert ulp.max() <= 2.0 ** -8 and ulp_plain.max() > ulp.max()
+    assert ulp.max() <= 1.1 * 2.0 ** -8 and ulp_plain.max() > ulp.max()   # half a bf16 ulp (+ fp32 sums)
     assert e_mu < 5e-5 and e_lv < 5e-5 and e_rec < 2e-5
     assert e_mu < 0.1 * e_mu_plain
     # the backward stays the plain split form's bf16 products, on this forward's (more exact) P1 /

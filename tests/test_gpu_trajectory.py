@@ -11,8 +11,8 @@ randomness is the engine's own (in-kernel eps read back, dropout masks replayed 
 * Teacher-forced: before EVERY step the oracle (oracle/vae_cpu.py) is handed the engine's state
   (parameters, Adam moments, step count) and takes the same step.  The ELBO of every step -- on a
   model that has learned, so the decoder's outputs decide it -- and the Adam update are compared:
-  fp32 mode (the north-star "ELBO within 1e-4 relative" mode) <= 1e-4 at every step; bf16 mode
-  <= BF16_ELBO (measured).
+  fp32 mode <= 1e-4 at every step, and the benchmarked bf16 mode (split-bf16 encoder / heads
+  forward) <= 1e-4 at every step too -- the north star's "ELBO within 1e-4 relative".
 * Free-running, fp64-anchored (round 5): the engine and the fp32 oracle each train their OWN copy
   from the same init for 100 steps, and the fp64 oracle a third on the same (exactly promoted)
   inputs and randomness.  Two fp32 implementations that round differently drift apart through the
@@ -38,7 +38,10 @@ F, E, Z, H, L, C = 80, 64, 32, 512, 2, 64
 B, T = 8, 100
 STEPS = 160
 FREE_STEPS = 100
-BF16_ELBO = 2e-3
+# the benchmarked bf16 step holds the north star too (round 6): its ELBO error was the bf16
+# rounding of the encoder's and the heads' weights (tools/elbo_budget.py), which the split-bf16
+# forward removes (VAEEngine.split_fwd); measured max 7.0e-5 over the 160 steps (was 4.5e-4)
+BF16_ELBO = 1e-4
 
 
 def _batches(seed=5):
