@@ -76,6 +76,7 @@ class Brain:
             meta = getattr(self.checkpointer, "recovered_meta", None) or {}
             if INTRA_EPOCH_CKPT_FLAG in meta:
                 self._resume_batches = int(meta.get("batches_done", 0))
+                self._resume_meta = meta
 
     def init_optimizers(self):
         if self.opt_class is not None:
@@ -162,6 +163,11 @@ class Brain:
             last_ckpt = time.time()
             skip, self._resume_batches = self._resume_batches, 0
             self._batches_skipped = skip
+            if skip:
+                self._check_resume_signature(train_set)
+            if skip and hasattr(train_set, "skip_next"):
+                train_set.skip_next(skip)   # index-level: the trained batches are not collated
+                skip = 0
             for i, batch in enumerate(train_set):
                 if i < skip:  # trained before the intra-epoch checkpoint this run resumed from
                     continue
@@ -175,7 +181,7 @@ class Brain:
                 if (self.checkpointer is not None and self.ckpt_interval_minutes > 0
                         and time.time() - last_ckpt >= self.ckpt_interval_minutes * 60.0):
                     if self.rank == 0:
-                        self._save_intra_epoch_ckpt()
+                        self._save_intra_epoch_ckpt(train_set)
                     last_ckpt = time.time()
             self.avg_train_loss = self._stage_loss(acc)
             self.on_stage_end(Stage.TRAIN, self.avg_train_loss, epoch)
@@ -197,11 +203,30 @@ class Brain:
             if self.debug and epoch == self.debug_epochs:
                 break
 
-    def _save_intra_epoch_ckpt(self):
+    def _save_intra_epoch_ckpt(self, train_set=None):
+        meta = {INTRA_EPOCH_CKPT_FLAG: True, "batches_done": self.step + self._batches_skipped}
+        sig = getattr(train_set, "signature", None)
+        if sig is not None:   # what a resume must match to skip the same utterances
+            meta.update({"loader_" + k: v for k, v in sig().items()})
         self.checkpointer.save_and_keep_only(
-            end_of_epoch=False, num_to_keep=1,
-            meta={INTRA_EPOCH_CKPT_FLAG: True, "batches_done": self.step + self._batches_skipped},
+            end_of_epoch=False, num_to_keep=1, meta=meta,
             ckpt_predicate=lambda meta: INTRA_EPOCH_CKPT_FLAG in meta)
+
+    def _check_resume_signature(self, train_set):
+        """An intra-epoch resume skips `batches_done` batches by count: refuse it when the batch
+        size, world size, sorting or epoch length differ from the saving run's (the count would
+        then skip the wrong utterances or retrain some)."""
+        meta = getattr(self, "_resume_meta", None) or {}
+        sig = getattr(train_set, "signature", None)
+        if sig is None:
+            return
+        bad = {k: (meta["loader_" + k], v) for k, v in sig().items()
+               if "loader_" + k in meta and meta["loader_" + k] != v}
+        if bad:
+            raise RuntimeError("intra-epoch checkpoint was saved with a different data layout "
+                               + ", ".join(f"{k}: saved {a!r}, now {b!r}" for k, (a, b) in bad.items())
+                               + "; resume with the same batch size / world size / sorting, or "
+                               "start the epoch over from an end-of-epoch checkpoint")
 
     def evaluate(self, test_set, max_key=None, min_key=None, progressbar=None,
                  test_loader_kwargs=None):

@@ -51,19 +51,50 @@ def _empty_like(e):
     return d
 
 
-def _batched(items, batch_size, rank=0, world=1, stage=None):
+def _batched(items, batch_size, rank=0, world=1, stage=None, skip=0):
+    """skip: the first `skip` batches are passed over at the index level (not collated)."""
     if world <= 1:
-        for i in range(0, len(items), batch_size):
+        for i in range(skip * batch_size, len(items), batch_size):
             yield PaddedBatch(items[i:i + batch_size])
         return
     g = batch_size * world
     train = stage is None or getattr(stage, "name", str(stage)).upper() == "TRAIN"
     end = len(items) - g + 1 if train else len(items)
-    for i in range(0, max(end, 0), g):
+    for i in range(skip * g, max(end, 0), g):
         glob = items[i:i + g]
         mine = glob[rank * batch_size:(rank + 1) * batch_size]
         mine = mine + [_empty_like(glob[0])] * (batch_size - len(mine))
         yield PaddedBatch(mine, pad_to=_seq_max(glob))
+
+
+class BatchLoader:
+    """The batches of one split, re-iterable: every pass (epoch) is a fresh walk over the items,
+    as a DataLoader is (a bare generator would leave every epoch after the first empty).
+    skip_next(n) makes the next pass start at batch n -- the resume point of an intra-epoch
+    checkpoint -- without collating the batches it passes over.  `signature` is what must match
+    for such a resume to skip the right utterances (batch size, world size, sorting, length)."""
+
+    def __init__(self, items, batch_size, rank=0, world=1, stage=None, sorting=None):
+        self.items, self.batch_size, self.rank, self.world = items, batch_size, rank, world
+        self.stage, self.sorting = stage, sorting
+        self._skip = 0
+
+    def __len__(self):
+        g = self.batch_size * self.world
+        train = self.world > 1 and (self.stage is None or
+                                    getattr(self.stage, "name", str(self.stage)).upper() == "TRAIN")
+        return len(self.items) // g if train else (len(self.items) + g - 1) // g
+
+    def skip_next(self, n):
+        self._skip = int(n)
+
+    def __iter__(self):
+        skip, self._skip = self._skip, 0
+        return _batched(self.items, self.batch_size, self.rank, self.world, self.stage, skip)
+
+    def signature(self):
+        return {"batch_size": self.batch_size, "world_size": self.world, "sorting": self.sorting,
+                "n_batches": len(self)}
 
 
 def _storage_from_bytes(b):
@@ -128,12 +159,13 @@ class PickledSet:
                 e[k] = v
             self.items.append(e)
         _sort(self.items, sorting)
+        self.sorting = sorting
 
     def __len__(self):
         return len(self.items)
 
     def batches(self, stage=None, batch_size=8, rank=0, world=1, **_):
-        return _batched(self.items, batch_size, rank, world, stage)
+        return BatchLoader(self.items, batch_size, rank, world, stage, self.sorting)
 
 
 class SyntheticSet:
@@ -146,12 +178,13 @@ class SyntheticSet:
             x = (x - x.mean()) / x.std()
             self.items.append({"id": f"utt{i:05d}", "feat": x})
         _sort(self.items, sorting)
+        self.sorting = sorting
 
     def __len__(self):
         return len(self.items)
 
     def batches(self, stage=None, batch_size=8, rank=0, world=1, **_):
-        return _batched(self.items, batch_size, rank, world, stage)
+        return BatchLoader(self.items, batch_size, rank, world, stage, self.sorting)
 
 
 def computed_dataset_dir(hparams):

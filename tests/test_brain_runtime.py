@@ -287,3 +287,76 @@ def test_resume_from_intra_epoch_checkpoint_skips_trained_batches(tmp_path, monk
     b2, ec2 = make(crash_after=-1)
     b2.fit(ec2, data)
     assert b2.trained == [4, 5]   # batches 0-3 were in the checkpoint; 4 was lost with the crash
+
+
+def _toy_brain(tmp_path, clock, epochs, bs_log):
+    import brain.core as core
+    from brain import Checkpointer, EpochCounter
+    from brain.core import Brain, Stage
+
+    class Toy(Brain):
+        def compute_forward(self, batch, stage):
+            return self.modules["lin"](batch["feat"][0])
+
+        def compute_objectives(self, out, batch, stage):
+            clock[0] += 40.0
+            return out.pow(2).mean()
+
+        def fit_batch(self, batch):
+            bs_log.append(tuple(batch["id"]))
+            if len(bs_log) == self.crash_after:
+                raise KeyboardInterrupt
+            return self.compute_objectives(self.compute_forward(batch, Stage.TRAIN), batch, Stage.TRAIN).detach()
+
+    lin = torch.nn.Linear(4, 2)
+    ec = EpochCounter(epochs)
+    ck = Checkpointer(tmp_path, {"lin": lin, "epoch_counter": ec})
+    b = Toy(modules={"lin": lin}, opt_class=lambda p: torch.optim.SGD(p, lr=0.1),
+            run_opts={"device": "cpu", "ckpt_interval_minutes": 1.0}, checkpointer=ck)
+    b.crash_after = -1
+    del core
+    return b, ec
+
+
+def test_every_epoch_walks_the_dataset_and_a_resume_skips_by_index(tmp_path, monkeypatch):
+    """The loaders are re-iterable (a bare generator left every epoch after the first empty), an
+    intra-epoch resume skips the trained batches without collating them, and it is refused when
+    the batch size differs from the saving run's (the count would skip the wrong
+    utterances)."""
+    import brain.core as core
+    from utils.data_io import SyntheticSet
+    clock = [1000.0]
+    monkeypatch.setattr(core.time, "time", lambda: clock[0])
+    ds = SyntheticSet(12, 4, 3, 6, seed=3)
+    seen = []
+    b, ec = _toy_brain(tmp_path / "a", clock, 2, seen)
+    b.fit(ec, ds, train_loader_kwargs={"batch_size": 3})
+    assert len(seen) == 8 and seen[:4] == seen[4:]          # both epochs saw all 4 batches
+    # crash after 3 batches of a run, resume: batches 0-1 were checkpointed (40 s per batch,
+    # one checkpoint a minute), so the resumed epoch starts at batch 2
+    seen2 = []
+    b2, ec2 = _toy_brain(tmp_path / "b", clock, 1, seen2)
+    b2.crash_after = 3
+    try:
+        b2.fit(ec2, ds, train_loader_kwargs={"batch_size": 3})
+    except KeyboardInterrupt:
+        pass
+    seen3 = []
+    b3, ec3 = _toy_brain(tmp_path / "b", clock, 1, seen3)
+    collated = []
+    from brain import dataio
+    real = dataio.PaddedBatch.__init__
+    monkeypatch.setattr(dataio.PaddedBatch, "__init__",
+                        lambda self, items, *a, **k: (collated.append(len(items)), real(self, items, *a, **k))[1])
+    b3.fit(ec3, ds, train_loader_kwargs={"batch_size": 3})
+    assert seen3 == seen[2:4] and len(collated) == 2       # only the two remaining batches built
+    # the same checkpoint under another batch size: refused
+    b4, ec4 = _toy_brain(tmp_path / "c", clock, 1, [])
+    b4.crash_after = 3
+    try:
+        b4.fit(ec4, ds, train_loader_kwargs={"batch_size": 3})
+    except KeyboardInterrupt:
+        pass
+    b5, ec5 = _toy_brain(tmp_path / "c", clock, 1, [])
+    with pytest.raises(RuntimeError, match="batch_size"):
+        b5.fit(ec5, ds, train_loader_kwargs={"batch_size": 4})

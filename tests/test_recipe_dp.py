@@ -30,7 +30,7 @@ def test_pickled_computed_dataset_loads_and_pads(tmp_path):
         pickle.dump(data, f)
     ds = PickledSet(tmp_path / "train.pkl")
     assert len(ds) == 5 and ds.items[0]["feat"].shape[0] == 24  # descending sort
-    b = next(ds.batches(batch_size=3))
+    b = next(iter(ds.batches(batch_size=3)))
     feats, lens = b["feat"]
     assert feats.shape == (3, 24, 5) and torch.allclose(lens, torch.tensor([1.0, 23 / 24, 22 / 24]))
     seqs, slens = b["gt_cnncl_seq"]
