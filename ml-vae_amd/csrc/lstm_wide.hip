@@ -487,6 +487,11 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         hvals[t] = valid ? og * tanh_fast(c[t]) : 0.f;
         gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
       }
+      if (DBG && !(DMODE(a) & (1 << 23))) {  // diagnostics: cell math done (slot 5)
+        __builtin_amdgcn_sched_barrier(0);
+        LSTAMP(5);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (s + 1 < T) {
         // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
         const unsigned tag = step_tag_lg(s, nlg);

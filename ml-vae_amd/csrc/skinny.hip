@@ -204,10 +204,14 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
   f32x4 acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // staging roles: A chunk = 64 frames x 8 pieces of 16 B; B chunk = 64 frames x NB/8 pieces
+  // staging roles: A chunk = 64 frames x 8 pieces of 16 B; B chunk = 64 frames x NB/8 pieces.
+  // The next chunk's loads are issued before this chunk's MFMAs (one register set ahead): with a
+  // load -> LDS -> MFMA loop each chunk cost one exposed HBM round trip (c5's 32,000 frames:
+  // 142 us for 262 MB, 1.8 TB/s)
   constexpr int PB = 64 * NB / 8;
-  for (int k0 = kbeg; k0 < kend; k0 += 64) {
-    u32x4 va[2], vb[(PB + 255) / 256];
+  constexpr int NVB = (PB + 255) / 256;
+  u32x4 va[2], vb[NVB];
+  auto load = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i, fr = idx >> 3, c8 = idx & 7;
@@ -215,12 +219,15 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
       va[i] = f < kend ? *reinterpret_cast<const u32x4*>(A + (size_t)f * lda + m0 + 8 * c8) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int i = 0; i < (PB + 255) / 256; ++i) {
+    for (int i = 0; i < NVB; ++i) {
       const int idx = tid + 256 * i, fr = idx / (NB / 8), c8 = idx % (NB / 8);
       const int f = k0 + fr;
       vb[i] = (idx < PB && f < kend) ? *reinterpret_cast<const u32x4*>(B + (size_t)f * ldb + 8 * c8)
                                      : u32x4{0u, 0u, 0u, 0u};
     }
+  };
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += 64) {
     __syncthreads();  // previous chunk's fragments are consumed
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -228,11 +235,12 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
       *reinterpret_cast<u32x4*>(sa + fr * LA + 8 * c8) = va[i];
     }
 #pragma unroll
-    for (int i = 0; i < (PB + 255) / 256; ++i) {
+    for (int i = 0; i < NVB; ++i) {
       const int idx = tid + 256 * i, fr = idx / (NB / 8), c8 = idx % (NB / 8);
       if (idx < PB) *reinterpret_cast<u32x4*>(sb + fr * LB + 8 * c8) = vb[i];
     }
     __syncthreads();
+    if (k0 + 64 < kend) load(k0 + 64);  // in flight under this chunk's MFMAs
     // wave w: m rows 16w .. 16w+15 (A^T fragment by transposed reads), all NB columns
     const int g = lane >> 4, i4 = lane & 15, qq = i4 >> 2, pp = i4 & 3;
 #pragma unroll
@@ -472,9 +480,11 @@ __global__ __launch_bounds__(256) void skinny_proj_kernel(int M, int N, int K,
   }
 }
 
+// frame splits: ~2048 workgroups (several per CU: each holds only 8 KB of A in flight, so the
+// bytes in flight chip-wide -- not the CU count -- set the stream rate; 512 ran at 1.8 TB/s)
 int tn_splits(int M, int K) {
   const int mb = (M + 63) / 64;
-  int s = (512 + mb - 1) / mb;
+  int s = (2048 + mb - 1) / mb;
   const int maxs = (K + 255) / 256;  // >= 4 chunks of 64 frames per split
   if (s > maxs) s = maxs;
   return s < 1 ? 1 : s;

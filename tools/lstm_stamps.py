@@ -77,7 +77,8 @@ def main():
     w = d[w0:w0 + wn]
     names = ({1: "poll done", 5: "cell inputs staged", 6: "prefetch issued", 2: "reduce done",
               7: "barrier", 3: "prefetch issued (late)", 4: "MFMA + publish"} if a.bwd else
-             {1: "poll done", 2: "barrier", 3: "MFMA issued", 4: "cell + publish", 5: "publish ack",
+             {1: "poll done", 2: "barrier", 3: "MFMA issued", 4: "cell + publish",
+              5: "publish ack" if a.mode & (1 << 23) else "cell done",
               6: "out ring", 7: "drop bits"})
     order = sorted((b for b in names if (w[:, b] != 0).all()),
                    key=lambda b: (w[:, b] - w[:, 0]).median().item())
