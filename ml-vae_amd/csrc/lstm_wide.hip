@@ -76,25 +76,43 @@ __device__ __forceinline__ int swz(int utt, int slot) { return slot ^ (utt & 15)
 // tiles of each SIMD and the io waves only move data: their DMA and stores right behind the
 // barrier, inside the pollers' MFMA / cell phase.  Same box, in the step: forward per launch
 // c2 0.954 -> 0.863, c5 (B = 64) 0.979 -> 0.872, c4 3.95 -> 3.49 ms (profiles/ab/r04_as.txt);
-// the default at TPW 1, debug bit 8 restores equal shares.  At TPW 2 the pollers' 3 tiles
-// spilled 46 VGPRs.
+// the only form at TPW 1 since round 6.  At TPW 2 the pollers' 3 tiles spilled 46 VGPRs.
 // ZP: the layer-0 input projection fused (a.Zb): io wave 4 DMAs the step's 16 z rows (64 B each)
 // into the gx ring's space and each tile's gate inputs are one v_mfma_f32_16x16x32_bf16 of the
 // resident W_ih fragment (K = 32 = the latent width) onto the tile's b_ih + b_hh -- instead of
 // reading 8 KB of fp16 projection per utterance and step that a separate kernel wrote.
-template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool ZP = false>
-__global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
+// NT: N-tiles (16 utterances each) per workgroup.  NT = 2 (the asymmetric TPW-1 split only): a
+// workgroup owns 32 utterances x 32 units, the pollers 2 M-tiles x 2 N-tiles each (every W_hh
+// A-fragment feeds two MFMAs), and the io waves own no tile at every batch size -- at B = 256
+// that replaces TPW 2 (16 utterances x 64 units, every wave owning tiles), whose io waves reached
+// the step barrier ~1,400 ticks after the pollers, waiting for the saved-activation stores they
+// had issued behind their own publish (profiles/r06_lstm_stamps.txt).  Tile-less io waves issue
+// those stores right behind the barrier instead, a whole step ahead of the wait.  Groups have
+// 16 members (H / 32), two groups per XCD.
+// W12: 12 waves (768 threads, three per SIMD).  Waves 0-7 each own ONE M-tile (4 units) across
+// the NT N-tiles -- its W_hh A-fragments all in registers (64 VGPRs, under the 168 a wave gets at
+// three per SIMD) -- and all eight poll; waves 8-11 only move data.  Every SIMD keeps two MFMA
+// waves (one's cell overlaps the other's MFMAs) beside a tile-less io wave.
+template <int TPW, int NKC, int OCC, bool DBG = false, bool AS = false, bool ZP = false, int NT = 1,
+          bool W12 = false>
+__global__ __launch_bounds__(W12 ? 768 : 512, W12 ? 1 : OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
+  static_assert(NT == 1 || (NT == 2 && AS && TPW == 1), "two N-tiles: the asymmetric TPW-1 split");
+  static_assert(!W12 || (AS && TPW == 1), "12 waves: the asymmetric TPW-1 split");
+  constexpr int NWV = W12 ? 12 : 8;           // waves per workgroup
+  constexpr int NPOLL = W12 ? 8 : 4;          // polling waves (0 .. NPOLL-1)
+  constexpr int IO0 = NWV - 4;                // first io wave
+  constexpr int BGW = BG * NT;                // utterances per workgroup
   constexpr int HJ = WW * TPW * 4;
   constexpr int H = NKC * 32;
-  constexpr int PL = NKC / 4;                 // poll loads (k-chunks) per lane, waves 0-3
+  constexpr int PL = NKC / NPOLL;             // poll loads (k-chunks) per lane and N-tile
   constexpr int ROWB = H * 2;                 // bytes of one h-image row (bf16)
-  constexpr int HIMG = 16 * ROWB;
+  constexpr int HIMG = BGW * ROWB;
   constexpr int GXU = 4 * HJ + 8;             // gx ring halfs per utterance: [gate][unit] + 16 B
   // out ring bytes per utterance: gates fp16 [i f g o][HJ] | c fp32 [HJ] | h fp32 [HJ] | 16 B
   constexpr int OUB = 4 * HJ * 2 + 2 * HJ * 4 + 16;
-  constexpr int NC8 = 16 * HJ / 8;            // 8-unit chunks of h per step
+  constexpr int NC8 = BGW * HJ / 8;           // 8-unit chunks of h per step
   // k-chunks whose A-fragments live in LDS (VGPR budget; at TPW 1 one tile's 16 fit in registers)
-  constexpr int KLF = (TPW == 1 && !AS) ? 0 : FWD_KLF;
+  constexpr int KLF = ((TPW == 1 && !AS) || W12) ? 0 : FWD_KLF;
   constexpr int KR = NKC - KLF;               // ... and in registers
   constexpr int HB = 4;                       // B-fragments (h) read ahead per batch
   constexpr int NQ = 16 * 4 * HJ / 4;         // 16-byte quads of gx / gates per step
@@ -103,10 +121,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LSTAMP_DECL;
   RTS_DECL;
-  char* himg = smem;                                        // [2][16][ROWB], swizzled slots
-  unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2][16][GXU] fp16
-  char* outr = reinterpret_cast<char*>(gxr + 2 * 16 * GXU);                 // [2][16][OUB]
-  bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * 16 * OUB);  // [wave][TPW][KLF][lane]
+  char* himg = smem;                                        // [2][BGW][ROWB], swizzled slots
+  unsigned short* gxr = reinterpret_cast<unsigned short*>(smem + 2 * HIMG);  // [2][BGW][GXU] fp16
+  char* outr = reinterpret_cast<char*>(gxr + 2 * BGW * GXU);                // [2][BGW][OUB]
+  bf16x8* wlds = reinterpret_cast<bf16x8*>(outr + 2 * BGW * OUB);  // [wave][TPW][KLF][lane]
   unsigned* dbl = reinterpret_cast<unsigned*>(wlds + 8 * TPW * KLF * 64);  // [2][NC8] keep bits
   __shared__ int abort_flag;
 
@@ -124,15 +142,16 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: role branches stay scalar
   const float* W = dir ? a.W1 : a.W0;
   const int bi = lane & 15, q = lane >> 4;
-  const int bglob = grp * BG + bi;
-  const bool valid = bglob < a.B;
+  bool valid[NT];  // utterance 16 n + bi of the workgroup exists
+#pragma unroll
+  for (int n = 0; n < NT; ++n) valid[n] = grp * BGW + 16 * n + bi < a.B;
 
   // tiles per poller / io wave (AS) and a wave's first tile
   // (TPW 2 as 3 + 1 spilled 46 VGPRs: the split applies to TPW 1 only)
   static_assert(!AS || TPW == 1, "asymmetric split: TPW 1 only");
-  constexpr int TPP = AS ? 2 : TPW;
+  constexpr int TPP = W12 ? 1 : AS ? 2 : TPW;
   constexpr int TPI = AS ? 0 : TPW;
-  static_assert(4 * TPP + 4 * TPI == WW * TPW, "every tile owned once");
+  static_assert(NPOLL * TPP + 4 * TPI == WW * TPW, "every tile owned once");
   // resident A-fragments: tile m, row r = bi -> unit 4m + (r >> 2), gate r & 3; k-chunks
   // [0, KR) in registers, [KR, NKC) in LDS (lane-linear, conflict-free 16-B reads)
   auto load_w = [&](auto* wreg, int m0, int mt) {
@@ -158,7 +177,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
                         !(DMODE(a) & 32768);  // bit 15: force write-through hand-offs
   if (tid == 0) abort_flag = 0;
 
-  const size_t xslot = (size_t)BG * H;  // elements per exchange slot
+  const size_t xslot = (size_t)BGW * H;  // elements per exchange slot: [H / 8][BGW][8]
   short* xb = reinterpret_cast<short*>(a.xbuf) + (size_t)(dir * a.NB + grp) * NSLOT * xslot;
   auto xr = make_rsrc(xb, (unsigned)(NSLOT * xslot * sizeof(short)));
 
@@ -167,11 +186,12 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   // per wave-instruction, no registers); the saved activations go LDS -> registers -> 16-byte
   // stores: gates (fp16), c (fp32), h (bf16 GEMM operand), the next layer's dropout(h) (bf16,
   // Philox mask: replaces a separate dropout pass) and -- only when asked -- h in fp32.
-  const int iot = tid - 256;
-  const bool io = wave >= 4;
+  const int iot = tid - 64 * IO0;
+  const bool io = wave >= IO0;
+  const int iow = wave - IO0;  // io wave index (0 .. 3)
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   unsigned short* G16 = reinterpret_cast<unsigned short*>(a.G);
-  const auto rgx = make_rsrc(G16 + (size_t)grp * BG * T * 8 * H, 0xffffffffu);
+  const auto rgx = make_rsrc(G16 + (size_t)grp * BGW * T * 8 * H, 0xffffffffu);
   // debug bit 10 (timing probe only, outputs wrong): the saved activations and the gx loads
   // addressed time-major (row t * B + b) -- one step's rows of all utterances contiguous in HBM
   const bool tmaj = (DMODE(a) & 1024) != 0;
@@ -185,26 +205,27 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     if (s_ >= T || (s_ > 0 && (DMODE(a) & 8192))) return;  // bit 13: timing without the loads
     const int t_ = dir ? T - 1 - s_ : s_;
     if constexpr (ZP) {
-      if (wave == 4) {
-        const int u = lane >> 2, b = grp * BG + u;
+      if (iow < NT) {  // io wave n: the z rows of N-tile n
+        const int u = iow * 16 + (lane >> 2), b = grp * BGW + u;
         const unsigned off = b < a.B ? (unsigned)((((size_t)b * T + t_) * a.ldz + 8 * (lane & 3)) * 2) : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_ptr_t)(zr + (s_ & 1) * 16 * 32), 16, off, 0, 0, NT_AUX);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rz, (lds_ptr_t)(zr + ((s_ & 1) * BGW + iow * 16) * 32), 16,
+                                                 off, 0, 0, NT_AUX);
       }
       return;
     }
-    constexpr int UPW = 16 / 4;  // utterances per io wave
+    constexpr int UPW = BGW / 4;  // utterances per io wave
     // one descriptor over the group's 16 utterances (per-utterance descriptors spilled SGPRs
     // into the io waves' MFMA phase); the host keeps 16 T 8H halfs under 4 GB
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
-      const int u = (wave - 4) * UPW + i, b = grp * BG + u;
+      const int u = iow * UPW + i, b = grp * BGW + u;
       if (b >= a.B) continue;
       // lane l < HJ/2 -> gate l / (HJ/8), units 8 (l % (HJ/8)) .. + 7
       const int g = lane / (HJ / 8), uu = (lane % (HJ / 8)) * 8;
       const unsigned off = tmaj ? (unsigned)((((size_t)t_ * a.B + b) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2)
                                 : (unsigned)((((size_t)u * T + t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) * 2);
       const auto rs = tmaj ? rgx_abs : rgx;
-      unsigned short* dst = gxr + (s_ & 1) * 16 * GXU + u * GXU;
+      unsigned short* dst = gxr + (s_ & 1) * BGW * GXU + u * GXU;
       // nt: read-once stream, kept from displacing the hand-off lines in L2
       if (lane < HJ / 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, NT_AUX);
     }
@@ -214,7 +235,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   auto drop_bits = [&](int s_, int c8) -> unsigned {
     const int u = c8 / (HJ / 8), uu = (c8 % (HJ / 8)) * 8;
     const int t_ = dir ? T - 1 - s_ : s_;
-    const size_t o = ((size_t)(grp * BG + u) * T + t_) * 2 * H + dir * H + j0 + uu;
+    const size_t o = ((size_t)(grp * BGW + u) * T + t_) * 2 * H + dir * H + j0 + uu;
     const unsigned long long k = drop_key(a.dseed);
     const unsigned long long r0 = drop_quad(k, (a.doff + o) >> 2), r1 = drop_quad(k, (a.doff + o + 4) >> 2);
     unsigned bits = 0;
@@ -228,20 +249,20 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
   auto io_store = [&](int s_) {  // saved activations of step s_ from out ring slot s_ & 1
     if (s_ < 0 || s_ >= T || (DMODE(a) & 1)) return;
     const int t_ = dir ? T - 1 - s_ : s_;
-    const char* src = outr + (s_ & 1) * 16 * OUB;
-    // activated gates (fp16 in the ring already): 16 utt x 4 gates x HJ/8 chunks, LDS -> HBM
-    constexpr int NG8 = 16 * 4 * HJ / 8;
+    const char* src = outr + (s_ & 1) * BGW * OUB;
+    // activated gates (fp16 in the ring already): BGW utt x 4 gates x HJ/8 chunks, LDS -> HBM
+    constexpr int NG8 = BGW * 4 * HJ / 8;
     for (int ci = iot; ci < NG8; ci += 256) {
       const int row = ci / (HJ / 8), uu = (ci % (HJ / 8)) * 8;
-      const int u = row >> 2, g = row & 3, b = grp * BG + u;
+      const int u = row >> 2, g = row & 3, b = grp * BGW + u;
       if (b >= a.B) continue;
       *reinterpret_cast<u32x4*>(G16 + rowof(b, t_) * 8 * H + dir * 4 * H + g * H + j0 + uu) =
           *reinterpret_cast<const u32x4*>(src + u * OUB + (g * HJ + uu) * 2);
     }
     // c (fp32) and, when asked, h (fp32): 16 x HJ/4 quads
-    constexpr int NQ2 = 16 * HJ / 4;
+    constexpr int NQ2 = BGW * HJ / 4;
     for (int qi = iot; qi < NQ2; qi += 256) {
-      const int u = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4, b = grp * BG + u;
+      const int u = qi / (HJ / 4), uu = (qi % (HJ / 4)) * 4, b = grp * BGW + u;
       if (b >= a.B) continue;
       const size_t o = rowof(b, t_) * 2 * H + dir * H + j0 + uu;
       const float* cf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ);
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     const bool drop8 = iot >= NC8;
     const int ci8 = drop8 ? iot - NC8 : iot;
     if (ci8 < NC8 && (drop8 ? (a.Ydb != nullptr || a.Y8 != nullptr) : a.Yb != nullptr)) {
-      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8, b = grp * BG + u;
+      const int u = ci8 / (HJ / 8), uu = (ci8 % (HJ / 8)) * 8, b = grp * BGW + u;
       if (b < a.B) {
         const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
@@ -290,7 +311,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
     constexpr bool IO = decltype(io_tag)::value;
     constexpr int MT = IO ? TPI : TPP;         // this wave's tiles
     constexpr int MTA = MT > 0 ? MT : 1;       // (array extent)
-    const int m0 = IO ? 4 * TPP + (wave - 4) * TPI : wave * TPP;
+    const int m0 = IO ? NPOLL * TPP + iow * TPI : wave * TPP;
     bf16x8 wreg[MTA][KR];
     load_w(wreg, m0, MT);
     // ZP: the tiles' W_ih fragments (row bi: gate bi & 3, unit 4 m + (bi >> 2); k = 8 q .. 8 q + 7)
@@ -321,39 +342,52 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    float c[MTA];
+    float c[MTA][NT];
 #pragma unroll
-    for (int t = 0; t < MTA; ++t) c[t] = 0.f;
+    for (int t = 0; t < MTA; ++t)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) c[t][n] = 0.f;
     stagger_start(gid, DMODE(a));
     for (int s = 0; s < T; ++s) {
       LSTAMP(0);
       IOSTAMP(0);
-      f32x4 acc[MTA];
+      f32x4 acc[MTA][NT];
 #pragma unroll
-      for (int t = 0; t < MTA; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < MTA; ++t)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
       char* hb = himg + (s & 1) * HIMG;
       // this step's input projection (fp16, LDS ring): read before the MFMAs, so the LDS
       // latency is not exposed between the last MFMA and the cell update
-      float gxv[MTA][4];
+      // gate inputs: ZP's fp32 z-projection results, else the fp16 ring words (converted in the
+      // cell, behind the padded end of the MFMA chain -- see there)
+      float gxv[MTA][NT][4];
+      unsigned short gxh[MTA][NT][4];
       auto read_gx = [&]() {
         if constexpr (ZP) {
           if constexpr (MT > 0) {
-            const bf16x8 zf = *reinterpret_cast<const bf16x8*>(zr + (s & 1) * 16 * 32 + bi * 32 + 8 * q);
 #pragma unroll
-            for (int t = 0; t < MT; ++t) {
-              const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wz[t], zf, bz4[t], 0, 0, 0);
+            for (int n = 0; n < NT; ++n) {
+              const bf16x8 zf = *reinterpret_cast<const bf16x8*>(zr + ((s & 1) * BGW + 16 * n + bi) * 32 + 8 * q);
 #pragma unroll
-              for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = r[g4];
+              for (int t = 0; t < MT; ++t) {
+                const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wz[t], zf, bz4[t], 0, 0, 0);
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) gxv[t][n][g4] = r[g4];
+              }
             }
           }
           return;
         }
-        const unsigned short* gx = gxr + (s & 1) * 16 * GXU + bi * GXU;
 #pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          const int u = 4 * (m0 + t) + q;
+        for (int n = 0; n < NT; ++n) {
+          const unsigned short* gx = gxr + ((s & 1) * BGW + 16 * n + bi) * GXU;
 #pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = h2f(gx[g4 * HJ + u]);
+          for (int t = 0; t < MT; ++t) {
+            const int u = 4 * (m0 + t) + q;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) gxh[t][n][g4] = gx[g4 * HJ + u];
+          }
         }
       };
       if (s == 0) read_gx();
@@ -366,10 +400,13 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           // poll = load: this wave's quarter of h_{t-1} (PL k-chunks), retried until every
           // granule carries step s-1's tag; then into the swizzled LDS image
           const unsigned tag = step_tag_lg(s - 1, nlg);
-          // load i: units u = 32 (wave PL + i) + 8 q = chunk u / 8 of utterance bi
-          const unsigned xbase = (unsigned)(((s - 1) & nmask) * xslot) + (((wave * PL * 32 + 8 * q) >> 3) * 16 + bi) * 8;
-          auto poll_off = [&](int i) -> unsigned { return xbase + (unsigned)i * (32 / 8) * 16 * 8; };
-          u32x4 hv[PL];
+          // load (i, n): units u = 32 (wave PL + i) + 8 q = chunk u / 8 of utterance 16 n + bi
+          const unsigned xbase = (unsigned)(((s - 1) & nmask) * xslot) + (((wave * PL * 32 + 8 * q) >> 3) * BGW + bi) * 8;
+          auto poll_off = [&](int i) -> unsigned {
+            return xbase + (unsigned)((i / NT) * (32 / 8) * BGW + (i % NT) * 16) * 8;
+          };
+          constexpr int PLN = PL * NT;  // loads per lane: PL chunks x NT utterances
+          u32x4 hv[PLN];
           unsigned spins = 0;
           // When the grid fills the chip, retries re-load only the chunks whose tags were stale,
           // with a shorter back-off (s_sleep 2 instead of 6): less L2 poll traffic per retry and
@@ -378,10 +415,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           // bit 28: full re-loads with s_sleep 6 at every size; bit 30: s_sleep 1
           const bool partial = (int)gridDim.x >= 256 && !(DMODE(a) & (1 << 28));
 #pragma unroll
-          for (int i = 0; i < PL; ++i) hv[i] = u32x4{tag ^ 1u, 0u, tag ^ 1u, 0u};  // stale: first sweep loads all
+          for (int i = 0; i < PLN; ++i) hv[i] = u32x4{tag ^ 1u, 0u, tag ^ 1u, 0u};  // stale: first sweep loads all
           while (true) {
 #pragma unroll
-            for (int i = 0; i < PL; ++i)
+            for (int i = 0; i < PLN; ++i)
               if (!partial || !tags_ok(hv[i], tag, true, true)) hv[i] = ld_sc1_b128(xr, poll_off(i) * sizeof(short));
             // step s-1's dropout keep bits, drawn while the first poll's loads are in flight
             // (drawn before them, at the end of step s-1, they delayed the poll's issue; with the
@@ -389,7 +426,7 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
             if (late_bits && spins == 0 && tid < NC8) dbl[((s - 1) & 1) * NC8 + tid] = drop_bits(s - 1, tid);
             bool ok = true;
 #pragma unroll
-            for (int i = 0; i < PL; ++i) ok &= tags_ok(hv[i], tag, true, true);
+            for (int i = 0; i < PLN; ++i) ok &= tags_ok(hv[i], tag, true, true);
             if (__all(ok)) break;
             if (++spins > SPIN_LIMIT) {
               if (lane == 0) { atomicExch(a.err, 1); abort_flag = 1; }
@@ -404,10 +441,10 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
           LSTAMP(1);
           RTS(8 + wave);
 #pragma unroll
-          for (int i = 0; i < PL; ++i)
-            *reinterpret_cast<u32x4*>(hb + bi * ROWB + swz(bi, (wave * PL + i) * 4 + q) * 16) = hv[i];
+          for (int i = 0; i < PLN; ++i)
+            *reinterpret_cast<u32x4*>(hb + (16 * (i % NT) + bi) * ROWB + swz(bi, (wave * PL + i / NT) * 4 + q) * 16) = hv[i];
         }
-        LWSTAMP();
+        if (wave < 8) LWSTAMP();  // (stamp slots 8 .. 15)
         __syncthreads();  // h image of step s complete; gx ring slot s & 1 landed
         LSTAMP(2);
         if (abort_flag) break;
@@ -435,29 +472,37 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
         // inside the chain they had one or two MFMAs of cover each
         constexpr int KLA = KLF > 0 ? KLF : 1;
         bf16x8 wl[MTA][KLA];
-        bf16x8 zf;
+        bf16x8 zf[NT];
 #pragma unroll
         for (int k0 = 0; k0 < NKC; k0 += HB) {
-          bf16x8 hfrag[HB];
+          bf16x8 hfrag[HB][NT];
 #pragma unroll
           for (int i = 0; i < HB; ++i)
-            hfrag[i] = *reinterpret_cast<const bf16x8*>(hb + bi * ROWB + swz(bi, ((k0 + i + KR) % NKC) * 4 + q) * 16);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+              hfrag[i][n] = *reinterpret_cast<const bf16x8*>(hb + (16 * n + bi) * ROWB + swz(bi, ((k0 + i + KR) % NKC) * 4 + q) * 16);
           if (k0 == 0) {
 #pragma unroll
             for (int t = 0; t < MT; ++t)
 #pragma unroll
               for (int j = 0; j < KLF; ++j) wl[t][j] = wlds[((m0 + t) * KLF + j) * 64 + lane];
-            if constexpr (ZP) zf = *reinterpret_cast<const bf16x8*>(zr + (s & 1) * 16 * 32 + bi * 32 + 8 * q);
+            if constexpr (ZP) {
+#pragma unroll
+              for (int n = 0; n < NT; ++n)
+                zf[n] = *reinterpret_cast<const bf16x8*>(zr + ((s & 1) * BGW + 16 * n + bi) * 32 + 8 * q);
+            }
           }
           __builtin_amdgcn_sched_barrier(0);  // the batch's reads issue before its MFMAs
           if constexpr (ZP) {
             if (k0 == 0) {
 #pragma unroll
-              for (int t = 0; t < MT; ++t) {
-                const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wz[t], zf, bz4[t], 0, 0, 0);
+              for (int t = 0; t < MT; ++t)
 #pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) gxv[t][g4] = r[g4];
-              }
+                for (int n = 0; n < NT; ++n) {
+                  const f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wz[t], zf[n], bz4[t], 0, 0, 0);
+#pragma unroll
+                  for (int g4 = 0; g4 < 4; ++g4) gxv[t][n][g4] = r[g4];
+                }
             }
           }
 #pragma unroll
@@ -466,27 +511,43 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
 #pragma unroll
             for (int t = 0; t < MT; ++t) {
               const bf16x8 wf = kc < KR ? wreg[t][kc < KR ? kc : 0] : wl[t][kc >= KR ? kc - KR : 0];
-              acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag[i], acc[t], 0, 0, 0);
+#pragma unroll
+              for (int n = 0; n < NT; ++n)
+                acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hfrag[i][n], acc[t][n], 0, 0, 0);
             }
           }
         }
+        // The cell reads the accumulators right behind the chain.  With one M-tile per wave (the
+        // 12-wave form at NT = 1, and the retired equal-shares TPW-1 form) hipcc (ROCm 7.2) put the
+        // gx conversions INSIDE the chain -- writing the B-fragment registers of the MFMA just
+        // issued -- and read the last MFMA's accumulator 3 wait states after it: a share of the
+        // lanes lost their gx term (tools/dbg_fwd_err.py: the wrong pre-activations equal h W^T
+        // exactly).  The chain now ends here, padded, and the fp16 gx words are converted only in
+        // the cell, behind this barrier.
+        __builtin_amdgcn_sched_barrier(0);
+        if (MT > 0) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         if (first) __builtin_amdgcn_s_setprio(0);
         LSTAMP(3);
         IOSTAMP(4);
       }
       // cell update: lane (utt bi, q) owns unit 4m + q of each of its tiles
-      char* ob = outr + (s & 1) * 16 * OUB + bi * OUB;
-      float hvals[MTA], gates[MTA][4];
+      float hvals[MTA][NT], gates[MTA][NT][4];
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const float ig = sigmoid_fast(acc[t][0] + gxv[t][0]);
-        const float fg = sigmoid_fast(acc[t][1] + gxv[t][1]);
-        const float gg = tanh_fast(acc[t][2] + gxv[t][2]);
-        const float og = sigmoid_fast(acc[t][3] + gxv[t][3]);
-        c[t] = valid ? fg * c[t] + ig * gg : 0.f;
-        hvals[t] = valid ? og * tanh_fast(c[t]) : 0.f;
-        gates[t][0] = ig; gates[t][1] = fg; gates[t][2] = gg; gates[t][3] = og;
-      }
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          float gi[4];
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) gi[g4] = ZP ? gxv[t][n][g4] : h2f(gxh[t][n][g4]);
+          const float ig = sigmoid_fast(acc[t][n][0] + gi[0]);
+          const float fg = sigmoid_fast(acc[t][n][1] + gi[1]);
+          const float gg = tanh_fast(acc[t][n][2] + gi[2]);
+          const float og = sigmoid_fast(acc[t][n][3] + gi[3]);
+          c[t][n] = valid[n] ? fg * c[t][n] + ig * gg : 0.f;
+          hvals[t][n] = valid[n] ? og * tanh_fast(c[t][n]) : 0.f;
+          gates[t][n][0] = ig; gates[t][n][1] = fg; gates[t][n][2] = gg; gates[t][n][3] = og;
+        }
       if (DBG && !(DMODE(a) & (1 << 23))) {  // diagnostics: cell math done (slot 5)
         __builtin_amdgcn_sched_barrier(0);
         LSTAMP(5);
@@ -495,44 +556,53 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (s + 1 < T) {
         // publish h_t: granule = 4 consecutive units (lanes q = 0..3) of one utterance
         const unsigned tag = step_tag_lg(s, nlg);
-        unsigned long long gr[MTA];
+        unsigned long long gr[MTA][NT];
 #pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          // units 4m+1..3 of lane (bi, 0) sit in lanes bi + 16, 32, 48: VALU permlane swaps
-          // (lane row 0 of each result) instead of three LDS-routed ds_bpermute round trips
-          const unsigned hu = __float_as_uint(hvals[t]);
-          const unsigned x1 = __builtin_amdgcn_permlane16_swap(hu, hu, false, false)[1];  // row0 <- row1
-          const unsigned x2 = __builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1];  // row0 <- row2
-          const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];  // row0 <- row3
-          const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
-          gr[t] = pack_bf16(hvals[t], h1, h2, h3, tag);
-        }
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            // units 4m+1..3 of lane (bi, 0) sit in lanes bi + 16, 32, 48: VALU permlane swaps
+            // (lane row 0 of each result) instead of three LDS-routed ds_bpermute round trips
+            const unsigned hu = __float_as_uint(hvals[t][n]);
+            const unsigned x1 = __builtin_amdgcn_permlane16_swap(hu, hu, false, false)[1];  // row0 <- row1
+            const unsigned x2 = __builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1];  // row0 <- row2
+            const unsigned x3 = __builtin_amdgcn_permlane32_swap(x1, x1, false, false)[1];  // row0 <- row3
+            const float h1 = __uint_as_float(x1), h2 = __uint_as_float(x2), h3 = __uint_as_float(x3);
+            gr[t][n] = pack_bf16(hvals[t][n], h1, h2, h3, tag);
+          }
         if (AS && q == 0) {
           if constexpr (MT == 2) {
             // the poller's two tiles are units 8 w .. 8 w + 7: adjacent granules, one 16-byte store
-            // (consecutive publish stores reach the consumers ~120 ns apart: see the BPTT's publish)
+            // per utterance (consecutive publish stores reach the consumers ~120 ns apart: see the
+            // BPTT's publish)
             const int u0 = j0 + 4 * m0;
-            const u32x4 v = {(unsigned)gr[0], (unsigned)(gr[0] >> 32), (unsigned)gr[1], (unsigned)(gr[1] >> 32)};
-            const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7);
-            if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, cell * sizeof(short), 0, 0);
-            else st_sc1_b128(xr, cell * sizeof(short), v);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+              const u32x4 v = {(unsigned)gr[0][n], (unsigned)(gr[0][n] >> 32), (unsigned)gr[1][n], (unsigned)(gr[1][n] >> 32)};
+              const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * BGW + 16 * n + bi) * 8 + (u0 & 7);
+              if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, cell * sizeof(short), 0, 0);
+              else st_sc1_b128(xr, cell * sizeof(short), v);
+            }
           } else {  // one 8-byte granule per tile
 #pragma unroll
-            for (int t = 0; t < MT; ++t) {
-              const int u0 = j0 + 4 * (m0 + t);
-              publish(xr, ((unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7)) * sizeof(short),
-                      gr[t], same_xcd);
-            }
+            for (int n = 0; n < NT; ++n)
+#pragma unroll
+              for (int t = 0; t < MT; ++t) {
+                const int u0 = j0 + 4 * (m0 + t);
+                publish(xr, ((unsigned)((s & nmask) * xslot) + ((u0 >> 3) * BGW + 16 * n + bi) * 8 + (u0 & 7)) * sizeof(short),
+                        gr[t][n], same_xcd);
+              }
           }
         } else if (q == 0) {
+          // (equal shares: NT = 1, static_assert at the top)
           const int u0 = j0 + 4 * TPW * wave;  // the wave's first unit
           const unsigned cell = (unsigned)((s & nmask) * xslot) + ((u0 >> 3) * 16 + bi) * 8 + (u0 & 7);
           if constexpr (TPW == 2) {
-            const u32x4 v = {(unsigned)gr[0], (unsigned)(gr[0] >> 32), (unsigned)gr[1], (unsigned)(gr[1] >> 32)};
+            const u32x4 v = {(unsigned)gr[0][0], (unsigned)(gr[0][0] >> 32), (unsigned)gr[1][0], (unsigned)(gr[1][0] >> 32)};
             if (same_xcd) __builtin_amdgcn_raw_buffer_store_b128(v, xr, cell * sizeof(short), 0, 0);
             else st_sc1_b128(xr, cell * sizeof(short), v);
           } else {
-            publish(xr, cell * sizeof(short), gr[0], same_xcd);
+            publish(xr, cell * sizeof(short), gr[0][0], same_xcd);
           }
         }
       }
@@ -551,14 +621,18 @@ __global__ __launch_bounds__(512, OCC) void lstm_fwd_wide_kernel(LstmArgs a) {
       if (IO && !PURE_IO && late_dma_s) io_load(s + 1);  // (slot s+1 & 1 was last read before barrier s)
       if (IO && !PURE_IO && s > 0) io_store(s - 1);
       IOSTAMP(6);
-      unsigned short* og = reinterpret_cast<unsigned short*>(ob);
-      float* of = reinterpret_cast<float*>(ob + 8 * HJ);
 #pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const int u = 4 * (m0 + t) + q;
-        og[u] = f2h(gates[t][0]); og[HJ + u] = f2h(gates[t][1]);
-        og[2 * HJ + u] = f2h(gates[t][2]); og[3 * HJ + u] = f2h(gates[t][3]);
-        of[u] = c[t]; of[HJ + u] = hvals[t];
+      for (int n = 0; n < NT; ++n) {
+        char* ob = outr + ((s & 1) * BGW + 16 * n + bi) * OUB;
+        unsigned short* og = reinterpret_cast<unsigned short*>(ob);
+        float* of = reinterpret_cast<float*>(ob + 8 * HJ);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int u = 4 * (m0 + t) + q;
+          og[u] = f2h(gates[t][n][0]); og[HJ + u] = f2h(gates[t][n][1]);
+          og[2 * HJ + u] = f2h(gates[t][n][2]); og[3 * HJ + u] = f2h(gates[t][n][3]);
+          of[u] = c[t][n]; of[HJ + u] = hvals[t][n];
+        }
       }
       LSTAMP(6);
       // the pollers draw step s's dropout keep bits before polling for step s+1 (drawn by io
@@ -1087,6 +1161,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------------------
 struct WidePlan {
   int tpw, nkc, NB, NJ, HJ;
+  int nt;    // forward: N-tiles (16 utterances each) per workgroup
+  bool w12;  // forward: the 12-wave form (lstm_fwd_wide_kernel W12)
   size_t lds, xbytes, xtab_off;
   bool ok;
 };
@@ -1099,28 +1175,48 @@ int wide_cus() {
   return cus;
 }
 
-size_t wide_lds(int H, int hj, bool fwd) {
+size_t wide_lds(int H, int hj, bool fwd, int nt = 1) {
+  const size_t bgw = (size_t)BG * nt;
   if (fwd)
-    return (size_t)2 * 16 * H * 2 + (size_t)2 * 16 * (4 * hj + 8) * 2 +  // h image, gx ring
-           (size_t)2 * 16 * (4 * hj * 2 + 2 * hj * 4 + 16) +              // out ring
-           (size_t)8 * (hj / 32) * FWD_KLF * 64 * 16 +  // + the LDS-resident A-fragments
-           (size_t)2 * (16 * hj / 8) * 4;         // + dropout keep bits
+    return 2 * bgw * H * 2 + 2 * bgw * (4 * hj + 8) * 2 +  // h image, gx ring
+           2 * bgw * (4 * hj * 2 + 2 * hj * 4 + 16) +      // out ring
+           (size_t)8 * (hj / 32) * FWD_KLF * 64 * 16 +     // + the LDS-resident A-fragments
+           2 * (bgw * hj / 8) * 4;                         // + dropout keep bits
   return (size_t)2 * 16 * 4 * hj * 2 +
          (size_t)8 * (H / 128) * (hj == 32 ? 0 : hj / 32) * 64 * 16 +  // + LDS B-fragments (KLB)
          (size_t)2 * 16 * ((4 * hj * 2 + 16) + 2 * (hj * 4 + 32));  // + staged cell inputs
 }
 
-WidePlan wide_plan(int B, int H, bool fwd) {
+// mode bits (mlvae_lstm_set_debug_mode, A/B): 9 -- past B = 64 the forward takes the 32-utterance
+// form (NT = 2) instead of TPW 2 (16 utterances x 64 units per workgroup); 11 -- the TPW-1 forward
+// in 8 waves (4 pollers with two M-tiles each + 4 io waves) instead of 12.
+// Same box, in the step (profiles/ab/r06_fwd_w12.txt): c2 forward 0.84 -> 0.74 ms per launch with
+// 12 waves (step 4.10 -> 3.90 ms); at c3 NT = 2 runs 1.25 ms in 12 waves, 1.48 in 8, against TPW 2's
+// 1.17 -- its h image is twice as large, and every MFMA wave reads all of it (256 vs 192 KB of LDS
+// reads per CU per step)
+WidePlan wide_plan(int B, int H, bool fwd, int mode = 0) {
   WidePlan p{};
   p.ok = false;
+  p.nt = 1;
+  p.w12 = false;
   if (H != 512) return p;  // the decoder's H (c2-c5); other H run the batch-group kernels
   p.nkc = H / 32;
   p.NB = (B + BG - 1) / BG;
   const int cus = wide_cus();
+  // forward past one HJ = 32 launch of 16-utterance groups (B > 64): 32 utterances x 32 units per
+  // workgroup, tile-less io waves (lstm_fwd_wide_kernel NT = 2)
+  if (fwd && (mode & 512) && 2 * p.NB * (H / 32) > cus) {
+    const int nb2 = (B + 2 * BG - 1) / (2 * BG);
+    if (2 * nb2 * (H / 32) <= cus) {
+      p.nt = 2; p.tpw = 1; p.HJ = 32; p.NJ = H / 32; p.NB = nb2; p.ok = true;
+    }
+  }
+  if (!p.ok)
   // HJ = 32 units per workgroup where the grid fits the chip (it beat HJ = 64 at every shard,
   // round 2: 7.94 vs 8.02, 5.58 vs 6.34, 4.72 vs 5.68 ms/step); HJ = 64 at B = 256
   for (int tpw = 1; tpw <= 2; ++tpw) {
     if (fwd && tpw * p.nkc * 4 > 128) break;   // resident A-fragments <= 128 VGPRs
+    p.NB = (B + BG - 1) / BG;
     const int hj = 32 * tpw, nj = H / hj;
     if (!fwd && (nj < 8 || nj % 8)) continue;   // reduce-scatter: NJ multiple of 8
     // one workgroup per CU.  (Two co-resident HJ = 32 workgroups per CU at B = 256, whose step
@@ -1133,8 +1229,9 @@ WidePlan wide_plan(int B, int H, bool fwd) {
     }
   }
   if (!p.ok) return p;
-  p.lds = wide_lds(H, p.HJ, fwd);
-  if (fwd) p.xbytes = (size_t)2 * p.NB * NSLOT * BG * H * 2;
+  if (fwd && p.tpw == 1) p.w12 = !(mode & 2048);
+  p.lds = wide_lds(H, p.HJ, fwd, p.nt);
+  if (fwd) p.xbytes = (size_t)2 * p.NB * NSLOT * BG * p.nt * H * 2;
   else p.xbytes = (size_t)2 * p.NB * NSLOT * p.NJ * p.NJ * p.HJ * 16 * 2;
   if (p.lds < (size_t)MIN_LDS) p.lds = MIN_LDS;  // one recurrence workgroup per CU (residency)
   p.xtab_off = p.xbytes;                          // + [groups][NJ] XCC ids (placement check)
@@ -1147,12 +1244,24 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
   // DBG instances (phase stamps) only while a stamp buffer is set; the BPTT's only for the bf16
   // train step's form (bf16 dY, no fp8 copy)
   const bool dbg = a.dbg != nullptr;
-  const bool as = TPW == 1 && !(a.dbg_mode & (1 << 8));   // the asymmetric split; bit 8: equal shares
+  // the forward at TPW 1 always takes the asymmetric split (the equal-shares form, debug bit 8
+  // through round 5, was retired in round 6); TPW 2 keeps equal shares
+  constexpr bool AS1 = TPW == 1;
   const bool zp = a.Zb != nullptr;          // fused layer-0 projection (checked: no DBG with it)
-  auto k = fwd ? (dbg ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC, true>)
-                      : (zp ? (as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1, true>
-                                  : lstm_fwd_wide_kernel<TPW, NKC, OCC, false, false, true>)
-                            : as ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, TPW == 1> : lstm_fwd_wide_kernel<TPW, NKC, OCC>))
+  auto k = (fwd && p.w12)
+               ? (p.nt == 2 ? (dbg ? lstm_fwd_wide_kernel<1, NKC, OCC, true, true, false, 2, true>
+                                   : zp ? lstm_fwd_wide_kernel<1, NKC, OCC, false, true, true, 2, true>
+                                        : lstm_fwd_wide_kernel<1, NKC, OCC, false, true, false, 2, true>)
+                            : (dbg ? lstm_fwd_wide_kernel<1, NKC, OCC, true, true, false, 1, true>
+                                   : zp ? lstm_fwd_wide_kernel<1, NKC, OCC, false, true, true, 1, true>
+                                        : lstm_fwd_wide_kernel<1, NKC, OCC, false, true, false, 1, true>))
+         : (fwd && p.nt == 2)
+               ? (dbg ? lstm_fwd_wide_kernel<1, NKC, OCC, true, true, false, 2>
+                      : zp ? lstm_fwd_wide_kernel<1, NKC, OCC, false, true, true, 2>
+                           : lstm_fwd_wide_kernel<1, NKC, OCC, false, true, false, 2>)
+         : fwd ? (dbg ? lstm_fwd_wide_kernel<TPW, NKC, OCC, true, AS1>
+                      : zp ? lstm_fwd_wide_kernel<TPW, NKC, OCC, false, AS1, true>
+                           : lstm_fwd_wide_kernel<TPW, NKC, OCC, false, AS1>)
                : (a.g8amax ? (a.dYb ? lstm_bwd_wide_kernel<TPW, NKC, OCC, true, true>
                                     : lstm_bwd_wide_kernel<TPW, NKC, OCC, true, false>)
                            : (a.dYb ? (dbg ? lstm_bwd_wide_kernel<TPW, NKC, OCC, false, true, true>
@@ -1163,15 +1272,16 @@ int launch_wide(bool fwd, const LstmArgs& a, const WidePlan& p, hipStream_t s) {
     mlvae_set_error("lstm_wide: cannot reserve %zu B LDS", p.lds);
     return 2;
   }
-  k<<<dim3(((2 * p.NB + 7) & ~7) * p.NJ), 512, p.lds, s>>>(a);
+  k<<<dim3(((2 * p.NB + 7) & ~7) * p.NJ), (fwd && p.w12) ? 768 : 512, p.lds, s>>>(a);
   MLVAE_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace
 
+// (the forward's 32-utterance groups: one descriptor spans 2 BG utterances' rows)
 bool lstm_wide_t_ok(int T, int H) {
-  return (size_t)BG * T * 8 * H * 2 <= 0xffffffffull && (size_t)BG * T * 2 * H * 4 <= 0xffffffffull;
+  return (size_t)2 * BG * T * 8 * H * 2 <= 0xffffffffull && (size_t)2 * BG * T * 2 * H * 4 <= 0xffffffffull;
 }
 
 int lstm_wide_workgroups(int B, int H, bool fwd) {
@@ -1181,8 +1291,9 @@ int lstm_wide_workgroups(int B, int H, bool fwd) {
 }
 
 size_t lstm_wide_xbytes(int B, int H, bool fwd) {
-  WidePlan p = wide_plan(B, H, fwd);
-  return p.ok ? p.xbytes : 0;
+  WidePlan p = wide_plan(B, H, fwd), q = wide_plan(B, H, fwd, 512);  // either form past B = 64
+  if (!p.ok) return 0;
+  return p.xbytes > q.xbytes ? p.xbytes : q.xbytes;
 }
 
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
@@ -1191,7 +1302,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                   unsigned long long dseed, unsigned long long doff, float dp,
                   unsigned long long* dbg, int dbg_mode, const WideFp8& f8, const unsigned short* dyb,
                   const WideZ& wz) {
-  WidePlan p = wide_plan(B, H, fwd);
+  WidePlan p = wide_plan(B, H, fwd, dbg_mode);
   if (!p.ok) return -1;
   // the kernels address a batch group's rows through one buffer descriptor (32-bit offsets)
   if (!lstm_wide_t_ok(T, H)) {

@@ -49,11 +49,14 @@ def _reference(B, T, seed, gx=None):
     return w, gx, y.detach(), torch.cat(cs, -1).detach(), torch.cat(gates, -1).detach(), dy, dG
 
 
-# mode: extra debug bits -- 256 (bit 8) runs the TPW 1 forward with equal tile shares instead of the
-# default asymmetric split (the io waves without tiles)
+# mode: extra debug bits -- 512 (bit 9) runs the B > 64 forward in the 32-utterance form (NT = 2,
+# 32 utterances x 32 units per workgroup) instead of TPW 2 (16 x 64); 2048 (bit 11) the TPW-1 forward
+# (and the NT = 2 form) in 8 waves instead of 12
 @pytest.mark.parametrize("B,T,force,mode", [(256, 16, False, 0), (128, 20, False, 0), (200, 12, False, 0),
-                                            (20, 15, True, 0), (48, 9, True, 0), (128, 20, False, 256),
-                                            (48, 9, True, 256)])
+                                            (20, 15, True, 0), (48, 9, True, 0), (256, 16, False, 512),
+                                            (200, 12, False, 512), (96, 7, False, 0), (256, 16, False, 512 | 2048),
+                                            (200, 12, False, 512 | 2048), (64, 11, False, 2048), (20, 15, True, 2048),
+                                            (128, 20, False, 2048)])
 def test_wide_recurrence_matches_fp64_loop(B, T, force, mode):
     need_gpu()
     w, gx, y, cs, gates, dy, dG = _reference(B, T, B + T)
@@ -109,9 +112,11 @@ def test_wide_recurrence_matches_fp64_loop(B, T, force, mode):
         lib().mlvae_lstm_set_debug_mode(0)
 
 
-# mode 4096: the wide kernels forced at a small batch; 256: TPW 1 with equal tile shares
-@pytest.mark.parametrize("B,T,ldz,mode", [(256, 16, 32, 0), (64, 20, 40, 0), (48, 9, 32, 4096), (64, 12, 32, 256),
-                                           (200, 12, 32, 0), (40, 17, 40, 0)])
+# mode 4096: the wide kernels forced at a small batch; 512: the NT = 2 forward past B = 64; 2048:
+# 8 waves instead of 12 (above)
+@pytest.mark.parametrize("B,T,ldz,mode", [(256, 16, 32, 0), (64, 20, 40, 0), (48, 9, 32, 4096), (256, 12, 32, 512),
+                                           (200, 12, 32, 512), (40, 17, 40, 0), (96, 9, 32, 0), (256, 12, 32, 512 | 2048),
+                                           (64, 20, 40, 2048), (48, 9, 32, 4096 | 2048), (200, 12, 32, 0)])
 def test_fused_z_projection_forward(B, T, ldz, mode):
     """mlvae_lstm_fwd_z (layer 0 with its input projection z W_ih^T + b_ih + b_hh computed inside the
     recurrence from the 32-wide bf16 latent) against the fp64 loop on the same projection: h, c, the
