@@ -1229,6 +1229,12 @@ WidePlan wide_plan(int B, int H, bool fwd, int mode = 0) {
     }
   }
   if (!p.ok) return p;
+  // (TPW 2 in 12 waves -- 2 M-tiles per MFMA wave -- spills 65-117 VGPRs past the 168 a wave has
+  // at three per SIMD: W_hh's resident 12 k-chunks alone take 96, and LDS has room for no more.
+  // The BPTT in 12 waves at TPW 1 -- 8 compute waves, 4 io waves staging the cell inputs and
+  // storing dG -- measured slower, 0.86 -> 0.97 ms per launch at c2 with the io traffic right
+  // behind the step barrier (it queued ahead of the compute waves' publish), 1.0 ms with it held
+  // until every compute wave had polled (the barrier then waited for the io waves).)
   if (fwd && p.tpw == 1) p.w12 = !(mode & 2048);
   p.lds = wide_lds(H, p.HJ, fwd, p.nt);
   if (fwd) p.xbytes = (size_t)2 * p.NB * NSLOT * BG * p.nt * H * 2;
