@@ -481,6 +481,202 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     }
     if (grpw == 0) __builtin_amdgcn_s_barrier();  // both groups pass the same number of barriers
     __syncthreads();  // every wave's last fragment reads are done: the LDS is the epilogue's
+  } else if constexpr (VAR == 16) {
+    // VAR 16: eight phases per two 64-deep K-tiles (two LDS buffers, BK = 64), k-contiguous A and
+    // B.  Two groups of four waves (0-3, 4-7: one of each per SIMD) run one barrier apart; a phase
+    // of a group is [its fragment reads + one staged half-tile (2 LDS-DMA pieces per wave) +
+    // counted waits] barrier [16 MFMAs: one quadrant of its 128 x 64 output, K = 64] barrier, so a
+    // SIMD's MFMA pipe is fed by one group while the other reads and stages, in quarter-size
+    // slices (VAR 12: 32-MFMA slots over BK = 32).  Quadrants (64-row sub sa, 32-col sub qb):
+    // Q1 (0,0) reads B qb 0 + A sub 0 (12 ds_read_b128), Q2 (0,1) B qb 1 (4), Q3 (1,1) A sub 1 (8),
+    // Q4 (1,0) none.  Half-tiles: A rows 0-127 / 128-255, B rows 0-127 / 128-255 of a buffer.
+    // Staging slots (phase: buffer half, K-tile): 1: b1 A0 t+1, 2: b1 A1 t+1, 3: b0 B0 t+2,
+    // 4: b0 B1 t+2, 5: b0 A0 t+2, 6: b0 A1 t+2, 7: b1 B0 t+3, 8: b1 B1 t+3 (t = 2 x iteration).
+    // RAW: every half-tile is issued >= 3 phases before its first read, and each phase waits
+    // vmcnt(4) (its last two phases' pieces may fly) before its first barrier: the reader's own
+    // pieces and the other group's are then retired before a barrier it has passed.  WAR: a half
+    // is restaged >= 1 phase after its last read, whose lgkmcnt(0) precedes that phase's first
+    // barrier.  K-tiles past the end stage as zeros (OOB), so every phase issues its pieces and
+    // the counted wait stays exact; an odd last K-tile multiplies zeros.
+    static_assert(AKC && BKC, "VAR 16: k-contiguous operands");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int grpw = wv >> 2;
+    auto img = [&](int buf, int ab) -> short* { return lds + (buf * 2 + ab) * IMG; };
+    // this wave's 2 pieces of half h (128 rows) of a 256 x 64 k-contiguous image.  Piece 16 h +
+    // 2 wave + j holds rows 128 h + 16 wave + 8 j + lane / 8, 16-byte chunk (lane ^ lane / 8) & 7 at
+    // slot lane & 7: the lane part of the source offset is computed once
+    const int lrow = 16 * wv + (lane >> 3), lc8 = 8 * ((lane ^ (lane >> 3)) & 7);
+    const unsigned baseA = 2u * ((unsigned)(m0 + lrow) * (unsigned)g.lda + (unsigned)lc8);
+    const unsigned baseB = 2u * ((unsigned)(n0 + lrow) * (unsigned)g.ldb + (unsigned)lc8);
+    auto stage_half = [&](int buf, int ab, int h, int kt) {
+      const int k0 = kbeg + kt * TBK;
+      const bool kok = kt < nk && lc8 < kend - k0;
+      const int R = (ab ? g.N - n0 : g.M - m0) - lrow;  // rows left below this lane's row
+      const unsigned ld2 = 2u * (unsigned)(ab ? g.ldb : g.lda);
+      const unsigned base = (ab ? baseB : baseA) + 2u * (unsigned)k0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int dr = 128 * h + 8 * j;
+        const unsigned off = (kok && dr < R) ? base + (unsigned)dr * ld2 : OOB;
+        dma16<false>(ab ? rb : ra, ab ? rwb : rwa, img(buf, ab) + (16 * h + wv * 2 + j) * 512, off);
+      }
+    };
+    // B qb 0 of a K-tile is read in the LAST phase of the K-tile before (into the other of two
+    // register sets), so the phases read 8 / 4 / 8 / 4 fragments: Q1 A sub 0, Q2 B qb 1, Q3 A sub 1,
+    // Q4 the next K-tile's B qb 0 (its halves are staged >= 3 phases before, and the current
+    // K-tile's B halves are last read in Q2: the staging windows above still hold)
+    bf16x8 afr[4][2], b1r[2][2], b0r[2][2][2];
+    auto read_a = [&](const short* As, int sa) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) afr[i][kh] = frag<true>(As, wm * 128 + sa * 64 + i * 16, kh * 32, lane);
+    };
+    auto read_b = [&](const short* Bs, int qb, bf16x8 (&dst)[2][2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) dst[j][kh] = frag<true>(Bs, wn * 64 + qb * 32 + j * 16, kh * 32, lane);
+    };
+    auto mfma_q = [&](int sa, int qb, const bf16x8 (&bq)[2][2]) {
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * sa + i][2 * qb + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][kh], afr[i][kh], acc[4 * sa + i][2 * qb + j], 0, 0, 0);
+    };
+    // one phase: reads (issued by the caller), the half-tile, waits, barrier, MFMAs, barrier
+    auto phase_tail = [&](int buf, int ab, int h, int kt, int sa, int qb, const bf16x8 (&bq)[2][2]) {
+      stage_half(buf, ab, h, kt);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mfma_q(sa, qb, bq);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    };
+    // prologue: K-tile 0 whole (buffer 0), K-tile 1's B halves (buffer 1); K-tile 0's B qb 0
+    stage_half(0, 0, 0, 0); stage_half(0, 0, 1, 0); stage_half(0, 1, 0, 0); stage_half(0, 1, 1, 0);
+    stage_half(1, 1, 0, 1); stage_half(1, 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (grpw == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+    read_b(img(0, 1), 0, b0r[0]);
+    const int niter = (nk + 1) / 2;
+    for (int itr = 0; itr < niter; ++itr) {
+      const int t = 2 * itr;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {  // K-tile t + b in buffer b
+        const short* As = img(b, 0);
+        const short* Bs = img(b, 1);
+        read_a(As, 0);
+        if (b == 0) phase_tail(1, 0, 0, t + 1, 0, 0, b0r[0]);   // phase 1: b1 A0 (t+1)
+        else phase_tail(0, 0, 0, t + 2, 0, 0, b0r[1]);          // phase 5: b0 A0 (t+2)
+        read_b(Bs, 1, b1r);
+        if (b == 0) phase_tail(1, 0, 1, t + 1, 0, 1, b1r);      // phase 2: b1 A1 (t+1)
+        else phase_tail(0, 0, 1, t + 2, 0, 1, b1r);             // phase 6: b0 A1 (t+2)
+        read_a(As, 1);
+        if (b == 0) phase_tail(0, 1, 0, t + 2, 1, 1, b1r);      // phase 3: b0 B0 (t+2)
+        else phase_tail(1, 1, 0, t + 3, 1, 1, b1r);             // phase 7: b1 B0 (t+3)
+        read_b(img(b ^ 1, 1), 0, b0r[b ^ 1]);                   // the next K-tile's B qb 0
+        if (b == 0) phase_tail(0, 1, 1, t + 2, 1, 0, b0r[0]);   // phase 4: b0 B1 (t+2)
+        else phase_tail(1, 1, 1, t + 3, 1, 0, b0r[1]);          // phase 8: b1 B1 (t+3)
+      }
+    }
+    if (grpw == 0) __builtin_amdgcn_s_barrier();  // both groups pass the same number of barriers
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-fill stages past the end land
+    __syncthreads();                                   // before the epilogue reuses the LDS
+  } else if constexpr (VAR == 18) {
+    // VAR 18: VAR 16's eight-phase loop for m/n-contiguous A and B (the weight gradients dW =
+    // dG^T X without time-shifted rows: with the three shift forms of B's staging the build spilled
+    // 10-57 VGPRs, so the time-shifted dW_hh keeps VAR 0).  An image is [64 k][256 m] (512-byte k-rows), so
+    // its contiguous halves are k-halves (32 k-rows = 16 pieces), and a phase multiplies one k-half
+    // of one 64-row sub: P1 (kh 0, sub 0) reads A 4 + B 4 fragments, P2 (kh 0, sub 1) A 4, P3 (kh 1,
+    // sub 1) A 4 + B 4, P4 (kh 1, sub 0) A 4 (16 MFMAs each; fragments by ds_read_b64_tr_b16).
+    // Last reads per K-tile: B kh0 P1, A kh0 P2, B kh1 P3, A kh1 P4; first reads: kh0 P1, kh1 P3.
+    // Staging slots (phase: buffer half, K-tile): 2: b0 Bk0 t+2, 3: b0 Ak0 t+2, 4: b0 Bk1 t+2,
+    // 5: b0 Ak1 t+2, 6: b1 Bk0 t+3, 7: b1 Ak0 t+3, 8: b1 Bk1 t+3, 1: b1 Ak1 t+1 -- each >= 1 phase
+    // after its half's last read and >= 3 phases before its first (VAR 16's waits and barriers).
+    static_assert(!AKC && !BKC, "VAR 18: m/n-contiguous operands");
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int grpw = wv >> 2;
+    // [operand][buffer]: the two buffers of an operand 32 KB apart, inside a ds_read's immediate
+    // offset, so one set of lane addresses serves both
+    auto img = [&](int buf, int ab) -> short* { return lds + (ab * 2 + buf) * IMG; };
+    // this wave's two pieces of k-half h are pieces 16 h + 2 wave + j: k-half 0's lane offsets
+    // serve both (k-half 1 = 32 k-rows further: the column swizzle repeats every 16 rows)
+    McLanes<2> lA, lB;
+    lA.init(2 * wv, lane, g.lda, m0, g.M);
+    lB.init(2 * wv, lane, g.ldb, n0, g.N);
+    auto stage_half = [&](int buf, int ab, int h, int kt) {
+      const int k0 = kbeg + kt * TBK + 32 * h;
+      const int ke = kt < nk ? kend : k0;  // K-tiles past the end: every row out of range (zeros)
+      if (ab == 0) lA.stage<0, true>(img(buf, 0) + 16 * h * 512, ra, rwa, g.lda, k0, ke, 0, 0, 2 * wv);
+      else lB.stage<0, true>(img(buf, 1) + 16 * h * 512, rb, rwb, g.ldb, k0, ke, 0, 0, 2 * wv);
+    };
+    bf16x8 afr[4], bfr[4];
+    auto read_a = [&](const short* As, int sa, int kh) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) afr[i] = frag<false>(As, wm * 128 + sa * 64 + i * 16, kh * 32, lane);
+    };
+    auto read_b = [&](const short* Bs, int kh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<false>(Bs, wn * 64 + j * 16, kh * 32, lane);
+    };
+    auto phase_tail = [&](int buf, int ab, int h, int kt, int sa) {
+      stage_half(buf, ab, h, kt);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 * sa + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], afr[i], acc[4 * sa + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    };
+    // prologue: K-tile 0 whole (buffer 0); K-tile 1's halves but A kh1 (slot 1 of the loop)
+    stage_half(0, 0, 0, 0); stage_half(0, 0, 1, 0); stage_half(0, 1, 0, 0); stage_half(0, 1, 1, 0);
+    stage_half(1, 1, 0, 1); stage_half(1, 0, 0, 1); stage_half(1, 1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (grpw == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+    const int niter = (nk + 1) / 2;
+    for (int itr = 0; itr < niter; ++itr) {
+      const int t = 2 * itr;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {  // K-tile t + b in buffer b
+        const short* As = img(b, 0);
+        const short* Bs = img(b, 1);
+        read_b(Bs, 0);
+        read_a(As, 0, 0);
+        if (b == 0) phase_tail(1, 0, 1, t + 1, 0);   // phase 1: b1 Ak1 (t+1)
+        else phase_tail(0, 0, 1, t + 2, 0);          // phase 5: b0 Ak1 (t+2)
+        read_a(As, 1, 0);
+        if (b == 0) phase_tail(0, 1, 0, t + 2, 1);   // phase 2: b0 Bk0 (t+2)
+        else phase_tail(1, 1, 0, t + 3, 1);          // phase 6: b1 Bk0 (t+3)
+        read_b(Bs, 1);
+        read_a(As, 1, 1);
+        if (b == 0) phase_tail(0, 0, 0, t + 2, 1);   // phase 3: b0 Ak0 (t+2)
+        else phase_tail(1, 0, 0, t + 3, 1);          // phase 7: b1 Ak0 (t+3)
+        read_a(As, 0, 1);
+        if (b == 0) phase_tail(0, 1, 1, t + 2, 0);   // phase 4: b0 Bk1 (t+2)
+        else phase_tail(1, 1, 1, t + 3, 0);          // phase 8: b1 Bk1 (t+3)
+      }
+    }
+    if (grpw == 0) __builtin_amdgcn_s_barrier();  // both groups pass the same number of barriers
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the zero-fill stages past the end land
+    __syncthreads();                                   // before the epilogue reuses the LDS
   } else if constexpr (VAR == 9) {
     static_assert(!AKC && !BKC, "VAR 9: fp8 operands stored m/n-contiguous");
     auto stage_both = [&](int buf, int k0) {
@@ -848,6 +1044,16 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
     case 5: return launch_fast_v<AKC, BKC, 0>(g, grid, s);  // the previous default (A/B)
     case 6: return launch_fast_v<AKC, BKC, 6>(g, grid, s);  // VAR 0 with the MLVAE_GEMM_ABL switches
     case 12: return launch_fast_v<AKC, BKC, 12>(g, grid, s);
+    case 18:  // the same for m/n-contiguous A and B (weight gradients without time-shifted rows)
+      if constexpr (!AKC && !BKC)
+        if (g.kshift == 0 && g.kshift_bstep == 0) return launch_fast_v<false, false, 18>(g, grid, s);
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 16>(g, grid, s);
+      if constexpr (AKC) return launch_fast_v<true, BKC, 12>(g, grid, s);
+      return launch_fast_v<AKC, BKC, 0>(g, grid, s);
+    case 16:  // eight phases over two 64-deep K-tiles (k-contiguous A and B; else the default)
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 16>(g, grid, s);
+      if constexpr (AKC) return launch_fast_v<true, BKC, 12>(g, grid, s);
+      return launch_fast_v<AKC, BKC, 0>(g, grid, s);
     case 13:  // VAR 12 with the timing ablations (k-contiguous operands only)
       if constexpr (AKC && BKC) return launch_fast_v<true, true, 13>(g, grid, s);
       return 1;
@@ -855,10 +1061,19 @@ int launch_fast(const GFArgs& g, dim3 grid, hipStream_t s, int var) {
       if constexpr (AKC && BKC) return launch_fast_v<true, true, 8>(g, grid, s);
       return 1;
     default:
-      // k-contiguous A (projection, dgrad): the ping-pong ring (same-process A/B at c3 against
-      // VAR 4: projection 1.328 -> 1.287 ms, dgrad 1.134 -> 1.098 (W^T) / 1.361 -> 1.252 (W),
-      // 4096^3 1,119 -> 1,217 TF/s); m-contiguous A (weight gradients): VAR 0
+      // k-contiguous A and B (projection, dgrad against W^T, the heads' products): the eight-phase
+      // loop (round 6, profiles/ab/r06_gemm_var16.txt: same process, c3 shapes, projection
+      // 1,305 -> 1,271 us, dgrad (W^T) 1,139 -> 1,082, 4096^3 1,185 -> 1,280 TF/s; in the c3 step
+      // projection 1.06 -> 1.01 ms, dgrad 0.96 -> 0.865, step 9.78 -> 9.60 ms).  k-contiguous A with
+      // m/n-contiguous B: the ping-pong ring (against VAR 4: projection 1.328 -> 1.287 ms, dgrad
+      // 1.134 -> 1.098 (W^T) / 1.361 -> 1.252 (W)); m-contiguous A (weight gradients): VAR 0
+      // m/n-contiguous A and B without time-shifted rows (dW_ih, the heads' dW1): VAR 18 (c3, in
+      // the step: dW_ih_l1 0.936 -> 0.82 ms, profiles/ab/r06_gemm_var18.txt); time-shifted (dW_hh):
+      // VAR 0
+      if constexpr (AKC && BKC) return launch_fast_v<true, true, 16>(g, grid, s);
       if constexpr (AKC) return launch_fast_v<true, BKC, 12>(g, grid, s);
+      if constexpr (!AKC && !BKC)
+        if (g.kshift == 0 && g.kshift_bstep == 0) return launch_fast_v<false, false, 18>(g, grid, s);
       return launch_fast_v<AKC, BKC, 0>(g, grid, s);
   }
 }
