@@ -190,7 +190,9 @@ int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* 
                        const float* cells, const float* dy, void* dg_bf16, float* dbias_rows,
                        void* dg_fp8, const float* dg8_scale, unsigned* dg_amax, void* xbuf,
                        size_t xbytes, int* err, void* stream);
-/* mlvae_lstm_bwd_fp8 with dy as bf16 [B*T, 2H] when dy_bf16 = 1 (as mlvae_lstm_bwd_ex3). */
+/* mlvae_lstm_bwd_fp8 with dy as bf16 [B*T, 2H] when dy_bf16 = 1 (as mlvae_lstm_bwd_ex3).  Both
+ * forms: dg_bf16 may be NULL when dg_fp8 is given (every dG reader on e4m3: the dgrad, dW_ih and
+ * dW_hh through mlvae_gemm_fp8_tn_ex); the bias rows still come from the fp32 dG. */
 int mlvae_lstm_bwd_fp8_ex(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
                           const float* cells, const void* dy, int dy_bf16, void* dg_bf16,
                           float* dbias_rows, void* dg_fp8, const float* dg8_scale, unsigned* dg_amax,
@@ -265,6 +267,17 @@ int mlvae_gemm_fp8_ex(int M, int N, int K, const void* A, int lda, const void* B
 size_t mlvae_gemm_fp8_tn_workspace_size(int M, int N, int K);
 int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
                       const float* alpha, float* ws, size_t ws_bytes, void* stream);
+/* mlvae_gemm_fp8_tn batched (A + z a_bstride, B + z b_bstride bytes, C + z c_bstride floats) with
+ * time-shifted B rows: row k of B_z is read at k + sh_z, sh_z = kshift + z kshift_bstep, when
+ * 0 <= k % kshift_T + sh_z < kshift_T, else as zeros (K % kshift_T == 0): the recurrent weight
+ * gradients dW_hh = sum_t dG_t^T h_{t-1} (forward) / h_{t+1} (reverse) of both directions in one
+ * launch on e4m3 dG and h (ref:src/modules/decoder.py:14-15,22; the bf16 form: mlvae_gemm_bf16's
+ * kshift arguments).  Strides % 16; workspace mlvae_gemm_fp8_tn_ex_workspace_size bytes. */
+size_t mlvae_gemm_fp8_tn_ex_workspace_size(int M, int N, int K, int batch);
+int mlvae_gemm_fp8_tn_ex(int M, int N, int K, int batch, const void* A, int lda, long long a_bstride,
+                         const void* B, int ldb, long long b_bstride, float* C, int ldc, long long c_bstride,
+                         const float* alpha, int kshift_T, int kshift, int kshift_bstep, float* ws,
+                         size_t ws_bytes, void* stream);
 size_t mlvae_fp8_scale_workspace_size(void);
 int mlvae_fp8_scale(size_t n, const float* x, float other_scale, float* out, float* ws, size_t ws_bytes,
                     void* stream);
@@ -420,6 +433,13 @@ int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, const void* Bt,
 size_t mlvae_skinny_tn_workspace_size(int M, int NB, int K);
 int mlvae_skinny_tn(int M, int NB, int K, const void* A, int lda, const void* B, int ldb, int nw,
                     float* W, float* bias1, float* bias2, float* ws, size_t ws_bytes, void* stream);
+/* fp8 mode (configs[4]), layer 0: the same two products on the e4m3 dG the fp8 BPTT writes (lda in
+ * bytes, % 16) -- converted to bf16 in registers (exact), results times *alpha (1 / dG's scale).
+ * mlvae_skinny_nt_fp8 needs K % 256 and M >= 4096; mlvae_skinny_tn_fp8 mlvae_skinny_tn's workspace. */
+int mlvae_skinny_nt_fp8(int M, int N, int K, const void* A8, int lda, const void* Bt, int ldb, float* C, int ldc,
+                        const float* alpha, void* stream);
+int mlvae_skinny_tn_fp8(int M, int NB, int K, const void* A8, int lda, const void* B, int ldb, int nw, float* W,
+                        float* bias1, float* bias2, const float* alpha, float* ws, size_t ws_bytes, void* stream);
 /* dZ = dG W_ih_l0 (as mlvae_skinny_nt) and dW_ih_l0 | b_ih = b_hh gradients = dG^T [z | 1] (as
  * mlvae_skinny_tn) from ONE pass over the layer-0 dG (ref:src/modules/decoder.py:14-15,22, the
  * autograd of nn.LSTM's layer-0 input projection): dG [M][lda] bf16 with K8 = 8H columns

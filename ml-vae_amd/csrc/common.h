@@ -207,6 +207,15 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
   return (unsigned)w;
 }
 
+// eight e4m3 (two dwords) -> eight bf16, exactly (every e4m3 value is a bf16 value: 3 of bf16's 7
+// mantissa bits, exponents inside its range), through v_cvt_pk_f32_fp8 (OCP, as pack4_fp8)
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(unsigned lo, unsigned hi) {
+  const auto a = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)lo, true);
+  const auto c = __builtin_amdgcn_cvt_pk_f32_fp8((int)hi, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)hi, true);
+  auto t = [](float x) { return (short)(__float_as_uint(x) >> 16); };
+  return bf16x8{t(a[0]), t(a[1]), t(b[0]), t(b[1]), t(c[0]), t(c[1]), t(d[0]), t(d[1])};
+}
+
 // Workgroup barrier for LDS reuse only: the LDS operations done, the global stores left in flight.
 // (__syncthreads() also waits for every outstanding global store: in the 256-squared GEMM's staged
 // epilogue that put four HBM write round trips of the chip-wide store burst into every tile -- the

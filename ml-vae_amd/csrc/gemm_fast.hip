@@ -25,6 +25,8 @@
 //     partial slabs + a fixed-order reduce: deterministic).
 #include "common.h"
 #include <stdlib.h>
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -276,16 +278,25 @@ __device__ __forceinline__ i32x8 frag8(const short* img, int base, int lane) {
 __device__ __forceinline__ int swz8(int kr) { return (kr & 7) | (((kr >> 5) & 1) << 3); }
 
 // this wave's 4 LDS-DMA pieces (1 KB each) of one [128 k][256 m] fp8 image; element (m, k) at byte
-// p[k * ld + m]; rows [r0, r0 + 256) bounded by R (R % 16 == 0), k [k0, k0 + 128) by kend
+// p[k * ld + m]; rows [r0, r0 + 256) bounded by R (R % 16 == 0), k [k0, k0 + 128) by kend.
+// Time-shifted k-rows (sh != 0, the recurrent dW_hh): row k reads k + sh when 0 <= k % shT + sh
+// < shT, else zeros (as mc_off: one scalar division per stage, one wrap per lane when shT >= 128)
 __device__ __forceinline__ void stage8_mc(short* img, __amdgpu_buffer_rsrc_t rs, i32x4 rw, int ld, int r0, int R, int k0,
-                                          int kend, int wave, int lane) {
+                                          int kend, int shT, int sh, int wave, int lane) {
+  const int tk = sh != 0 ? k0 % shT : 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int piece = wave * 4 + j;
     const int p = piece * 64 + lane;
     const int kr = p >> 4, c = (p & 15) ^ swz8(kr);
     const int gk = k0 + kr, gm = r0 + 16 * c;
-    const unsigned off = (gk < kend && gm < R) ? (unsigned)gk * (unsigned)ld + (unsigned)gm : OOB;
+    bool ok = gk < kend && gm < R;
+    if (sh != 0) {
+      int t = tk + kr;
+      t = shT >= 128 ? (int)min((unsigned)t, (unsigned)(t - shT)) : t % shT;
+      ok = ok && (unsigned)(t + sh) < (unsigned)shT;
+    }
+    const unsigned off = ok ? (unsigned)(gk + sh) * (unsigned)ld + (unsigned)gm : OOB;
     dma16<true>(rs, rw, img + piece * 512, off);
   }
 }
@@ -498,6 +509,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
     // is restaged >= 1 phase after its last read, whose lgkmcnt(0) precedes that phase's first
     // barrier.  K-tiles past the end stage as zeros (OOB), so every phase issues its pieces and
     // the counted wait stays exact; an odd last K-tile multiplies zeros.
+    // (the same schedule over fp8 operands, 8 block-scaled 16x16x128 MFMAs per quadrant, measured
+    // no faster than VAR 8 and spilled: profiles/ab/r06_fp8_var20.txt)
     static_assert(AKC && BKC, "VAR 16: k-contiguous operands");
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     const int grpw = wv >> 2;
@@ -680,8 +693,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GFArgs g) {
   } else if constexpr (VAR == 9) {
     static_assert(!AKC && !BKC, "VAR 9: fp8 operands stored m/n-contiguous");
     auto stage_both = [&](int buf, int k0) {
-      stage8_mc(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, wave, lane);
-      stage8_mc(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, wave, lane);
+      stage8_mc(lds + (buf * 2 + 0) * IMG, ra, rwa, g.lda, m0, g.M, k0, kend, 0, 0, wave, lane);
+      stage8_mc(lds + (buf * 2 + 1) * IMG, rb, rwb, g.ldb, n0, g.N, k0, kend, g.kshiftT, sh, wave, lane);
     };
     if (nk > 0) {
       stage_both(0, kbeg);
@@ -1242,8 +1255,8 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
 // C[M,N] (fp32) = (*alpha) * A^T B over fp8 e4m3 (OCP) operands stored [K][M] and [K][N] (m- and
 // n-contiguous: the weight gradient dW = dG^T X over K frames), deterministic split-K through the
 // workspace (mlvae_gemm_fp8_tn_workspace_size).  gemm256_kernel VAR 9.
-static void fp8_tn_plan(int M, int N, int K, int* splits, int* kchunk) {
-  const long tiles = (long)((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
+static void fp8_tn_plan(int M, int N, int K, int batch, int* splits, int* kchunk) {
+  const long tiles = (long)((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN) * batch;
   int s = 1;
   if (tiles < 128 && K >= 128 * 16) {
     s = (int)((split_target() + tiles - 1) / tiles);
@@ -1259,49 +1272,69 @@ static void fp8_tn_plan(int M, int N, int K, int* splits, int* kchunk) {
   *kchunk = kc;
 }
 
-extern "C" size_t mlvae_gemm_fp8_tn_workspace_size(int M, int N, int K) {
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
+extern "C" size_t mlvae_gemm_fp8_tn_ex_workspace_size(int M, int N, int K, int batch) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch < 1) return 0;
   int s, kc;
-  fp8_tn_plan(M, N, K, &s, &kc);
-  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  fp8_tn_plan(M, N, K, batch, &s, &kc);
+  return s > 1 ? (size_t)s * M * N * batch * sizeof(float) : 0;
 }
 
-extern "C" int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C,
-                                 int ldc, const float* alpha, float* ws, size_t ws_bytes, void* stream) {
-  if (M < 0 || N < 0 || K < 0 || !C || !alpha || (K > 0 && (!A || !B))) {
+extern "C" size_t mlvae_gemm_fp8_tn_workspace_size(int M, int N, int K) {
+  return mlvae_gemm_fp8_tn_ex_workspace_size(M, N, K, 1);
+}
+
+// batched, with time-shifted B rows: C_z = (*alpha) A_z^T B_z~ (z < batch; A_z = A + z a_bstride,
+// B_z = B + z b_bstride bytes, C_z = C + z c_bstride floats) where B_z~ row k is B_z row k + sh_z,
+// sh_z = kshift + z kshift_bstep, for 0 <= k % kshift_T + sh_z < kshift_T, else zeros -- the
+// recurrent weight gradient dW_hh of both directions, sum_t dG_t^T h_{t -/+ 1}, on e4m3 operands
+// (as mlvae_gemm_bf16's kshift arguments)
+extern "C" int mlvae_gemm_fp8_tn_ex(int M, int N, int K, int batch, const void* A, int lda, long long a_bstride,
+                                    const void* B, int ldb, long long b_bstride, float* C, int ldc,
+                                    long long c_bstride, const float* alpha, int kshift_T, int kshift,
+                                    int kshift_bstep, float* ws, size_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || batch < 1 || !C || !alpha || (K > 0 && (!A || !B))) {
     mlvae_set_error("mlvae_gemm_fp8_tn: bad shape/ptr");
     return 1;
   }
   if (M == 0 || N == 0) return 0;
   if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || (lda % 16) || (ldb % 16) || (M % 16) || (N % 16) ||
-      lda < M || ldb < N || N % 4 || ldc % 4 || ((uintptr_t)C % 16) || ldc < N) {
-    mlvae_set_error("mlvae_gemm_fp8_tn: M, N, lda, ldb %% 16, aligned operands, ldc %% 4, aligned C");
+      lda < M || ldb < N || N % 4 || ldc % 4 || ((uintptr_t)C % 16) || ldc < N || (a_bstride % 16) ||
+      (b_bstride % 16) || (c_bstride % 4) || a_bstride < 0 || b_bstride < 0 || c_bstride < 0) {
+    mlvae_set_error("mlvae_gemm_fp8_tn: M, N, lda, ldb %% 16, aligned operands and batch strides, ldc %% 4, aligned C");
     return 1;
   }
-  if ((size_t)K * lda >= OOB || (size_t)K * ldb >= OOB) {
+  const bool shifted = kshift != 0 || kshift_bstep != 0;
+  const int shmax = std::max(std::abs(kshift), std::abs(kshift + (batch - 1) * kshift_bstep));
+  if (shifted && (kshift_T <= 0 || K % kshift_T || shmax >= kshift_T)) {
+    mlvae_set_error("mlvae_gemm_fp8_tn: time-shifted rows need K %% kshift_T == 0 and |shift| < kshift_T");
+    return 1;
+  }
+  if ((size_t)K * lda + (size_t)(batch - 1) * a_bstride >= OOB ||
+      (size_t)K * ldb + (size_t)(batch - 1) * b_bstride >= OOB) {
     mlvae_set_error("mlvae_gemm_fp8_tn: operand larger than 2 GB");
     return 1;
   }
   int s, kc;
-  fp8_tn_plan(M, N, K, &s, &kc);
-  if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * sizeof(float))) {
+  fp8_tn_plan(M, N, K, batch, &s, &kc);
+  if (s > 1 && (!ws || ws_bytes < (size_t)s * M * N * batch * sizeof(float))) {
     mlvae_set_error("mlvae_gemm_fp8_tn: workspace too small (%zu B)", ws_bytes);
     return 1;
   }
   GFArgs g;
   g.M = M; g.N = N; g.K = K;
-  g.A = static_cast<const short*>(A); g.lda = lda; g.a_bs = 0;   // byte units (VAR 9)
-  g.B = static_cast<const short*>(B); g.ldb = ldb; g.b_bs = 0;
-  g.C = C; g.ldc = ldc; g.c_bs = 0; g.beta = 0.f;
+  // byte units (VAR 9); the batch strides in the kernel's 2-byte pointer units
+  g.A = static_cast<const short*>(A); g.lda = lda; g.a_bs = a_bstride / 2;
+  g.B = static_cast<const short*>(B); g.ldb = ldb; g.b_bs = b_bstride / 2;
+  g.C = C; g.ldc = ldc; g.c_bs = c_bstride; g.beta = 0.f;
   g.bias1 = nullptr; g.bias2 = nullptr; g.epi = EPI_NONE; g.aux = nullptr; g.ldaux = 0;
-  g.kshiftT = 0; g.kshift = 0; g.kshift_bstep = 0;
+  g.kshiftT = shifted ? kshift_T : 0; g.kshift = kshift; g.kshift_bstep = kshift_bstep;
   g.dseed = 0; g.doff = 0; g.dkeep = 1.f; g.dscale = 1.f;
   g.ws = ws; g.alpha = alpha; g.abl = 0;
   g.splits = s; g.kchunk = kc;
   g.group_m = 1;
   g.c16 = 0;
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), 1, s);
+  dim3 grid(((N + TBN - 1) / TBN) * ((M + TBM - 1) / TBM), batch, s);
   const int rc = launch_fast_v<false, false, 9>(g, grid, st);
   if (rc) return rc;
   MLVAE_CHECK_LAUNCH();
@@ -1309,10 +1342,15 @@ extern "C" int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, co
     const size_t MN = (size_t)M * N;
     int blocks = (int)((MN + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    splitk_reduce_fast<<<dim3(blocks, 1), 256, 0, st>>>(g);
+    splitk_reduce_fast<<<dim3(blocks, batch), 256, 0, st>>>(g);
     MLVAE_CHECK_LAUNCH();
   }
   return 0;
+}
+
+extern "C" int mlvae_gemm_fp8_tn(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C,
+                                 int ldc, const float* alpha, float* ws, size_t ws_bytes, void* stream) {
+  return mlvae_gemm_fp8_tn_ex(M, N, K, 1, A, lda, 0, B, ldb, 0, C, ldc, 0, alpha, 0, 0, 0, ws, ws_bytes, stream);
 }
 
 // C[M,N] (fp32, or fp16 with EPI_OUT_F16) = (*alpha) * A . B^T + bias1 + bias2 over fp8 e4m3 (OCP)

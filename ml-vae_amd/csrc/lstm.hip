@@ -1075,7 +1075,10 @@ int run(bool fwd, int prec, int B, int T, int H, const float* W0, const float* W
     return 1;
   }
   if (wide) {
-    if (!fwd && !dgb) { mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 (NULL)"); return 1; }
+    if (!fwd && !dgb && !ex.f8.dg8) {
+      mlvae_set_error("lstm: the wide-batch backward writes dG to dg_bf16 or (fp8 mode) dg_fp8 (both NULL)");
+      return 1;
+    }
     if (ex.ydb && !(ex.p >= 0.f && ex.p < 1.f)) { mlvae_set_error("lstm: dropout p=%g", ex.p); return 1; }
     return lstm_wide_run(fwd, B, T, H, W0, W1, G, Cs, Y, xbuf, xbytes, err, st, yb, dgb, ex.dbias, ex.ydb,
                          ex.seed, ex.off, ex.p, g_dbg, g_dbg_mode, ex.f8, ex.dyb, ex.wz);

@@ -1103,7 +1103,8 @@ __global__ __launch_bounds__(512, OCC) void lstm_bwd_wide_kernel(LstmArgs a) {
         const int k = kslot * 8, g = k / HJ, u = k % HJ;
         const u32x4 v = *reinterpret_cast<const u32x4*>(ab + r * ROWB + swz(r, kslot) * 16);
         const size_t o = ((size_t)b * T + t) * 8 * H + dir * 4 * H + g * H + j0 + u;
-        *reinterpret_cast<u32x4*>(a.dGb + o) = v;  // G is fp16 here: dG always goes to dGb
+        // G is fp16 here: dG goes to dGb (NULL in fp8 mode when every reader takes the e4m3 copy)
+        if (!F8 || a.dGb) *reinterpret_cast<u32x4*>(a.dGb + o) = v;
         if constexpr (F8) {
           float f[8];
 #pragma unroll

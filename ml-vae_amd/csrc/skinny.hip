@@ -128,24 +128,40 @@ __global__ __launch_bounds__(256) void skinny_nt_ks_kernel(int M, int K, const u
 // 16 rows (twice the bytes of its A stream) and held 2.5 TB/s on the 1 GB dG of c3 (409 us).
 // A chunk c+1 (16 B x 8 per lane, 64 KB per workgroup in flight) and Bt chunk c+1 are loaded
 // while chunk c's MFMAs run.  K % 256 == 0.
+// F8: A is e4m3 (fp8 mode's layer-0 dG, lda in bytes) converted to bf16 in registers (exact; the
+// kernel streams A, so half its bytes is half its time) and C scaled by *alpha (1 / dG's scale).
 constexpr int NTL_KC = 256, NTL_LB = NTL_KC + 8;  // K-chunk, LDS row stride (shorts)
-template <int NT>
-__global__ __launch_bounds__(512) void skinny_nt_lds_kernel(int M, int K, const unsigned short* __restrict__ A,
+template <int NT, bool F8 = false>
+__global__ __launch_bounds__(512) void skinny_nt_lds_kernel(int M, int K, const void* __restrict__ Av,
                                                             int lda, const unsigned short* __restrict__ Bt,
-                                                            int ldb, float* __restrict__ C, int ldc) {
+                                                            int ldb, float* __restrict__ C, int ldc,
+                                                            const float* __restrict__ alpha) {
   constexpr int NB = 16 * NT, BPT = (NB * NTL_KC / 8 + 511) / 512;  // 16-byte Bt pieces per thread
   __shared__ __attribute__((aligned(16))) short sb[2][NB * NTL_LB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, q = lane >> 4;
   const int row = blockIdx.x * 128 + wave * 16 + l15;
   const bool rv = row < M;
-  const unsigned short* ap = A + (size_t)(rv ? row : 0) * lda + 8 * q;
+  const unsigned short* ap = static_cast<const unsigned short*>(Av) + (size_t)(rv ? row : 0) * lda + 8 * q;
+  const unsigned char* ap8 = static_cast<const unsigned char*>(Av) + (size_t)(rv ? row : 0) * lda + 8 * q;
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
   bf16x8 ac[8], an[8];
+  u32x2 a8[8];  // F8: the next chunk's raw e4m3 (converted when it becomes current)
   u32x4 br[BPT];
   auto aload = [&](int k0, bf16x8 (&d)[8]) {
+    if constexpr (F8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) d[u] = rv ? *reinterpret_cast<const bf16x8*>(ap + k0 + 32 * u) : z8;
+      for (int u = 0; u < 8; ++u) a8[u] = rv ? *reinterpret_cast<const u32x2*>(ap8 + k0 + 32 * u) : u32x2{0u, 0u};
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d[u] = rv ? *reinterpret_cast<const bf16x8*>(ap + k0 + 32 * u) : z8;
+    }
+  };
+  auto aconv = [&](bf16x8 (&d)[8]) {
+    if constexpr (F8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d[u] = fp8x8_to_bf16(a8[u][0], a8[u][1]);
+    }
   };
   auto bload = [&](int k0) {
 #pragma unroll
@@ -166,6 +182,7 @@ __global__ __launch_bounds__(512) void skinny_nt_lds_kernel(int M, int K, const 
   for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nc = K / NTL_KC;
   aload(0, ac);
+  aconv(ac);
   bload(0);
   bstore(0);
   __syncthreads();
@@ -180,21 +197,33 @@ __global__ __launch_bounds__(512) void skinny_nt_lds_kernel(int M, int K, const 
         acc[j] = mfma16(*reinterpret_cast<const bf16x8*>(b + (16 * j + l15) * NTL_LB + 32 * u + 8 * q), ac[u], acc[j]);
     if (more) bstore((c + 1) & 1);
     __syncthreads();
+    if constexpr (F8) {
+      if (more) aconv(ac);
+    } else {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) ac[u] = an[u];
+      for (int u = 0; u < 8; ++u) ac[u] = an[u];
+    }
   }
   if (!rv) return;
+  if constexpr (F8) {
+    const float al = *alpha;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] *= al;
+  }
   // swapped operands: lane holds C[row][16j + 4q + r]
 #pragma unroll
   for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(C + (size_t)row * ldc + 16 * j + 4 * q) = acc[j];
 }
 
 // LDS images: A [64 frames][64 m + 8], B [64 frames][NB + 8] (bf16); transposed fragment reads.
-template <int NT>
-__global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk,
-                                                        const unsigned short* __restrict__ A, int lda,
-                                                        const unsigned short* __restrict__ B, int ldb,
-                                                        float* __restrict__ ws) {
+// F8: A is e4m3 (fp8 mode's layer-0 dG, lda in bytes), converted to bf16 on its way into the LDS
+// image (exact), the partial slabs scaled by *alpha (1 / dG's scale).
+template <int NT, bool F8 = false>
+__global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk, const void* __restrict__ Av,
+                                                        int lda, const unsigned short* __restrict__ B, int ldb,
+                                                        float* __restrict__ ws, const float* __restrict__ alpha) {
+  const unsigned short* A = static_cast<const unsigned short*>(Av);
+  const unsigned char* A8 = static_cast<const unsigned char*>(Av);
   constexpr int NB = 16 * NT, LA = 64 + 8, LB = NB + 8;
   __shared__ __attribute__((aligned(16))) short sa[64 * LA];
   __shared__ __attribute__((aligned(16))) short sb[64 * LB];
@@ -216,7 +245,12 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i, fr = idx >> 3, c8 = idx & 7;
       const int f = k0 + fr;
-      va[i] = f < kend ? *reinterpret_cast<const u32x4*>(A + (size_t)f * lda + m0 + 8 * c8) : u32x4{0u, 0u, 0u, 0u};
+      if constexpr (F8) {
+        const u32x2 r = f < kend ? *reinterpret_cast<const u32x2*>(A8 + (size_t)f * lda + m0 + 8 * c8) : u32x2{0u, 0u};
+        va[i] = u32x4{r[0], r[1], 0u, 0u};
+      } else {
+        va[i] = f < kend ? *reinterpret_cast<const u32x4*>(A + (size_t)f * lda + m0 + 8 * c8) : u32x4{0u, 0u, 0u, 0u};
+      }
     }
 #pragma unroll
     for (int i = 0; i < NVB; ++i) {
@@ -232,7 +266,8 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i, fr = idx >> 3, c8 = idx & 7;
-      *reinterpret_cast<u32x4*>(sa + fr * LA + 8 * c8) = va[i];
+      if constexpr (F8) *reinterpret_cast<bf16x8*>(sa + fr * LA + 8 * c8) = fp8x8_to_bf16(va[i][0], va[i][1]);
+      else *reinterpret_cast<u32x4*>(sa + fr * LA + 8 * c8) = va[i];
     }
 #pragma unroll
     for (int i = 0; i < NVB; ++i) {
@@ -260,6 +295,11 @@ __global__ __launch_bounds__(256) void skinny_tn_kernel(int M, int K, int kchunk
   }
   const int m = m0 + 16 * wave + (lane & 15), q = lane >> 4;
   if (m >= M) return;
+  if constexpr (F8) {
+    const float al = *alpha;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] *= al;
+  }
   float* out = ws + ((size_t)s * M + m) * NB;
 #pragma unroll
   for (int j = 0; j < NT; ++j) *reinterpret_cast<f32x4*>(out + 16 * j + 4 * q) = acc[j];
@@ -507,10 +547,10 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
                                          // (c3 409 -> 210 us, c2 52 -> 49 us)
     dim3 g128((M + 127) / 128);
     switch (N / 16) {
-      case 1: skinny_nt_lds_kernel<1><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
-      case 2: skinny_nt_lds_kernel<2><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
-      case 3: skinny_nt_lds_kernel<3><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
-      default: skinny_nt_lds_kernel<4><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+      case 1: skinny_nt_lds_kernel<1><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc, nullptr); break;
+      case 2: skinny_nt_lds_kernel<2><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc, nullptr); break;
+      case 3: skinny_nt_lds_kernel<3><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc, nullptr); break;
+      default: skinny_nt_lds_kernel<4><<<g128, 512, 0, st>>>(M, K, a, lda, b, ldb, C, ldc, nullptr); break;
     }
     MLVAE_CHECK_LAUNCH();
     return 0;
@@ -532,6 +572,29 @@ extern "C" int mlvae_skinny_nt(int M, int N, int K, const void* A, int lda, cons
     case 2: skinny_nt_kernel<2><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
     case 3: skinny_nt_kernel<3><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
     default: skinny_nt_kernel<4><<<grid, 256, 0, st>>>(M, K, a, lda, b, ldb, C, ldc); break;
+  }
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp8 mode (configs[4]), layer 0: dZ = alpha dG8 W_ih with dG8 e4m3 [M][lda bytes] (the fp8 BPTT's
+// copy, alpha = 1 / its scale) and W_ih^T bf16 -- skinny_nt's LDS form (K % 256, M >= 4096)
+extern "C" int mlvae_skinny_nt_fp8(int M, int N, int K, const void* A8, int lda, const void* Bt, int ldb,
+                                   float* C, int ldc, const float* alpha, void* stream) {
+  if (M <= 0) return 0;
+  if (!A8 || !Bt || !C || !alpha || N % 16 || N < 16 || N > 64 || K % NTL_KC || M < 4096 || lda % 16 ||
+      ldb % 8 || ldc % 4 || ((uintptr_t)A8 % 16) || ((uintptr_t)Bt % 16) || ((uintptr_t)C % 16)) {
+    mlvae_set_error("mlvae_skinny_nt_fp8: N in {16..64} %% 16, K %% 256, M >= 4096, aligned rows (lda %% 16 B)");
+    return 1;
+  }
+  const unsigned short* b = static_cast<const unsigned short*>(Bt);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g128((M + 127) / 128);
+  switch (N / 16) {
+    case 1: skinny_nt_lds_kernel<1, true><<<g128, 512, 0, st>>>(M, K, A8, lda, b, ldb, C, ldc, alpha); break;
+    case 2: skinny_nt_lds_kernel<2, true><<<g128, 512, 0, st>>>(M, K, A8, lda, b, ldb, C, ldc, alpha); break;
+    case 3: skinny_nt_lds_kernel<3, true><<<g128, 512, 0, st>>>(M, K, A8, lda, b, ldb, C, ldc, alpha); break;
+    default: skinny_nt_lds_kernel<4, true><<<g128, 512, 0, st>>>(M, K, A8, lda, b, ldb, C, ldc, alpha); break;
   }
   MLVAE_CHECK_LAUNCH();
   return 0;
@@ -590,10 +653,46 @@ extern "C" int mlvae_skinny_tn(int M, int NB, int K, const void* A, int lda, con
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(M / 64, S);
   switch (NB / 16) {
-    case 1: skinny_tn_kernel<1><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
-    case 2: skinny_tn_kernel<2><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
-    case 3: skinny_tn_kernel<3><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
-    default: skinny_tn_kernel<4><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws); break;
+    case 1: skinny_tn_kernel<1><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws, nullptr); break;
+    case 2: skinny_tn_kernel<2><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws, nullptr); break;
+    case 3: skinny_tn_kernel<3><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws, nullptr); break;
+    default: skinny_tn_kernel<4><<<grid, 256, 0, st>>>(M, K, kc, a, lda, b, ldb, ws, nullptr); break;
+  }
+  MLVAE_CHECK_LAUNCH();
+  const size_t total = (size_t)M * (nw + 1);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  skinny_reduce<<<blocks, 256, 0, st>>>(M, NB, S, nw, ws, W, bias1, bias2);
+  MLVAE_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp8 mode, layer 0: W [M, nw] (+ biases) = alpha A8^T B as mlvae_skinny_tn, A8 the e4m3 dG [K][lda
+// bytes] (workspace: mlvae_skinny_tn_workspace_size)
+extern "C" int mlvae_skinny_tn_fp8(int M, int NB, int K, const void* A8, int lda, const void* B, int ldb,
+                                   int nw, float* W, float* bias1, float* bias2, const float* alpha, float* ws,
+                                   size_t ws_bytes, void* stream) {
+  if (M <= 0) return 0;
+  if (!A8 || !B || !W || !alpha || M % 64 || NB % 16 || NB < 16 || NB > 64 || nw < 1 ||
+      nw + ((bias1 || bias2) ? 1 : 0) > NB || lda % 16 || ldb % 8 || ((uintptr_t)A8 % 16) || ((uintptr_t)B % 16)) {
+    mlvae_set_error("mlvae_skinny_tn_fp8: M %% 64, NB in {16..64} %% 16, nw (+1) <= NB, aligned rows (lda %% 16 B)");
+    return 1;
+  }
+  const int S = tn_splits(M, K);
+  if (!ws || ws_bytes < (size_t)S * M * NB * sizeof(float)) {
+    mlvae_set_error("mlvae_skinny_tn_fp8: workspace too small");
+    return 1;
+  }
+  int kc = (K + S - 1) / S;
+  kc = (kc + 63) / 64 * 64;
+  const unsigned short* b = static_cast<const unsigned short*>(B);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(M / 64, S);
+  switch (NB / 16) {
+    case 1: skinny_tn_kernel<1, true><<<grid, 256, 0, st>>>(M, K, kc, A8, lda, b, ldb, ws, alpha); break;
+    case 2: skinny_tn_kernel<2, true><<<grid, 256, 0, st>>>(M, K, kc, A8, lda, b, ldb, ws, alpha); break;
+    case 3: skinny_tn_kernel<3, true><<<grid, 256, 0, st>>>(M, K, kc, A8, lda, b, ldb, ws, alpha); break;
+    default: skinny_tn_kernel<4, true><<<grid, 256, 0, st>>>(M, K, kc, A8, lda, b, ldb, ws, alpha); break;
   }
   MLVAE_CHECK_LAUNCH();
   const size_t total = (size_t)M * (nw + 1);

@@ -83,6 +83,8 @@ _SIGS = {
     "mlvae_skinny_nt": [I, I, I, P, I, P, I, P, I, P],
     "mlvae_skinny_tn_workspace_size": [I, I, I],
     "mlvae_skinny_tn": [I, I, I, P, I, P, I, I, P, P, P, P, SZ, P],
+    "mlvae_skinny_nt_fp8": [I, I, I, P, I, P, I, P, I, P, P],
+    "mlvae_skinny_tn_fp8": [I, I, I, P, I, P, I, I, P, P, P, P, P, SZ, P],
     "mlvae_skinny_dzw": [I, I, P, I, P, I, P, I, I, P, I, P, P, P, P, SZ, P],
     "mlvae_skinny_dzw_workspace_size": [I, I],
     "mlvae_encoder_supported": [I, I, I],
@@ -125,6 +127,9 @@ _SIGS = {
     "mlvae_gemm_fp8_ex": [I, I, I, P, I, P, I, P, I, P, P, P, I, U64, U64, F, P],
     "mlvae_gemm_fp8_tn_workspace_size": [I, I, I],
     "mlvae_gemm_fp8_tn": [I, I, I, P, I, P, I, P, I, P, P, SZ, P],
+    "mlvae_gemm_fp8_tn_ex_workspace_size": [I, I, I, I],
+    "mlvae_gemm_fp8_tn_ex": [I, I, I, I, P, I, C.c_longlong, P, I, C.c_longlong, P, I, C.c_longlong, P, I, I, I,
+                             P, SZ, P],
     "mlvae_norm_supported": [I],
     "mlvae_norm_stats": [I, I, I, P, P, P, P, F, P],
     "mlvae_norm_update": [I, P, P, P, I, F, F, P],
@@ -136,6 +141,7 @@ _RESTYPE = {
     "mlvae_skinny_dzw_workspace_size": SZ,
     "mlvae_fp8_scale_workspace_size": SZ,
     "mlvae_gemm_fp8_tn_workspace_size": SZ,
+    "mlvae_gemm_fp8_tn_ex_workspace_size": SZ,
     "mlvae_gemm_workspace_size": SZ,
     "mlvae_gemm_ex_workspace_size": SZ,
     "mlvae_colsum_workspace_size": SZ,

@@ -195,7 +195,7 @@ class _Pool:
 class _Work:
     """Activation/gradient workspaces for one (B, T): views of the engine's growing pool."""
 
-    def __init__(self, cfg, B, T, device, enc_fused=False, pool=None):
+    def __init__(self, cfg, B, T, device, enc_fused=False, pool=None, f8_l0=False):
         N = B * T
         F, E, Z, H, L, C = cfg.F, cfg.E, cfg.Z, cfg.H, cfg.L, cfg.C
         pool = pool or _Pool(device)
@@ -243,7 +243,12 @@ class _Work:
         # the layers below run (one shared pair was overwritten at L >= 3)
         f8 = self.bf and cfg.fp8
         self.X8 = {li: empty(N, 2 * H, dtype=torch.uint8) for li in range(1, L)} if f8 else None
-        self.dG8 = {li: empty(N, 8 * H, dtype=torch.uint8) for li in range(1, L)} if f8 else None
+        # (layer 0 too when its dG readers can take e4m3: the skinny dZ / dW_ih_l0 kernels, i.e. the
+        # fused encoder without the one-pass skinny_dzw form, engine.py _f8_layer0)
+        self.dG8 = {li: empty(N, 8 * H, dtype=torch.uint8) for li in range(0 if f8_l0 else 1, L)} if f8 else None
+        # ... and H8[li] the e4m3 copy of layer li's own h (x-scale), dW_hh's operand: the fp8 BPTT
+        # then writes dG as e4m3 only (12 -> 4 KB per frame)
+        self.H8 = {li: empty(N, 2 * H, dtype=torch.uint8) for li in range(0 if f8_l0 else 1, L)} if f8 else None
         self.E1b = empty(N, E, **b16) if self.enc_fused else None
         self.E2b = empty(N, E, **b16) if self.enc_fused else None
         if self.bf:
@@ -388,16 +393,22 @@ class VAEEngine:
                 # scaling, and the amax words the BPTT writes (two: this step's / the last step's)
                 self.w8t = {li: torch.empty(2 * cfg.H * 8 * cfg.H, device=self.device, dtype=torch.uint8)
                             for li in range(1, cfg.L)}
-                self.g8 = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
-                self.g8_amax = {li: torch.zeros(2, device=self.device, dtype=torch.int32) for li in range(1, cfg.L)}
+                self.g8 = {li: torch.zeros(2, device=self.device) for li in range(0, cfg.L)}
+                self.g8_amax = {li: torch.zeros(2, device=self.device, dtype=torch.int32) for li in range(0, cfg.L)}
                 # the fp8 weight gradient dW_ih = dG^T X (e4m3 dG and layer input): alpha =
                 # 1 / (q_dG * x-scale) (False: bf16)
                 self.fp8_wgrad = True
+                # ... and dW_hh = sum_t dG_t^T h_{t-/+1} on e4m3 dG and h (time-shifted rows in the
+                # fp8 TN kernel), so that no bf16 dG is written (False: bf16 dW_hh and dG)
+                self.fp8_whh = True
+                # ... and layer 0's dG readers (dZ, dW_ih_l0, dW_hh_l0) on e4m3 as well (False: bf16)
+                self.fp8_l0 = True
+                self.one1 = torch.ones(1, device=self.device)  # layer 0's "other" scale: alpha = 1 / q_dG
                 # ... and then (from the second step) the recurrence below writes the e4m3 layer
                 # input alone: no bf16 GEMM reads dropout(h) (False: both copies every step)
                 self.fp8_skip_ydb = True
                 self.x8s = torch.tensor([x8_scale(cfg.dropout)], device=self.device)
-                self.g8w = {li: torch.zeros(2, device=self.device) for li in range(1, cfg.L)}
+                self.g8w = {li: torch.zeros(2, device=self.device) for li in range(0, cfg.L)}
                 self.g8_ready = False  # a previous step's amax exists (the first step's dgrad is bf16)
                 self.g8_par = 0
                 self.f8ws = torch.empty(lib().mlvae_fp8_scale_workspace_size() // 4 + 1, device=self.device)
@@ -523,11 +534,38 @@ class VAEEngine:
             return None
         return _pb(self.flat_bf, self.layout.offsets[name])
 
+    def _fp8_whh(self, w, li, N, T, gp):
+        """fp8 mode: both directions' dW_hh_l{li} = sum_t dG_t^T h_{t-1} / h_{t+1} on e4m3 operands in
+        one batched launch (mlvae_gemm_fp8_tn_ex, time-shifted rows): the layer's e4m3 dG from its
+        BPTT and h cast to e4m3 with the layer-input scale (|h| < 1), so alpha = 1 / (q_dG x-scale)"""
+        H = self.cfg.H
+        l = lib()
+        ws = w.gws_side if self._on_side else w.gws
+        st = self._stream()
+        check(l.mlvae_cast_fp8(N * 2 * H, _pb(w.Yb[li]), 1, None, x8_scale(self.cfg.dropout), w.H8[li].data_ptr(),
+                               st), "cast_fp8")
+        check(l.mlvae_gemm_fp8_tn_ex(4 * H, H, N, 2, w.dG8[li].data_ptr(), 8 * H, 4 * H, w.H8[li].data_ptr(), 2 * H, H,
+                                     gp(f"decoder.rnn.weight_hh_l{li}"), H, 4 * H * H, _p(self.g8w[li], 1), T, -1, 2,
+                                     _p(ws), w.gws_bytes, st), "gemm_fp8_tn_ex")
+
+    def _dzw_path(self, N):
+        """dZ and dW_ih_l0 from the one-pass skinny_dzw kernel (bf16 dG only)"""
+        cfg = self.cfg
+        return bool(self.dzw and cfg.Z == 32 and (8 * cfg.H) % 256 == 0 and N >= 65536)
+
+    def _f8_layer0(self, N):
+        """fp8 mode: layer 0's BPTT writes its dG as e4m3 alone from the second step on, and dZ,
+        dW_ih_l0 (+ biases) and dW_hh_l0 read that copy -- the skinny e4m3 kernels (skinny.hip) and
+        the time-shifted fp8 TN GEMM; needs the fused encoder without the one-pass skinny_dzw form"""
+        cfg = self.cfg
+        return bool(cfg.fp8 and cfg.prec == "bf16" and getattr(self, "fp8_l0", False) and self.fused_encoder
+                    and not self._dzw_path(N) and N >= 4096 and (8 * cfg.H) % 256 == 0 and cfg.H % 16 == 0)
+
     def work(self, B, T):
         key = (B, T)
         if key not in self._work:
             self._work = {key: _Work(self.cfg, B, T, self.device,  # views of the growing pool
-                                     enc_fused=self.fused_encoder, pool=self._pool)}
+                                     enc_fused=self.fused_encoder, pool=self._pool, f8_l0=self._f8_layer0(B * T))}
         return self._work[key]
 
     # ------------------------------------------------------------------ launch helpers
@@ -1071,6 +1109,21 @@ class VAEEngine:
             # the first step has no amax yet and keeps the bf16 dgrad
             f8 = bool(cfg.fp8 and w.g16 and w.dG8 is not None and li in w.dG8 and li in getattr(self, "g8", {}))
             f8_dgrad = f8 and self.g8_ready
+            # configs[4]: dW_ih of an fp8 layer on the e4m3 dG (this step's BPTT) and e4m3 input
+            f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and li in w.X8 and ldx == din and din % 16 == 0
+                       and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, din, N) <= w.gws_bytes)
+            # ... and both directions' dW_hh on the e4m3 dG and h: then no reader is left for a
+            # bf16 dG and the BPTT writes the e4m3 copy alone
+            f8hh = bool(f8w and getattr(self, "fp8_whh", False) and w.H8 is not None and li in w.H8
+                        and H % 16 == 0 and l.mlvae_gemm_fp8_tn_ex_workspace_size(4 * H, H, N, 2) <= w.gws_bytes)
+            # layer 0 (fused encoder, w.dG8 holds it only where _f8_layer0): dZ, dW_ih_l0 | biases and
+            # dW_hh_l0 all on the e4m3 dG
+            f8l0 = bool(li == 0 and f8_dgrad and w.enc_fused and w.H8 is not None and 0 in w.H8
+                        and l.mlvae_gemm_fp8_tn_ex_workspace_size(4 * H, H, N, 2) <= w.gws_bytes
+                        and l.mlvae_skinny_tn_workspace_size(8 * H, w.ZA, N) <= w.gws_bytes)
+            if li == 0:
+                f8hh = f8l0
+            w.__dict__.setdefault("f8hh", {})[li] = f8hh
             with self._timed("lstm_bwd"):
                 # the layer-0 biases come with dW_ih_l0 from skinny_tn when the encoder is fused
                 rows = w.dbias_rows[li] if (w.g16 and not (li == 0 and w.enc_fused)) else None
@@ -1081,12 +1134,14 @@ class VAEEngine:
                     if f8_dgrad and self.fp8_wgrad:  # [q_dG, 1 / (q_dG x-scale)] of the fp8 weight gradient
                         check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), None, _p(self.x8s), G8_MARGIN,
                                                         _p(self.g8w[li]), s), "fp8_delayed_scale")
-                    check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), am + 4 * par, _p(self.w8s[li]), G8_MARGIN,
+                    # [q_dG, alpha]: the fp8 dgrad's 1 / (q_dG q_W); layer 0's skinny products' 1 / q_dG
+                    other = self.one1 if li == 0 else self.w8s[li]
+                    check(l.mlvae_fp8_delayed_scale(am + 4 * (1 - par), am + 4 * par, _p(other), G8_MARGIN,
                                                     _p(self.g8[li]), s), "fp8_delayed_scale")
                     dyb = bool(getattr(w, "dy_bf16", {}).get(li, False))
                     check(l.mlvae_lstm_bwd_fp8_ex(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(Gl),
-                                               _p(w.Cs[li]), _p(w.dY[li]), int(dyb), _pb(dGb),
+                                               _p(w.Cs[li]), _p(w.dY[li]), int(dyb), None if f8hh else _pb(dGb),
                                                _p(rows) if rows is not None else None,
                                                w.dG8[li].data_ptr() if f8_dgrad else None, _p(self.g8[li]),
                                                am + 4 * par, _p(w.xbuf), w.xbuf.numel(), _p(self.err), s),
@@ -1106,20 +1161,21 @@ class VAEEngine:
             pgb = lambda t, off=0: None if t is None else _pb(t, off)
             Ybl = w.Yb[li] if w.bf else None
 
-            # configs[4]: dW_ih of an fp8 layer on the e4m3 dG (this step's BPTT) and e4m3 input
-            f8w = bool(f8_dgrad and self.fp8_wgrad and w.X8 is not None and li in w.X8 and ldx == din and din % 16 == 0
-                       and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, din, N) <= w.gws_bytes)
             if w.__dict__.get("ydb_skipped", {}).get(li) and not f8w:
                 raise RuntimeError(f"layer {li}: the forward skipped the bf16 dropout(h) the bf16 weight gradient reads")
 
             def wgl_body(li=li, dG=dG, dG_bf=dG_bf, xin=xin, xin_bf=xin_bf, din=din, ldx=ldx,
-                         Ybl=Ybl, f8w=f8w):
+                         Ybl=Ybl, f8w=f8w, f8hh=f8hh):
                 if li == 0 and w.enc_fused:
                     # both directions' dW_hh_l0 in one batched 256² launch; dW_ih_l0 and the
                     # biases follow the encoder backward on the main stream (skinny_tn below)
-                    self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
-                               gp("decoder.rnn.weight_hh_l0"), H, batch=2, a_bs=4 * H, b_bs=H,
-                               c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                    with self._timed("wgrad_hh_l0"):
+                        if f8hh:
+                            self._fp8_whh(w, 0, N, T, gp)
+                        else:
+                            self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
+                                       gp("decoder.rnn.weight_hh_l0"), H, batch=2, a_bs=4 * H, b_bs=H,
+                                       c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
                     return
                 if dG_bf is not None and xin_bf is not None and din % 8 == 0 and H % 8 == 0:
                     # 256² GEMMs: dW_ih = dG^T X, and both directions' dW_hh = sum_t dG_t^T h_{t-/+1}
@@ -1136,9 +1192,12 @@ class VAEEngine:
                             self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
                                        gp(f"decoder.rnn.weight_ih_l{li}"), din)
                     with self._timed(f"wgrad_hh_l{li}"):
-                        self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
-                                   gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
-                                   c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                        if f8hh:
+                            self._fp8_whh(w, li, N, T, gp)
+                        else:
+                            self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
+                                       gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
+                                       c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
                 else:
                     self._mm(w, 1, 0, 8 * H, din, N, pg(dG), 8 * H, pg(xin), din,
                              gp(f"decoder.rnn.weight_ih_l{li}"), din, A_bf=pgb(dG_bf), B_bf=pgb(xin_bf))
@@ -1182,7 +1241,7 @@ class VAEEngine:
             drop = li > 0 and xin is not w.Y[li - 1]  # dropout between layers li-1 and li
             seed, mask_ptr = w._drop_seed[li - 1] if drop else (None, None)
             if li == 0 and w.enc_fused:
-                if self.dzw and Z == 32 and w.ZA >= 48 and (8 * H) % 256 == 0 and N >= 65536:
+                if self._dzw_path(N) and w.ZA >= 48:
                     # dZ = dG W_ih_l0 and dW_ih_l0 | db = dG^T [z | 1] from one pass over dG
                     # (skinny.hip skinny_dzw: the skinny NT and TN kernels each read all of it).
                     # Same box, alternating: c3 10.70 -> 10.49 ms/step; at c2's 16,000 frames its
@@ -1193,6 +1252,9 @@ class VAEEngine:
                                              gp("decoder.rnn.bias_ih_l0"), gp("decoder.rnn.bias_hh_l0"),
                                              _p(w.gws), w.gws_bytes, s), "skinny_dzw")
                     dzw_done = True
+                elif f8hh:  # fp8 mode: on the e4m3 dG, alpha = 1 / q_dG
+                    check(l.mlvae_skinny_nt_fp8(N, Z, 8 * H, w.dG8[0].data_ptr(), 8 * H, _pb(self.wih_t[0]), 8 * H,
+                                                _p(w.dZs), Z, _p(self.g8[0], 1), s), "skinny_nt_fp8")
                 else:
                     # dZ = dG W_ih_l0: [N, 8H] x [8H, Z] on the skinny NT kernel
                     check(l.mlvae_skinny_nt(N, Z, 8 * H, _pb(dG_bf), 8 * H, _pb(self.wih_t[0]), 8 * H,
@@ -1260,7 +1322,12 @@ class VAEEngine:
                                         w.enc_ws.numel() * 4, s), "encoder_bwd")
             # dW_ih_l0 | db_ih_l0 = db_hh_l0 = dG^T [z | 1] (skinny.hip), on the main stream
             # while the side stream finishes dW_hh_l0 (the step's two tails run side by side)
-            if not dzw_done:
+            if w.f8hh.get(0):  # fp8 mode: on layer 0's e4m3 dG, alpha = 1 / q_dG
+                check(l.mlvae_skinny_tn_fp8(8 * H, w.ZA, N, w.dG8[0].data_ptr(), 8 * H, _pb(w.Zb), w.ZA, Z,
+                                            gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
+                                            gp("decoder.rnn.bias_hh_l0"), _p(self.g8[0], 1), _p(w.gws), w.gws_bytes,
+                                            s), "skinny_tn_fp8")
+            elif not dzw_done:
                 check(l.mlvae_skinny_tn(8 * H, w.ZA, N, _pb(w.dGb[0]), 8 * H, _pb(w.Zb), w.ZA, Z,
                                         gp("decoder.rnn.weight_ih_l0"), gp("decoder.rnn.bias_ih_l0"),
                                         gp("decoder.rnn.bias_hh_l0"), _p(w.gws), w.gws_bytes, s), "skinny_tn")

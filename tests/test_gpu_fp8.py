@@ -54,7 +54,8 @@ def test_fp8_scale():
 
 
 @pytest.mark.parametrize("M,N,K,f16", [(300, 260, 256, False), (1000, 512, 1024, True), (256, 4096, 1024, True),
-                                       (513, 132, 144, False), (4000, 1024, 2048, False)])
+                                       (513, 132, 144, False), (4000, 1024, 2048, False), (272, 520, 384, False),
+                                       (32, 48, 16, False)])
 def test_gemm_fp8_matches_fp64_on_the_same_operands(M, N, K, f16):
     need_gpu()
     torch.manual_seed(M + N + K)
@@ -97,6 +98,88 @@ def test_gemm_fp8_tn_matches_fp64_on_the_same_operands(M, N, K):
     assert torch.equal(C, C2)
 
 
+@pytest.mark.parametrize("M,N,B,T,split", [(2048, 512, 16, 500, True), (256, 256, 3, 40, False),
+                                           (512, 272, 5, 130, True), (256, 128, 2, 7, False)])
+def test_gemm_fp8_tn_ex_time_shifted_batch_matches_fp64(M, N, B, T, split):
+    """mlvae_gemm_fp8_tn_ex: both directions' dW_hh in one batched launch -- C_z = alpha A_z^T B_z~
+    with B_z~ row k = B_z row k + sh_z (sh = -1 forward, +1 reverse) inside each utterance's T
+    frames, zeros across its ends; A_z / B_z are column blocks of one [K][2M] / [K][2N] operand
+    (the e4m3 dG and h layouts).  Utterance ends inside a 128-frame K-tile, T < 128 and T >= 128,
+    split-K on and off (fewer CUs), against fp64 on the same e4m3 operands; rerun bit-identical."""
+    need_gpu()
+    K = B * T
+    torch.manual_seed(M + N + K)
+    A = (torch.randn(K, 2 * M, device="cuda") * 4).clamp(-448, 448).to(torch.float8_e4m3fn)
+    Bm = (torch.randn(K, 2 * N, device="cuda") * 4).clamp(-448, 448).to(torch.float8_e4m3fn)
+    alpha = torch.tensor([0.0071], device="cuda")
+    C = torch.empty(2, M, N, device="cuda")
+    prev = lib().mlvae_gemm_bf16_set_split_target(256 if split else 1)
+    try:
+        nb = lib().mlvae_gemm_fp8_tn_ex_workspace_size(M, N, K, 2)
+        ws = torch.empty(nb // 4 + 1, device="cuda")
+        call = lambda out: check(lib().mlvae_gemm_fp8_tn_ex(M, N, K, 2, A.data_ptr(), 2 * M, M, Bm.data_ptr(), 2 * N, N,
+                                                            P(out), N, M * N, P(alpha), T, -1, 2, P(ws), nb, stream()))
+        call(C)
+        C2 = torch.empty_like(C)
+        call(C2)
+    finally:
+        lib().mlvae_gemm_bf16_set_split_target(prev)
+    torch.cuda.synchronize()
+    a64, b64 = _f8(A.cpu()), _f8(Bm.cpu())
+    t = torch.arange(K) % T
+    for z, sh in ((0, -1), (1, 1)):
+        bz = b64[:, z * N:(z + 1) * N]
+        src = torch.arange(K) + sh
+        ok = ((t + sh) >= 0) & ((t + sh) < T)
+        bs = torch.zeros_like(bz)
+        bs[ok] = bz[src[ok]]
+        ref = a64[:, z * M:(z + 1) * M].t() @ bs * 0.0071
+        assert rel_err(C[z], ref) < 1e-4, (z, rel_err(C[z], ref))
+    assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("M,N", [(5000, 32), (4096, 48)])
+def test_skinny_nt_fp8_matches_fp64(M, N):
+    """mlvae_skinny_nt_fp8 (fp8 mode's layer-0 dZ = alpha dG8 W_ih): e4m3 A converted to bf16 in
+    registers (exact) against fp64 on the same operands; ragged last 128-row block."""
+    need_gpu()
+    K = 4096
+    torch.manual_seed(M + N)
+    A = (torch.randn(M, K, device="cuda") * 8).clamp(-448, 448).to(torch.float8_e4m3fn)
+    Bt = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    C = torch.empty(M, N, device="cuda")
+    alpha = torch.tensor([0.013], device="cuda")
+    check(lib().mlvae_skinny_nt_fp8(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, P(C), N, P(alpha), stream()))
+    torch.cuda.synchronize()
+    ref = (_f8(A.cpu()) @ Bt.cpu().double().t()) * 0.013
+    assert rel_err(C, ref) < 1e-5, rel_err(C, ref)
+
+
+def test_skinny_tn_fp8_matches_fp64():
+    """mlvae_skinny_tn_fp8 (fp8 mode's dW_ih_l0 | biases = alpha dG8^T [z | 1]): e4m3 A [K][M]
+    converted on its way into LDS, split over frames, ragged K, the ones column's bias sums."""
+    need_gpu()
+    M, NB, nw, K = 4096, 48, 32, 7001
+    torch.manual_seed(K)
+    A = (torch.randn(K, M, device="cuda") * 8).clamp(-448, 448).to(torch.float8_e4m3fn)
+    Bm = torch.zeros(K, NB, device="cuda")
+    Bm[:, :nw] = torch.randn(K, nw, device="cuda")
+    Bm[:, nw] = 1.0
+    Bb = Bm.to(torch.bfloat16)
+    W = torch.empty(M, nw, device="cuda")
+    b1 = torch.empty(M, device="cuda")
+    b2 = torch.empty(M, device="cuda")
+    alpha = torch.tensor([0.021], device="cuda")
+    nb = lib().mlvae_skinny_tn_workspace_size(M, NB, K)
+    ws = torch.empty(nb // 4 + 1, device="cuda")
+    check(lib().mlvae_skinny_tn_fp8(M, NB, K, A.data_ptr(), M, Bb.data_ptr(), NB, nw, P(W), P(b1), P(b2), P(alpha),
+                                    P(ws), nb, stream()))
+    torch.cuda.synchronize()
+    ref = (_f8(A.cpu()).t() @ Bb.cpu().double()) * 0.021
+    assert rel_err(W, ref[:, :nw]) < 1e-5, rel_err(W, ref[:, :nw])
+    assert rel_err(b1, ref[:, nw]) < 1e-5 and torch.equal(b1, b2)
+
+
 def test_gemm_fp8_tn_rejects_bad_shapes():
     need_gpu()
     C = torch.empty(16, 16, device="cuda")
@@ -106,6 +189,11 @@ def test_gemm_fp8_tn_rejects_bad_shapes():
                                    stream()) != 0   # lda < M
     assert lib().mlvae_gemm_fp8_tn(12, 16, 16, a.data_ptr(), 16, a.data_ptr(), 16, P(C), 16, P(alpha), None, 0,
                                    stream()) != 0   # M % 16
+    # time-shifted rows: K a multiple of T, |shift| < T
+    assert lib().mlvae_gemm_fp8_tn_ex(16, 16, 15, 2, a.data_ptr(), 16, 0, a.data_ptr(), 16, 0, P(C), 16, 0,
+                                      P(alpha), 4, -1, 2, None, 0, stream()) != 0
+    assert lib().mlvae_gemm_fp8_tn_ex(16, 16, 16, 1, a.data_ptr(), 16, 0, a.data_ptr(), 16, 0, P(C), 16, 0,
+                                      P(alpha), 1, -1, 0, None, 0, stream()) != 0
 
 
 def test_fp8_mode_training_step_matches_oracle():

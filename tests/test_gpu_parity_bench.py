@@ -79,7 +79,7 @@ def test_c5_fp8_B64_T500_matches_oracle():
 
 def test_c5_fp8_second_step_fp8_dgrad_matches_oracle():
     """configs[4] in its steady state: from the second step on the fp8 mode also runs the layer-1
-    dgrad on e4m3 operands (dG written by the BPTT under delayed scaling from the first step's
+    dgrad, dW_ih and dW_hh and layer 0's dZ, dW_ih | biases and dW_hh on e4m3 operands (dG written by the BPTT under delayed scaling from the first step's
     amax, W_ih^T with the forward's scale, the dropout backward in the epilogue) and the layer
     input arrives as e4m3 from the recurrence itself -- alone, without the bf16 copy no GEMM
     reads any more.  The oracle replays step 2 from the engine's
@@ -92,8 +92,11 @@ def test_c5_fp8_second_step_fp8_dgrad_matches_oracle():
     eng, w, rec, new_ref, params = run_second_step(cfg, B, T, 810, lens)
     assert eng.g8_ready and float(eng.g8[1][0].item()) != 1.0   # a real delayed scale was used
     assert w.ydb_skipped.get(1)   # layer 0 wrote the e4m3 dropout(h) alone (no bf16 reader)
+    assert w.f8hh.get(1)          # dW_hh_l1 on e4m3 dG and h: the BPTT wrote no bf16 dG
+    assert w.f8hh.get(0)          # layer 0 too: dZ, dW_ih_l0 | biases, dW_hh_l0 on its e4m3 dG
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
-    report("c5 fp8 step 2 (fp8 dgrad) B=64 T=500", e, grads)
+    report("c5 fp8 step 2 (fp8 dgrad, dW_ih, dW_hh; layer-0 e4m3 dG) B=64 T=500", e, grads)
+    print("  e4m3-operand gradients:", {k: f"{grads[k]:.2e}" for k in grads if "rnn" in k or "encoder" in k})
     _check(e, grads, 0.12, 3e-2)
 
 
@@ -111,6 +114,7 @@ def test_fp8_three_layers_second_step_matches_oracle():
     eng, w, rec, new_ref, params = run_second_step(cfg, B, T, 811, lens)
     assert eng.g8_ready and all(float(eng.g8[li][0].item()) != 1.0 for li in (1, 2))
     assert w.ydb_skipped.get(1) and w.ydb_skipped.get(2)
+    assert w.f8hh.get(1) and w.f8hh.get(2) and w.f8hh.get(0)
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report("fp8 L=3 step 2 B=48 T=120", e, grads)
     _check(e, grads, 0.12, 3e-2)

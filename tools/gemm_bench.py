@@ -60,6 +60,31 @@ def _time(call, iters, M, Nc, K):
     return ms, 2.0 * M * Nc * K / ms / 1e9
 
 
+def run_fp8(M, Nc, K, iters=10):
+    """mlvae_gemm_fp8 (e4m3 operands A [M][K], B [N][K], fp16 C as the step's projection)"""
+    l = lib()
+    A = torch.randn(M, K, device="cuda").clamp(-448, 448).to(torch.float8_e4m3fn)
+    B = torch.randn(Nc, K, device="cuda").clamp(-448, 448).to(torch.float8_e4m3fn)
+    C = torch.empty(M, Nc, device="cuda", dtype=torch.float16)
+    alpha = torch.ones(1, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+
+    def call():
+        check(l.mlvae_gemm_fp8(M, Nc, K, A.data_ptr(), K, B.data_ptr(), K, C.data_ptr(), Nc, alpha.data_ptr(),
+                               None, None, 16, s))
+    return _time(call, iters, M, Nc, K)
+
+
+def fp8_shapes():
+    """fp8 k-contiguous products (GEMM_FP8=1): the projection and dgrad shapes on e4m3 operands"""
+    for name, ta, tb, M, Nc, K in SHAPES:
+        if ta or K == 32:
+            continue
+        ms = sorted(run_fp8(M, Nc, K)[0] for _ in range(3))
+        print(f"fp8 {name} M={M:6d} N={Nc:5d} K={K:6d} | med {ms[1] * 1e3:7.1f} us min {ms[0] * 1e3:7.1f} us "
+              f"{2.0 * M * Nc * K / ms[0] / 1e9:6.1f} TF", flush=True)
+
+
 def ab(vars_, rounds=3):
     """Same-process A/B of gemm256 main-loop variants (GEMM_VARS=0,10): interleaved rounds, the
     median and min per variant (cdna_hip_programming.md §5.4 rule 24)."""
@@ -81,6 +106,8 @@ def ab(vars_, rounds=3):
 
 
 def main():
+    if os.environ.get("GEMM_FP8"):
+        return fp8_shapes()
     if os.environ.get("GEMM_VARS"):
         return ab([int(v) for v in os.environ["GEMM_VARS"].split(",")])
     only = os.environ.get("GEMM_ONLY")        # substring of a shape name: run just that one
