@@ -441,7 +441,7 @@ def extra_runs(args, device):
         dyb = 2 if getattr(eng, "dy_bf16", False) else 4
         lv = loss.tolist()
         out[key] = {"global_batch": B, "seq_len": T,
-                    "dtype": "fp8-e4m3 layer-1 projection/dgrad/weight gradient, bf16 elsewhere" if cname in FP8 else prec,
+                    "dtype": "fp8-e4m3 layer-1 projection/dgrad/dW_ih/dW_hh, layer-0 dW_hh, both layers' dG (layer-0 dZ / dW_ih read it), bf16 elsewhere" if cname in FP8 else prec,
                     "steps": steps,
                     "ms_per_step": dt / steps * 1e3, "frames_per_s": B * T * steps / dt,
                     "loss": lv[2]}

@@ -186,6 +186,17 @@ int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, const float* w_
                      float* cells, float* y, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
                      unsigned long long drop_seed, unsigned long long drop_offset, float drop_p, void* xbuf,
                      size_t xbytes, int* err, void* stream);
+/* mlvae_lstm_fwd_z with y_bf16_prev = 1: y_bf16 row t receives the h ENTERING step t (h_{t-1} in
+ * the forward direction, h_{t+1} in the reverse one, zeros at each utterance's first step) instead
+ * of h_t -- the time-shifted operand of dW_hh_l0 = sum_t dG_t^T h_{t-/+1} pre-shifted, so that the
+ * weight gradient runs as a plain (unshifted) product.  For a y_bf16 no other product reads (the
+ * next layer's input is the dropout copy). */
+int mlvae_lstm_fwd_z2(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, const void* z_bf16,
+                      int ldz, int Z, const float* w_ih_fwd, const float* w_ih_rev, const float* b_ih_fwd,
+                      const float* b_hh_fwd, const float* b_ih_rev, const float* b_hh_rev, void* gates,
+                      float* cells, float* y, void* y_bf16, int y_bf16_prev, void* y_drop_bf16, void* y_drop_fp8,
+                      float x8_scale, unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                      void* xbuf, size_t xbytes, int* err, void* stream);
 int mlvae_lstm_bwd_fp8(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev, void* gates,
                        const float* cells, const float* dy, void* dg_bf16, float* dbias_rows,
                        void* dg_fp8, const float* dg8_scale, unsigned* dg_amax, void* xbuf,

@@ -1216,13 +1216,15 @@ extern "C" int mlvae_lstm_fwd_fp8(int B, int T, int H, const float* w_hh_fwd, co
 // written -- each step's gate inputs come from the 32-wide bf16 layer input z [B*T rows, ldz]
 // inside the recurrence (one MFMA per tile); gates receives the activated gates as from
 // mlvae_lstm_fwd_ex2.  y (fp32 h), y_drop_bf16 and y_drop_fp8 (with x8_scale) are optional.
-extern "C" int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
-                                const void* z_bf16, int ldz, int Z, const float* w_ih_fwd,
-                                const float* w_ih_rev, const float* b_ih_fwd, const float* b_hh_fwd,
-                                const float* b_ih_rev, const float* b_hh_rev, void* gates, float* cells,
-                                float* y, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
-                                unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
-                                void* xbuf, size_t xbytes, int* err, void* stream) {
+// y_bf16_prev = 1: y_bf16 row t receives the h entering step t (h_{t-1} forward, h_{t+1} reverse,
+// zeros at each utterance's first step) -- dW_hh_l0's time-shifted operand pre-shifted.
+extern "C" int mlvae_lstm_fwd_z2(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                 const void* z_bf16, int ldz, int Z, const float* w_ih_fwd,
+                                 const float* w_ih_rev, const float* b_ih_fwd, const float* b_hh_fwd,
+                                 const float* b_ih_rev, const float* b_hh_rev, void* gates, float* cells,
+                                 float* y, void* y_bf16, int y_bf16_prev, void* y_drop_bf16, void* y_drop_fp8,
+                                 float x8_scale, unsigned long long drop_seed, unsigned long long drop_offset,
+                                 float drop_p, void* xbuf, size_t xbytes, int* err, void* stream) {
   if (Z != 32 || !z_bf16 || !use_wide(B, H, PREC_BF16) || (y_drop_fp8 && !(x8_scale > 0.f))) {
     mlvae_set_error("lstm_fwd_z: Z = 32 on wide-batch shapes; an e4m3 dropout output needs a scale");
     return 1;
@@ -1236,8 +1238,20 @@ extern "C" int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, cons
   ex.wz.ldz = ldz;
   ex.wz.w0 = w_ih_fwd; ex.wz.w1 = w_ih_rev;
   ex.wz.b[0] = b_ih_fwd; ex.wz.b[1] = b_hh_fwd; ex.wz.b[2] = b_ih_rev; ex.wz.b[3] = b_hh_rev;
+  ex.wz.yb_prev = y_bf16 && y_bf16_prev ? 1 : 0;
   return run(true, PREC_BF16, B, T, H, w_hh_fwd, w_hh_rev, static_cast<float*>(gates), cells, y, xbuf, xbytes,
              err, (hipStream_t)stream, static_cast<unsigned short*>(y_bf16), nullptr, 1, ex);
+}
+extern "C" int mlvae_lstm_fwd_z(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
+                                const void* z_bf16, int ldz, int Z, const float* w_ih_fwd,
+                                const float* w_ih_rev, const float* b_ih_fwd, const float* b_hh_fwd,
+                                const float* b_ih_rev, const float* b_hh_rev, void* gates, float* cells,
+                                float* y, void* y_bf16, void* y_drop_bf16, void* y_drop_fp8, float x8_scale,
+                                unsigned long long drop_seed, unsigned long long drop_offset, float drop_p,
+                                void* xbuf, size_t xbytes, int* err, void* stream) {
+  return mlvae_lstm_fwd_z2(B, T, H, w_hh_fwd, w_hh_rev, z_bf16, ldz, Z, w_ih_fwd, w_ih_rev, b_ih_fwd, b_hh_fwd,
+                           b_ih_rev, b_hh_rev, gates, cells, y, y_bf16, 0, y_drop_bf16, y_drop_fp8, x8_scale,
+                           drop_seed, drop_offset, drop_p, xbuf, xbytes, err, stream);
 }
 extern "C" int mlvae_lstm_bwd_fp8_ex(int B, int T, int H, const float* w_hh_fwd, const float* w_hh_rev,
                                      void* gates, const float* cells, const void* dy, int dy_bf16,

@@ -68,6 +68,10 @@ struct LstmArgs {
   const float* Wz0;           // W_ih forward / reverse [4H, 32]
   const float* Wz1;
   const float* bz[4];         // b_ih, b_hh forward; b_ih, b_hh reverse [4H]
+  // wide forward, optional: Yb row t receives the h ENTERING step t (h_{t-1} forward, h_{t+1}
+  // reverse; zeros at each utterance's first step) -- dW_hh's time-shifted operand pre-shifted,
+  // when no other reader takes Yb (the layer below a dropout)
+  int yb_prev;
 };
 
 // XCC (XCD) id of the executing workgroup: s_getreg_b32 HW_REG_XCC_ID (id 20, bits [3:0])
@@ -228,6 +232,7 @@ struct WideZ {  // the wide forward's fused layer-0 input projection (LstmArgs Z
   const float* w0 = nullptr;
   const float* w1 = nullptr;
   const float* b[4] = {nullptr, nullptr, nullptr, nullptr};
+  int yb_prev = 0;  // LstmArgs::yb_prev
 };
 int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W1, float* G,
                   float* Cs, float* Y, void* xbuf, size_t xbytes, int* err, hipStream_t st,

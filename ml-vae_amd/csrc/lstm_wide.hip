@@ -279,7 +279,14 @@ __global__ __launch_bounds__(W12 ? 768 : 512, W12 ? 1 : OCC) void lstm_fwd_wide_
         const float* hf = reinterpret_cast<const float*>(src + u * OUB + 8 * HJ) + HJ;
         f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
-        const size_t o = rowof(b, t_) * 2 * H + dir * H + j0 + uu;
+        size_t o = rowof(b, t_) * 2 * H + dir * H + j0 + uu;
+        if (!drop8 && a.yb_prev) {  // h_t enters step s_ + 1: row t + 1 (forward) / t - 1 (reverse)
+          if (s_ == 0)  // nothing enters the first step
+            *reinterpret_cast<bf16x8*>(a.Yb + o) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          const int tn = dir ? t_ - 1 : t_ + 1;
+          if (tn < 0 || tn >= T) return;
+          o = rowof(b, tn) * 2 * H + dir * H + j0 + uu;
+        }
         if (drop8) {  // keep bits drawn by the pollers at the end of step s_
           const unsigned bits = dbl[(s_ & 1) * NC8 + ci8];
 #pragma unroll
@@ -1337,7 +1344,7 @@ int lstm_wide_run(bool fwd, int B, int T, int H, const float* W0, const float* W
                       "both W_ih and all four biases, a 16-byte aligned z with ldz >= 32, ldz %% 8 == 0");
       return 1;
     }
-    a.Zb = wz.zb; a.ldz = wz.ldz; a.Wz0 = wz.w0; a.Wz1 = wz.w1;
+    a.Zb = wz.zb; a.ldz = wz.ldz; a.Wz0 = wz.w0; a.Wz1 = wz.w1; a.yb_prev = wz.yb_prev;
     for (int i = 0; i < 4; ++i) a.bz[i] = wz.b[i];
   }
   if (a.Y8 && (!fwd || !(a.x8scale > 0.f) || !(dp >= 0.f && dp < 1.f))) {

@@ -121,6 +121,7 @@ _SIGS = {
     "mlvae_lstm_set_debug_mode": [I],
     "mlvae_lstm_fwd_fp8": [I, I, I, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_fwd_z": [I, I, I, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, F, U64, U64, F, P, SZ, P, P],
+    "mlvae_lstm_fwd_z2": [I, I, I, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, F, U64, U64, F, P, SZ, P, P],
     "mlvae_lstm_bwd_fp8": [I, I, I, P, P, P, P, P, P, P, P, P, P, P, SZ, P, P],
     "mlvae_lstm_bwd_fp8_ex": [I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, SZ, P, P],
     "mlvae_fp8_delayed_scale": [P, P, P, F, P, P],

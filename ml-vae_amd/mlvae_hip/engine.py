@@ -534,7 +534,7 @@ class VAEEngine:
             return None
         return _pb(self.flat_bf, self.layout.offsets[name])
 
-    def _fp8_whh(self, w, li, N, T, gp):
+    def _fp8_whh(self, w, li, N, T, gp, shifted=False):
         """fp8 mode: both directions' dW_hh_l{li} = sum_t dG_t^T h_{t-1} / h_{t+1} on e4m3 operands in
         one batched launch (mlvae_gemm_fp8_tn_ex, time-shifted rows): the layer's e4m3 dG from its
         BPTT and h cast to e4m3 with the layer-input scale (|h| < 1), so alpha = 1 / (q_dG x-scale)"""
@@ -545,7 +545,8 @@ class VAEEngine:
         check(l.mlvae_cast_fp8(N * 2 * H, _pb(w.Yb[li]), 1, None, x8_scale(self.cfg.dropout), w.H8[li].data_ptr(),
                                st), "cast_fp8")
         check(l.mlvae_gemm_fp8_tn_ex(4 * H, H, N, 2, w.dG8[li].data_ptr(), 8 * H, 4 * H, w.H8[li].data_ptr(), 2 * H, H,
-                                     gp(f"decoder.rnn.weight_hh_l{li}"), H, 4 * H * H, _p(self.g8w[li], 1), T, -1, 2,
+                                     gp(f"decoder.rnn.weight_hh_l{li}"), H, 4 * H * H, _p(self.g8w[li], 1),
+                                     0 if shifted else T, 0 if shifted else -1, 0 if shifted else 2,
                                      _p(ws), w.gws_bytes, st), "gemm_fp8_tn_ex")
 
     def _dzw_path(self, N):
@@ -842,19 +843,24 @@ class VAEEngine:
                             and l.mlvae_gemm_fp8_tn_workspace_size(8 * H, 2 * H, N) <= w.gws_bytes)
             w.__dict__.setdefault("ydb_skipped", {})[li + 1] = skip_ydb
             ydb_arg = None if skip_ydb else (_pb(w.Ydb[li]) if fuse_drop else None)
+            # the bf16 h of a layer below a fused dropout has one reader, its own dW_hh: the
+            # recurrence writes it pre-shifted (row t = the h entering step t) and the weight
+            # gradient runs unshifted (the m/n-contiguous eight-phase GEMM loop)
+            yb_prev = bool(zproj and fuse_drop and getattr(self, "yb_prev", True))
+            w.__dict__.setdefault("yb_prev", {})[li] = yb_prev
             with self._timed("lstm_fwd"):
                 if zproj:
                     rp = lambda n: self._ptr(f"decoder.rnn.{n}")
-                    check(l.mlvae_lstm_fwd_z(B, T, H, rp("weight_hh_l0"), rp("weight_hh_l0_reverse"), _pb(xin_bf),
-                                             ldx, din, rp("weight_ih_l0"), rp("weight_ih_l0_reverse"),
-                                             rp("bias_ih_l0"), rp("bias_hh_l0"), rp("bias_ih_l0_reverse"),
-                                             rp("bias_hh_l0_reverse"), _p(w.G[li]), _p(w.Cs[li]),
-                                             _p(w.Y[li]) if need_y else None, _pb(w.Yb[li]),
-                                             ydb_arg,
+                    check(l.mlvae_lstm_fwd_z2(B, T, H, rp("weight_hh_l0"), rp("weight_hh_l0_reverse"), _pb(xin_bf),
+                                              ldx, din, rp("weight_ih_l0"), rp("weight_ih_l0_reverse"),
+                                              rp("bias_ih_l0"), rp("bias_hh_l0"), rp("bias_ih_l0_reverse"),
+                                              rp("bias_hh_l0_reverse"), _p(w.G[li]), _p(w.Cs[li]),
+                                              _p(w.Y[li]) if need_y else None, _pb(w.Yb[li]), int(yb_prev),
+                                              ydb_arg,
                                              x8_ptr,
-                                             x8_scale(cfg.dropout) if x8_fused else 0.0, seed, self._drop_off,
-                                             cfg.dropout if fuse_drop else 0.0, _p(w.xbuf), w.xbuf.numel(),
-                                             _p(self.err), s), "lstm_fwd_z")
+                                              x8_scale(cfg.dropout) if x8_fused else 0.0, seed, self._drop_off,
+                                              cfg.dropout if fuse_drop else 0.0, _p(w.xbuf), w.xbuf.numel(),
+                                              _p(self.err), s), "lstm_fwd_z2")
                 elif x8_fused:
                     check(l.mlvae_lstm_fwd_fp8(B, T, H, self._ptr(f"decoder.rnn.weight_hh_l{li}"),
                                                self._ptr(f"decoder.rnn.weight_hh_l{li}_reverse"), _p(w.G[li]),
@@ -1169,13 +1175,15 @@ class VAEEngine:
                 if li == 0 and w.enc_fused:
                     # both directions' dW_hh_l0 in one batched 256² launch; dW_ih_l0 and the
                     # biases follow the encoder backward on the main stream (skinny_tn below)
+                    pre = bool(w.__dict__.get("yb_prev", {}).get(0))  # Yb rows already shifted
                     with self._timed("wgrad_hh_l0"):
                         if f8hh:
-                            self._fp8_whh(w, 0, N, T, gp)
+                            self._fp8_whh(w, 0, N, T, gp, shifted=pre)
                         else:
                             self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
                                        gp("decoder.rnn.weight_hh_l0"), H, batch=2, a_bs=4 * H, b_bs=H,
-                                       c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                                       c_bs=4 * H * H, kshift_T=0 if pre else T, kshift=0 if pre else -1,
+                                       kstep=0 if pre else 2)
                     return
                 if dG_bf is not None and xin_bf is not None and din % 8 == 0 and H % 8 == 0:
                     # 256² GEMMs: dW_ih = dG^T X, and both directions' dW_hh = sum_t dG_t^T h_{t-/+1}

@@ -168,6 +168,18 @@ def test_fused_z_projection_forward(B, T, ldz, mode):
                                      0.0, 0, 0, 0.0, P(xbuf), xb.value, P(err), stream()))
         torch.cuda.synchronize()
         assert err.item() == 0 and torch.equal(Yb1, Yb) and torch.equal(G1, G)
+        # mlvae_lstm_fwd_z2 with y_bf16_prev (the train step's layer-0 form under a fused dropout):
+        # bf16 row t holds the h entering step t -- h_{t-1} forward, h_{t+1} reverse, zeros at each
+        # utterance's first step -- bit for bit; the gates and the dropout copy unchanged
+        G2, Yb2, Ydb2 = torch.empty_like(G), torch.full_like(Yb, float("nan")), torch.empty_like(Ydb)
+        check(lib().mlvae_lstm_fwd_z2(B, T, H, P(W0), P(W1), zb.data_ptr(), ldz, Z, P(wi[0]), P(wi[1]), P(bs[0]),
+                                      P(bs[1]), P(bs[2]), P(bs[3]), P(G2), P(Cs), None, Yb2.data_ptr(), 1,
+                                      Ydb2.data_ptr(), None, 0.0, seed, doff, p, P(xbuf), xb.value, P(err), stream()))
+        torch.cuda.synchronize()
+        assert err.item() == 0 and torch.equal(G2, G) and torch.equal(Ydb2, Ydb)
+        y3, p3 = Yb.view(B, T, 2 * H), Yb2.view(B, T, 2 * H)
+        assert torch.equal(p3[:, 1:, :H], y3[:, :-1, :H]) and torch.equal(p3[:, :-1, H:], y3[:, 1:, H:])
+        assert (p3[:, 0, :H] == 0).all() and (p3[:, -1, H:] == 0).all()
     finally:
         lib().mlvae_lstm_set_debug_mode(0)
     # argument checks: Z != 32, a misaligned ldz

@@ -23,32 +23,53 @@ import json
 import os
 import sys
 
-# kernel-name fragment -> role of its k-th dispatch within a step (engine.py launch order)
-ROLES_BF16 = [
+# kernel-name fragment -> role of its k-th dispatch within a step (engine.py launch order; the
+# round-6 main loops: VAR 16 k-contiguous, VAR 18 m/n-contiguous unshifted, VAR 0 time-shifted dW_hh,
+# fp8 VAR 8 k-contiguous and VAR 9 m/n-contiguous)
+_COMMON = [
     ("lstm_fwd_wide_kernel", ["lstm_fwd_l0", "lstm_fwd_l1"]),
     ("lstm_bwd_wide_kernel", ["lstm_bwd_l1", "lstm_bwd_l0"]),
-    ("gemm256_kernel<true, true, 12>", ["proj_l1", "dgrad_l1"]),
-    ("heads_nt_kernel<true", ["heads_p1"]),    # from 64K frames the heads' products run on the
-    ("heads_nt_kernel<false", ["heads_dy"]),   # 128-row kernel (heads.hip heads_nt)
-    ("gemm256_kernel<false, false, 0>", ["heads_dw1", "wgrad_ih_l1", "wgrad_hh_l1", "wgrad_hh_l0"]),
     ("heads_mid_kernel", ["heads_mid"]),
     ("encoder_fwd_kernel", ["encoder_fwd"]),
     ("encoder_bwd_kernel", ["encoder_bwd"]),
+]
+ROLES_BF16 = _COMMON + [   # c3: from 64K frames the heads' products run on the 128-row heads_nt kernel
+    ("gemm256_kernel<true, true, 16>", ["proj_l1", "dgrad_l1"]),
+    ("heads_nt_kernel<true", ["heads_p1"]),
+    ("heads_nt_kernel<false", ["heads_dy"]),
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1"]),
+    ("gemm256_kernel<false, false, 0>", ["wgrad_hh_l1", "wgrad_hh_l0"]),
     ("skinny_dzw_kernel", ["skinny_dzw"]),
+]
+ROLES_C4 = _COMMON + [     # Conv1d encoder: layer 0 has its own 256-wide input projection / dW_ih
+    ("gemm256_kernel<true, true, 16>", ["proj_l1", "dgrad_l1"]),
+    ("heads_nt_kernel<true", ["heads_p1"]),
+    ("heads_nt_kernel<false", ["heads_dy"]),
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1", "wgrad_ih_l0"]),
+    ("gemm256_kernel<false, false, 0>", ["wgrad_hh_l1", "wgrad_hh_l0"]),
     ("conv_kernel<4, false>", ["conv_fwd_l1", "conv_fwd_l2"]),
     ("conv_kernel<4, true>", ["conv_dgrad"]),
     ("conv_wgrad_kernel", ["conv_wgrad_l2", "conv_wgrad_l1"]),
 ]
-ROLES_FP8 = [r for r in ROLES_BF16 if not r[0].startswith(("gemm256", "heads_nt"))] + [
-    ("gemm256_kernel<true, true, 12>", ["heads_p1", "heads_dy"]),
-    ("gemm256_kernel<true, true, 8>", ["proj_l1", "dgrad_l1"]),       # e4m3 operands
-    ("gemm256_kernel<false, false, 9>", ["wgrad_ih_l1"]),               # e4m3 operands
-    ("gemm256_kernel<false, false, 0>", ["heads_dw1", "wgrad_hh_l1", "wgrad_hh_l0"]),
+# below 64K frames (c2, the c5 shard in bf16, c3h): P1 on heads_nt, dY on the 256² GEMM
+ROLES_SMALL = _COMMON + [
+    ("gemm256_kernel<true, true, 16>", ["proj_l1", "heads_dy", "dgrad_l1"]),
+    ("heads_nt_kernel<true", ["heads_p1"]),
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1"]),
+    ("gemm256_kernel<false, false, 0>", ["wgrad_hh_l1", "wgrad_hh_l0"]),
+    ("skinny_nt_lds_kernel<2, false>", ["skinny_dz"]),
+    ("skinny_tn_kernel<3, false>", ["skinny_dwih_l0"]),
 ]
-# below 64K frames (c2, the c5 shard, c3h) the heads' products stay on the 256² GEMM
-ROLES_SMALL = [r for r in ROLES_BF16 if not r[0].startswith(("gemm256_kernel<true", "heads_nt"))] + [
-    ("gemm256_kernel<true, true, 12>", ["proj_l1", "heads_p1", "heads_dy", "dgrad_l1"])]
-ROLES = {"c5": ROLES_FP8, "c2": ROLES_SMALL, "c3h": ROLES_SMALL}
+ROLES_FP8 = _COMMON + [    # c5: e4m3 operands from the second step on (the first step's bf16 forms skip)
+    ("gemm256_kernel<true, true, 8>", ["proj_l1", "dgrad_l1"]),
+    ("heads_nt_kernel<true", ["heads_p1"]),
+    ("gemm256_kernel<true, true, 16>", ["heads_dy"]),
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1"]),
+    ("gemm256_kernel<false, false, 9>", ["wgrad_ih_l1", "wgrad_hh_l1", "wgrad_hh_l0"]),
+    ("skinny_nt_lds_kernel<2, true>", ["skinny_dz"]),
+    ("skinny_tn_kernel<3, true>", ["skinny_dwih_l0"]),
+]
+ROLES = {"c5": ROLES_FP8, "c2": ROLES_SMALL, "c3h": ROLES_SMALL, "c5bf16": ROLES_SMALL, "c4": ROLES_C4}
 
 
 def dispatches(path):
