@@ -280,7 +280,9 @@ __global__ __launch_bounds__(W12 ? 768 : 512, W12 ? 1 : OCC) void lstm_fwd_wide_
         f32x4 v0 = *reinterpret_cast<const f32x4*>(hf + uu);
         f32x4 v1 = *reinterpret_cast<const f32x4*>(hf + uu + 4);
         size_t o = rowof(b, t_) * 2 * H + dir * H + j0 + uu;
-        if (!drop8 && a.yb_prev) {  // h_t enters step s_ + 1: row t + 1 (forward) / t - 1 (reverse)
+        // (the fused-z layer-0 instances only: mlvae_lstm_fwd_z2 -- in the others the branch cost
+        // the TPW-2 forward 8 spilled SGPRs and ~5 % per launch)
+        if (ZP && !drop8 && a.yb_prev) {  // h_t enters step s_ + 1: row t + 1 (forward) / t - 1 (reverse)
           if (s_ == 0)  // nothing enters the first step
             *reinterpret_cast<bf16x8*>(a.Yb + o) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
           const int tn = dir ? t_ - 1 : t_ + 1;
