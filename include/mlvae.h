@@ -58,7 +58,7 @@ int mlvae_gemm_ex_drop(int trans_a, int trans_b, int M, int N, int K, float alph
                        float* ws, size_t ws_bytes, void* stream);
 /* Large bf16 GEMMs (256 x 256 tiles, LDS-DMA staging, bf16 operands only, fp32 C):
  *   C_b = epi( op(A_b) op(B_b) + bias1 + bias2 + beta C_b ),  b = 0 .. batch-1
- * A_b = A + b*a_bstride (elements), likewise B_b, C_b.  trans_a = 0: A [M,K] k-contiguous;
+ * A_b = A + b*a_bstride (elements; strides may be negative), likewise B_b, C_b.  trans_a = 0: A [M,K] k-contiguous;
  * trans_a = 1: A stored [K,M].  trans_b = 1: B stored [N,K]; trans_b = 0: B stored [K,N].
  * kshift (+ b*kshift_bstep) time-shifts the rows of a [K,N] B operand as mlvae_gemm does.
  * epi as mlvae_gemm_ex_drop (3 = dropout mask of (drop_seed, row*ldc + col)); epi | 16

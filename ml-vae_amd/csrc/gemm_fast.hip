@@ -1188,10 +1188,10 @@ extern "C" int mlvae_gemm_bf16(int trans_a, int trans_b, int M, int N, int K, in
     mlvae_set_error("mlvae_gemm_bf16: operands need 16-byte chunks (ld, contiguous extent %% 8)");
     return 1;
   }
-  // every in-range byte offset must stay below the descriptor's 2^31 range
+  // every in-range byte offset must stay below the descriptor's 2^31 range (each batch entry has
+  // its own descriptor at A + z a_bstride, so the strides -- negative ones too -- do not count)
   const size_t a_rows = akc ? (size_t)M : (size_t)K, b_rows = bkc ? (size_t)N : (size_t)K;
-  if ((a_rows * lda + (size_t)(batch - 1) * a_bstride) * 2 >= OOB ||
-      (b_rows * ldb + (size_t)(batch - 1) * b_bstride) * 2 >= OOB) {
+  if (a_rows * lda * 2 >= OOB || b_rows * ldb * 2 >= OOB) {
     mlvae_set_error("mlvae_gemm_bf16: operand larger than 2 GB");
     return 1;
   }

@@ -436,6 +436,10 @@ class VAEEngine:
         self.skinny_proj = True
         # layer 0's dZ and dW_ih_l0 from one pass over dG (False: the NT + TN pair)
         self.dzw = True
+        # dW_hh as unshifted products minus the utterance-boundary terms (_whh_bf16; False: the
+        # time-shifted batched product), and layer 0's bf16 h written pre-shifted (False: as h_t)
+        self.whh_unshift = True
+        self.yb_prev = True
         # the wide recurrence writes dropout(h) itself (False: a separate dropout pass)
         self._fuse_drop = True
         self.side_stream = torch.cuda.Stream(self.device)
@@ -549,6 +553,32 @@ class VAEEngine:
                                      0 if shifted else T, 0 if shifted else -1, 0 if shifted else 2,
                                      _p(ws), w.gws_bytes, st), "gemm_fp8_tn_ex")
 
+    def _whh_bf16(self, w, li, N, T, dG_bf, Yb, gp):
+        """Both directions' dW_hh_l{li} = sum_t dG_t^T h_{t-1} (forward) / h_{t+1} (reverse) as
+        UNSHIFTED products (the m/n-contiguous eight-phase loop; with time-shifted rows it spills and
+        runs on the older loop): over all N frames the operands offset by one row pair dG row k with
+        h row k -/+ 1, which at each utterance's first (forward) / last (reverse) step is the
+        neighbouring utterance's h -- those B - 1 terms are summed first by a small strided product
+        (rows T apart) and subtracted by the main product's beta = -1."""
+        H = self.cfg.H
+        if not getattr(self, "whh_unshift", True):  # (A/B: the time-shifted batched product)
+            self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Yb), 2 * H, gp(f"decoder.rnn.weight_hh_l{li}"),
+                       H, batch=2, a_bs=4 * H, b_bs=H, c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+            return
+        nb = N // T
+        ld, lh = 8 * H, 2 * H
+        C = gp(f"decoder.rnn.weight_hh_l{li}")  # the reverse direction's gradient follows it
+        # both directions in one batched launch each (batch strides: the reverse entry's offsets
+        # minus the forward one's): forward dG from row 1 with h from row 0, reverse dG from row 0
+        # with h from row 1; the boundary terms at rows T apart: forward (dG row bT, h row bT - 1),
+        # reverse (dG row bT + T - 1, h row (b + 1) T)
+        if nb > 1:
+            ca0, cb0 = T * ld, (T - 1) * lh
+            self._fast(w, 1, 0, 4 * H, H, nb - 1, _pb(dG_bf, ca0), T * ld, _pb(Yb, cb0), T * lh, C, H, batch=2,
+                       a_bs=(T - 1) * ld + 4 * H - ca0, b_bs=T * lh + H - cb0, c_bs=4 * H * H)
+        self._fast(w, 1, 0, 4 * H, H, N - 1, _pb(dG_bf, ld), ld, _pb(Yb), lh, C, H, batch=2,
+                   a_bs=4 * H - ld, b_bs=lh + H, c_bs=4 * H * H, beta=-1.0 if nb > 1 else 0.0)
+
     def _dzw_path(self, N):
         """dZ and dW_ih_l0 from the one-pass skinny_dzw kernel (bf16 dG only)"""
         cfg = self.cfg
@@ -613,7 +643,7 @@ class VAEEngine:
 
     def _fast(self, w, ta, tb, M, N, K, A_bf, lda, B_bf, ldb, C, ldc, batch=1, a_bs=0, b_bs=0,
               c_bs=0, bias1=None, bias2=None, kshift_T=0, kshift=0, kstep=0, drop_seed=None,
-              out_f16=False, out_bf16=False):
+              out_f16=False, out_bf16=False, beta=0.0):
         """bf16 256² LDS-DMA GEMM (mlvae_gemm_bf16) over bf16 operands: the step's big products.
         out_f16: C is fp16 (the wide recurrence's gate buffer); out_bf16: C is bf16 (dY)."""
         ws = w.gws_side if self._on_side else w.gws
@@ -623,7 +653,7 @@ class VAEEngine:
         if out_bf16:
             epi |= EPI_OUT_BF16
         check(lib().mlvae_gemm_bf16(ta, tb, M, N, K, batch, A_bf, lda, a_bs, B_bf, ldb, b_bs, C, ldc,
-                                    c_bs, 0.0, bias1, bias2, epi, None, 0, kshift_T, kshift, kstep,
+                                    c_bs, beta, bias1, bias2, epi, None, 0, kshift_T, kshift, kstep,
                                     drop_seed or 0, self._drop_off, p, _p(ws), w.gws_bytes,
                                     self._stream()),
               "mlvae_gemm_bf16")
@@ -1179,11 +1209,12 @@ class VAEEngine:
                     with self._timed("wgrad_hh_l0"):
                         if f8hh:
                             self._fp8_whh(w, 0, N, T, gp, shifted=pre)
-                        else:
+                        elif pre:
                             self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
                                        gp("decoder.rnn.weight_hh_l0"), H, batch=2, a_bs=4 * H, b_bs=H,
-                                       c_bs=4 * H * H, kshift_T=0 if pre else T, kshift=0 if pre else -1,
-                                       kstep=0 if pre else 2)
+                                       c_bs=4 * H * H)
+                        else:
+                            self._whh_bf16(w, 0, N, T, dG_bf, Ybl, gp)
                     return
                 if dG_bf is not None and xin_bf is not None and din % 8 == 0 and H % 8 == 0:
                     # 256² GEMMs: dW_ih = dG^T X, and both directions' dW_hh = sum_t dG_t^T h_{t-/+1}
@@ -1203,9 +1234,7 @@ class VAEEngine:
                         if f8hh:
                             self._fp8_whh(w, li, N, T, gp)
                         else:
-                            self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
-                                       gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
-                                       c_bs=4 * H * H, kshift_T=T, kshift=-1, kstep=2)
+                            self._whh_bf16(w, li, N, T, dG_bf, Ybl, gp)
                 else:
                     self._mm(w, 1, 0, 8 * H, din, N, pg(dG), 8 * H, pg(xin), din,
                              gp(f"decoder.rnn.weight_ih_l{li}"), din, A_bf=pgb(dG_bf), B_bf=pgb(xin_bf))
