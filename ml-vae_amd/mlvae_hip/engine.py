@@ -1231,8 +1231,14 @@ class VAEEngine:
                             self._fast(w, 1, 0, 8 * H, din, N, _pb(dG_bf), 8 * H, _pb(xin_bf), ldx,
                                        gp(f"decoder.rnn.weight_ih_l{li}"), din)
                     with self._timed(f"wgrad_hh_l{li}"):
+                        # (layer 0 of the Conv1d-encoder configs also writes its h pre-shifted)
+                        pre = bool(w.__dict__.get("yb_prev", {}).get(li))
                         if f8hh:
-                            self._fp8_whh(w, li, N, T, gp)
+                            self._fp8_whh(w, li, N, T, gp, shifted=pre)
+                        elif pre:
+                            self._fast(w, 1, 0, 4 * H, H, N, _pb(dG_bf), 8 * H, _pb(Ybl), 2 * H,
+                                       gp(f"decoder.rnn.weight_hh_l{li}"), H, batch=2, a_bs=4 * H, b_bs=H,
+                                       c_bs=4 * H * H)
                         else:
                             self._whh_bf16(w, li, N, T, dG_bf, Ybl, gp)
                 else:

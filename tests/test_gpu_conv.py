@@ -177,5 +177,7 @@ def test_c4_conv_encoder_training_step_matches_oracle():
     assert e_mu <= 1e-2 and e_lv <= 1e-2 and e_mux <= 1e-2
     print(" ".join(f"{k} {v:.2e}" for k, v in grads.items() if k.startswith("encoder.")))
     for k, v in grads.items():
-        assert v <= 4e-2, (k, v)
+        assert v <= 3e-2, (k, v)
+        if k.startswith("decoder.rnn."):  # (a one-step time shift of h in dW_hh_l0 gave 4.6e-2)
+            assert v <= 1.5e-2, (k, v)
     assert par <= 2.5e-3

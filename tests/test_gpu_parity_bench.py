@@ -22,7 +22,7 @@ SIGN_MIN = 0.995
 UPDATE_ERR = 0.15
 
 
-def _check(e, grads, grad_max, grad_med, out_max=1e-2):
+def _check(e, grads, grad_max, grad_med, out_max=1e-2, update_max=UPDATE_ERR, rnn_max=None):
     assert e["loss"] <= 1e-3 and e["recon_loss"] <= 1e-3, e
     assert e["kld_loss"] <= 1e-2, e
     for k in ("mu", "log_var", "mu_x", "log_var_x"):
@@ -31,7 +31,11 @@ def _check(e, grads, grad_max, grad_med, out_max=1e-2):
         assert v <= grad_max, (k, v)
     assert float(np.median(list(grads.values()))) <= grad_med
     assert e["update_sign"] >= SIGN_MIN, e["update_sign"]
-    assert e["update_err"] <= UPDATE_ERR, e["update_err"]
+    assert e["update_err"] <= update_max, e["update_err"]
+    if rnn_max is not None:  # the recurrent weights' gradients (a one-step time shift of h in dW_hh
+        for k, v in grads.items():  # once passed the looser bounds at 3.9e-2: tools/gpu_c4chk.sh)
+            if k.startswith("decoder.rnn."):
+                assert v <= rnn_max, (k, v)
 
 
 def test_c3_headline_B256_T500_matches_oracle():
@@ -47,7 +51,7 @@ def test_c3_headline_B256_T500_matches_oracle():
     eng, w, rec, new_ref, params = run_step(cfg, B, T, 2718, lens)
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report(f"c3 B=256 T=500 wide {wgs} WGs", e, grads)
-    _check(e, grads, 4e-2, 1.5e-2)
+    _check(e, grads, 4e-2, 1.5e-2, update_max=1.5e-2, rnn_max=1.5e-2)
 
 
 def test_c4_conv_B64_T2000_matches_oracle():
@@ -60,7 +64,7 @@ def test_c4_conv_B64_T2000_matches_oracle():
     eng, w, rec, new_ref, params = run_step(cfg, B, T, 4243, lens)
     e, grads = errors(eng, w, rec, new_ref, params, B, T)
     report("c4 conv K=5 B=64 T=2000", e, grads)
-    _check(e, grads, 4e-2, 1.5e-2)
+    _check(e, grads, 4e-2, 1.5e-2, update_max=1.5e-2, rnn_max=1.5e-2)
 
 
 def test_c5_fp8_B64_T500_matches_oracle():
