@@ -1,4 +1,4 @@
-# same-box A/B of the current library against the round-6 start build (abl/libmlvae_r6start.so)
+# same-box A/B of the current library against the round-6 start build (abl/libmlvae_r6start.so: built from 6b841cc into abl/ first; not kept in the tree)
 # at c3 and the fp8 / bf16 c5 shard
 set -o pipefail
 cd $GRAFT_REPO_ROOT
