@@ -1066,7 +1066,12 @@ class VAEEngine:
         full = self._full_chip(B)
         self.overlap = not full
         dzw_done = False   # dW_ih_l0 already produced by the layer-0 skinny_dzw pass
-        split_overlap, split_tail = (256, 256) if full else (self.split_overlap, self.split_tail)
+        # the side-stream weight gradients' workgroup target scales with their work against the
+        # BPTT they overlap (fixed length): proportional to the batch, halved on e4m3 operands
+        # (twice the MFMA rate). split_overlap is the target at B = 64 in bf16; same process
+        # (profiles/ab/r06_split_overlap.txt): B = 32 bf16 and B = 64 fp8 run best at 64, B = 64 bf16 at 128
+        so = int(round(self.split_overlap * B / 64 * (0.5 if (cfg.fp8 and self.g8_ready) else 1.0)))
+        split_overlap, split_tail = (256, 256) if full else (min(256, max(32, so)), self.split_tail)
         E, Z, H, C, Fd = cfg.E, cfg.Z, cfg.H, cfg.C, cfg.F
         l, s = lib(), self._stream()
         g = self.grad
