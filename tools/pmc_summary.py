@@ -25,7 +25,7 @@ import sys
 
 # kernel-name fragment -> role of its k-th dispatch within a step (engine.py launch order; the
 # round-6 main loops: VAR 16 k-contiguous, VAR 18 m/n-contiguous unshifted, VAR 0 time-shifted dW_hh,
-# fp8 VAR 8 k-contiguous and VAR 9 m/n-contiguous)
+# fp8 VAR 8 k-contiguous and VAR 9 m/n-contiguous; the time-shifted VAR 0 no longer runs)
 _COMMON = [
     ("lstm_fwd_wide_kernel", ["lstm_fwd_l0", "lstm_fwd_l1"]),
     ("lstm_bwd_wide_kernel", ["lstm_bwd_l1", "lstm_bwd_l0"]),
@@ -37,16 +37,18 @@ ROLES_BF16 = _COMMON + [   # c3: from 64K frames the heads' products run on the 
     ("gemm256_kernel<true, true, 16>", ["proj_l1", "dgrad_l1"]),
     ("heads_nt_kernel<true", ["heads_p1"]),
     ("heads_nt_kernel<false", ["heads_dy"]),
-    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1"]),
-    ("gemm256_kernel<false, false, 0>", ["wgrad_hh_l1", "wgrad_hh_l0"]),
+    # dW_hh_l1: the utterance-boundary terms, then the unshifted product; dW_hh_l0 on the
+    # pre-shifted h (engine _whh_bf16 / yb_prev)
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1", "wgrad_hh_l1_bnd", "wgrad_hh_l1",
+                                          "wgrad_hh_l0"]),
     ("skinny_dzw_kernel", ["skinny_dzw"]),
 ]
 ROLES_C4 = _COMMON + [     # Conv1d encoder: layer 0 has its own 256-wide input projection / dW_ih
     ("gemm256_kernel<true, true, 16>", ["proj_l1", "dgrad_l1"]),
     ("heads_nt_kernel<true", ["heads_p1"]),
     ("heads_nt_kernel<false", ["heads_dy"]),
-    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1", "wgrad_ih_l0"]),
-    ("gemm256_kernel<false, false, 0>", ["wgrad_hh_l1", "wgrad_hh_l0"]),
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1", "wgrad_hh_l1_bnd", "wgrad_hh_l1",
+                                          "wgrad_ih_l0", "wgrad_hh_l0"]),
     ("conv_kernel<4, false>", ["conv_fwd_l1", "conv_fwd_l2"]),
     ("conv_kernel<4, true>", ["conv_dgrad"]),
     ("conv_wgrad_kernel", ["conv_wgrad_l2", "conv_wgrad_l1"]),
@@ -55,8 +57,8 @@ ROLES_C4 = _COMMON + [     # Conv1d encoder: layer 0 has its own 256-wide input 
 ROLES_SMALL = _COMMON + [
     ("gemm256_kernel<true, true, 16>", ["proj_l1", "heads_dy", "dgrad_l1"]),
     ("heads_nt_kernel<true", ["heads_p1"]),
-    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1"]),
-    ("gemm256_kernel<false, false, 0>", ["wgrad_hh_l1", "wgrad_hh_l0"]),
+    ("gemm256_kernel<false, false, 18>", ["heads_dw1", "wgrad_ih_l1", "wgrad_hh_l1_bnd", "wgrad_hh_l1",
+                                          "wgrad_hh_l0"]),
     ("skinny_nt_lds_kernel<2, false>", ["skinny_dz"]),
     ("skinny_tn_kernel<3, false>", ["skinny_dwih_l0"]),
 ]
